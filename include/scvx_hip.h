@@ -1,0 +1,134 @@
+/*
+ * libscvx_hip.so -- C-ABI of the MI355X-native batched SCvx inner loop.
+ *
+ * Every pointer argument of a compute entry point is a CALLER-OWNED DEVICE buffer (e.g. a
+ * PyTorch-ROCm tensor's data_ptr()); `stream` is a hipStream_t (NULL = default stream).  The
+ * library never allocates caller-visible memory, never synchronises the stream and never throws:
+ * every function returns SCVX_OK (0) or a negative SCVX_E* code, with a message available from
+ * scvx_last_error().  Per-agent solver outcomes are reported in `status` arrays
+ * (SCVX_STATUS_*), which the Python layer maps to CVXPY status strings.
+ *
+ * Layouts are agent-major (agent = outermost index) so that one agent's data is contiguous:
+ *   X      [N][K][n]        == per agent the reference's X (n,K) in order='F'
+ *   U      [N][K][m]
+ *   disc   [N][K-1][n*(n+2m+2)]   per interval vec_F(A_k) | vec_F(B_k) | vec_F(C_k) | S_k | z_k
+ *          == columns k of the reference's (A_bar, B_bar, C_bar, S_bar, z_bar)
+ *          (SCvx/discretization/first_order_hold.py:20-24, 75-85).
+ */
+#ifndef SCVX_HIP_H
+#define SCVX_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SCVX_HIP_VERSION 1
+
+#define SCVX_OK 0
+#define SCVX_EINVAL (-1)
+#define SCVX_EUNSUPPORTED (-2)
+#define SCVX_ELAUNCH (-3)
+#define SCVX_EWORKSPACE (-4)
+
+/* model ids (csrc/models.hpp) */
+#define SCVX_MODEL_DOUBLE_INTEGRATOR 0 /* n=6,  m=3  Distributed_opt/dist_scvx_3d.py:10-21 */
+#define SCVX_MODEL_UNICYCLE 1          /* n=3,  m=2  SCvx/models/unicycle_model.py:54-63   */
+#define SCVX_MODEL_SINGLE_INTEGRATOR 2 /* n=3,  m=3  SCvx/models/single_integrator_model.py:54-57 */
+#define SCVX_MODEL_QUADROTOR 3         /* n=12, m=4  build-defined           */
+
+/* per-agent solver status (maps to cvxpy.OPTIMAL / OPTIMAL_INACCURATE / ...) */
+#define SCVX_STATUS_OPTIMAL 0
+#define SCVX_STATUS_MAX_ITER 1
+#define SCVX_STATUS_NUMERICAL 2
+
+int scvx_version(void);
+const char* scvx_last_error(void);
+
+/*
+ * Batched FOH discretization.  Replaces FirstOrderHold.calculate_discretization
+ * (SCvx/discretization/first_order_hold.py:52-87) for N agents in one launch.
+ *   X [N][K][n], U [N][K][m], sigma [N]  ->  out [N][K-1][n*(n+2m+2)]
+ * nsub = RK4 substeps per interval (1 is exact for the double integrator).
+ * params: model parameters (quadrotor: mass, g, Jx, Jy, Jz) or NULL for defaults.
+ */
+int scvx_foh_batched(int model_id, const double* params, int K, int N, const double* X, const double* U,
+                     const double* sigma, int nsub, double* out, void* stream);
+
+/*
+ * Batched nonlinear roll-outs: FirstOrderHold.integrate_nonlinear_piecewise (piecewise=1) and
+ * integrate_nonlinear_full (piecewise=0) (first_order_hold.py:127-155).  Xout [N][K][n].
+ */
+int scvx_integrate_nonlinear_batched(int model_id, const double* params, int K, int N, const double* X,
+                                     const double* U, const double* sigma, int nsub, int piecewise,
+                                     double* Xout, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Batched trust-region subproblem (one per agent), the convex solve the reference hands to
+ * CVXPY+Clarabel in Distributed_opt/dist_scvx_3d.py:51-111 (x_traj_opt), written in absolute
+ * variables x_t = xbar_t + d_t, u_t = ubar_t + w_t:
+ *
+ *   min  sum_{t<K-1} ||u_t||^2 + w_last ||u_{K-1}||^2 + w_coll sum_t S_t + w_obs sum_{t,o} s_{t,o}
+ *   s.t. x_0 = x_init                                                    (:73, d_0 = 0)
+ *        x_{t+1} = A_t x_t + B_t u_t + C_t u_{t+1} + S_t sigma + z_t      (:80-83; FOH form)
+ *        x_{K-1} = x_final                     if has_final               (:74)
+ *        u_{K-1} = ubar_{K-1}                  if fix_last_input          (:63, unused w row)
+ *   for nodes t < K-1 (and t = K-1 if ineq_last):
+ *        ||u_t - ubar_t||_1 <= tr                                        (:84)
+ *        box_lo[i] <= x_t[box_idx[i]] <= box_hi[i]                         (:87-90)
+ *        b_j - g_j' p_t <= S_t (j < coll_count[t]),  S_t >= 0           (:93-107, shared slack)
+ *        a_o' (p_t - c_o) >= r_o - s_{t,o},  s_{t,o} >= 0,
+ *           a_o = (pbar_t - c_o)/(||pbar_t - c_o|| + 1e-6)   (single_integrator_model.py:113-126)
+ *        ||u_t||_2 <= u_max                    if has_soc                 (single_integrator_model.py:103-104)
+ * with p_t = x_t[0:pos_dim].  Solved by a batched primal-dual interior-point method (Mehrotra
+ * predictor-corrector, Nesterov-Todd scaling for the SOC) whose KKT systems are factored by a
+ * Riccati recursion over the K nodes.
+ * ------------------------------------------------------------------------------------------ */
+#define SCVX_MAX_BOX 4
+#define SCVX_MAX_OBS 16
+
+typedef struct scvx_qp_template {
+    int32_t model_id;       /* only used for n_x/n_u consistency checks */
+    int32_t n_x, n_u, K;
+    int32_t pos_dim;        /* 2 or 3 */
+    int32_t has_final;
+    int32_t fix_last_input;
+    int32_t ineq_last;
+    double w_last;
+    int32_t n_box;
+    int32_t box_idx[SCVX_MAX_BOX];
+    double box_lo[SCVX_MAX_BOX];
+    double box_hi[SCVX_MAX_BOX];
+    int32_t n_obs;
+    double obs_center[SCVX_MAX_OBS][3];
+    double obs_radius[SCVX_MAX_OBS];
+    double w_obs;
+    int32_t j_max;          /* collision rows per node (0 = no coupling) */
+    double w_coll;
+    int32_t has_soc;
+    double u_max;
+    int32_t max_iter;
+    double tol;
+} scvx_qp_template;
+
+/*
+ * Inputs (device, agent-major):
+ *   disc [N][K-1][n(n+2m+2)], sigma [N], Xref [N][K][n], Uref [N][K][m], x_init [N][n],
+ *   x_final [N][n] (ignored unless has_final), tr [N],
+ *   coll_rows [N][K][j_max][pos_dim+1] rows (g, b), coll_count [N][K] (both ignored if j_max=0)
+ * Outputs (device):
+ *   X [N][K][n], U [N][K][m], slack_coll [N][K] (S_t, zeros if j_max = 0), obj [N],
+ *   status [N], iters [N]
+ */
+int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const double* disc, const double* sigma,
+                          const double* Xref, const double* Uref, const double* x_init, const double* x_final,
+                          const double* tr, const double* coll_rows, const int32_t* coll_count, double* X,
+                          double* U, double* slack_coll, double* obj, int32_t* status, int32_t* iters,
+                          void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SCVX_HIP_H */

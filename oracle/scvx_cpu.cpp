@@ -1,0 +1,1007 @@
+// ORACLE / TEST INFRASTRUCTURE ONLY (bench.py cpu_baseline leg, kind "port"; tests).
+//
+// Plain-C++ float64 CPU restatement of the batched trust-region subproblem declared in
+// include/scvx_hip.h (scvx_qp_solve_batched): the per-agent convex solve of
+// Distributed_opt/dist_scvx_3d.py:51-111, which the reference hands to CVXPY+Clarabel.
+// Same problem, same algorithm family as the HIP kernel (primal-dual Mehrotra IPM, NT scaling for
+// the SOC, Riccati factorisation of the node-banded KKT system) but written independently in
+// scalar dense form: every node keeps a dense constraint matrix over (x, u, aux) and the
+// auxiliary slacks are eliminated by a generic dense Schur complement.  Agents are solved one
+// after another (or OpenMP-parallel over agents when nthreads > 1).
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../include/scvx_hip.h"
+
+namespace {
+
+using Vec = std::vector<double>;
+
+struct Mat {
+    int r = 0, c = 0;
+    Vec a;
+    Mat() {}
+    Mat(int r_, int c_) : r(r_), c(c_), a((size_t)r_ * c_, 0.0) {}
+    double& operator()(int i, int j) { return a[(size_t)i * c + j]; }
+    double operator()(int i, int j) const { return a[(size_t)i * c + j]; }
+};
+
+static Mat mul(const Mat& A, const Mat& B) {
+    Mat C(A.r, B.c);
+    for (int i = 0; i < A.r; ++i)
+        for (int k = 0; k < A.c; ++k) {
+            double v = A(i, k);
+            if (v == 0.0) continue;
+            for (int j = 0; j < B.c; ++j) C(i, j) += v * B(k, j);
+        }
+    return C;
+}
+static Mat tr(const Mat& A) {
+    Mat T(A.c, A.r);
+    for (int i = 0; i < A.r; ++i)
+        for (int j = 0; j < A.c; ++j) T(j, i) = A(i, j);
+    return T;
+}
+static Mat add(const Mat& A, const Mat& B) {
+    Mat C = A;
+    for (size_t i = 0; i < C.a.size(); ++i) C.a[i] += B.a[i];
+    return C;
+}
+static Vec matvec(const Mat& A, const Vec& x) {
+    Vec y(A.r, 0.0);
+    for (int i = 0; i < A.r; ++i)
+        for (int j = 0; j < A.c; ++j) y[i] += A(i, j) * x[j];
+    return y;
+}
+static Vec matTvec(const Mat& A, const Vec& x) {
+    Vec y(A.c, 0.0);
+    for (int i = 0; i < A.r; ++i)
+        for (int j = 0; j < A.c; ++j) y[j] += A(i, j) * x[i];
+    return y;
+}
+// Cholesky in place (lower), returns false if not PD
+static bool chol(Mat& L) {
+    int n = L.r;
+    for (int j = 0; j < n; ++j) {
+        double d = L(j, j);
+        for (int k = 0; k < j; ++k) d -= L(j, k) * L(j, k);
+        if (!(d > 0.0)) return false;
+        d = std::sqrt(d);
+        L(j, j) = d;
+        for (int i = j + 1; i < n; ++i) {
+            double v = L(i, j);
+            for (int k = 0; k < j; ++k) v -= L(i, k) * L(j, k);
+            L(i, j) = v / d;
+        }
+        for (int i = 0; i < j; ++i) L(i, j) = 0.0;
+    }
+    return true;
+}
+static void chol_solve(const Mat& L, double* b) {
+    int n = L.r;
+    for (int i = 0; i < n; ++i) {
+        double v = b[i];
+        for (int k = 0; k < i; ++k) v -= L(i, k) * b[k];
+        b[i] = v / L(i, i);
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        double v = b[i];
+        for (int k = i + 1; k < n; ++k) v -= L(k, i) * b[k];
+        b[i] = v / L(i, i);
+    }
+}
+static Mat chol_solve_mat(const Mat& L, const Mat& B) {
+    Mat X = B;
+    Vec col(B.r);
+    for (int j = 0; j < B.c; ++j) {
+        for (int i = 0; i < B.r; ++i) col[i] = X(i, j);
+        chol_solve(L, col.data());
+        for (int i = 0; i < B.r; ++i) X(i, j) = col[i];
+    }
+    return X;
+}
+// LU with partial pivoting solve (small dense)
+static bool lu_solve(Mat A, Vec& b) {
+    int n = A.r;
+    for (int k = 0; k < n; ++k) {
+        int p = k;
+        for (int i = k + 1; i < n; ++i)
+            if (std::fabs(A(i, k)) > std::fabs(A(p, k))) p = i;
+        if (A(p, k) == 0.0) return false;
+        if (p != k) {
+            for (int j = 0; j < n; ++j) std::swap(A(k, j), A(p, j));
+            std::swap(b[k], b[p]);
+        }
+        for (int i = k + 1; i < n; ++i) {
+            double f = A(i, k) / A(k, k);
+            for (int j = k; j < n; ++j) A(i, j) -= f * A(k, j);
+            b[i] -= f * b[k];
+        }
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        double v = b[i];
+        for (int j = i + 1; j < n; ++j) v -= A(i, j) * b[j];
+        b[i] = v / A(i, i);
+    }
+    return true;
+}
+
+// ------------------------------- second-order cone helpers -----------------------------------
+struct Soc {
+    int k = 0;
+    Mat W, Wi, Wi2;
+};
+static double socJ(const double* x, int k) {
+    double v = x[0] * x[0];
+    for (int i = 1; i < k; ++i) v -= x[i] * x[i];
+    return v;
+}
+static void soc_nt(const double* s, const double* z, int k, Soc& S) {
+    S.k = k;
+    double Js = socJ(s, k), Jz = socJ(z, k);
+    double ns = std::sqrt(Js), nz = std::sqrt(Jz);
+    Vec sb(k), zb(k), w(k);
+    double dot = 0.0;
+    for (int i = 0; i < k; ++i) { sb[i] = s[i] / ns; zb[i] = z[i] / nz; dot += sb[i] * zb[i]; }
+    double gam = std::sqrt((1.0 + dot) / 2.0);
+    for (int i = 0; i < k; ++i) w[i] = (sb[i] + (i == 0 ? zb[i] : -zb[i])) / (2.0 * gam);
+    // hyperbolic-rotation form of the NT scaling (W z = W^-1 s), eta = (J(s)/J(z))^(1/4)
+    double eta = std::pow(Js / Jz, 0.25);
+    S.W = Mat(k, k);
+    S.Wi = Mat(k, k);
+    S.W(0, 0) = eta * w[0];
+    S.Wi(0, 0) = w[0] / eta;
+    for (int i = 1; i < k; ++i) {
+        S.W(0, i) = S.W(i, 0) = eta * w[i];
+        S.Wi(0, i) = S.Wi(i, 0) = -w[i] / eta;
+        for (int j = 1; j < k; ++j) {
+            double v = (i == j ? 1.0 : 0.0) + w[i] * w[j] / (1.0 + w[0]);
+            S.W(i, j) = eta * v;
+            S.Wi(i, j) = v / eta;
+        }
+    }
+    S.Wi2 = mul(S.Wi, S.Wi);
+}
+static void jprod(const double* a, const double* b, int k, double* o) {
+    double d = 0.0;
+    for (int i = 0; i < k; ++i) d += a[i] * b[i];
+    Vec t(k);
+    t[0] = d;
+    for (int i = 1; i < k; ++i) t[i] = a[0] * b[i] + b[0] * a[i];
+    for (int i = 0; i < k; ++i) o[i] = t[i];
+}
+static void jdiv(const double* x, const double* r, int k, double* o) {
+    double d = socJ(x, k);
+    double r0 = x[0] * r[0];
+    for (int i = 1; i < k; ++i) r0 -= x[i] * r[i];
+    r0 /= d;
+    Vec t(k);
+    t[0] = r0;
+    for (int i = 1; i < k; ++i) t[i] = (r[i] - r0 * x[i]) / x[0];
+    for (int i = 0; i < k; ++i) o[i] = t[i];
+}
+static double soc_step(const double* x, const double* dx, int k) {
+    double a = socJ(dx, k);
+    double b = x[0] * dx[0];
+    for (int i = 1; i < k; ++i) b -= x[i] * dx[i];
+    b *= 2.0;
+    double c = socJ(x, k);
+    double best = 1e300;
+    if (std::fabs(a) < 1e-300) {
+        if (b < 0) best = std::min(best, -c / b);
+    } else {
+        double disc = b * b - 4 * a * c;
+        if (disc >= 0) {
+            double sq = std::sqrt(disc);
+            double r1 = (-b - sq) / (2 * a), r2 = (-b + sq) / (2 * a);
+            if (r1 > 0) best = std::min(best, r1);
+            if (r2 > 0) best = std::min(best, r2);
+        }
+    }
+    if (dx[0] < 0) best = std::min(best, -x[0] / dx[0]);
+    return best;
+}
+
+// ------------------------------------ per-agent solver --------------------------------------
+struct Node {
+    int nv = 0, na = 0;   // node vars = n + m + na
+    Mat G;                // orthant rows (nr x nv)
+    Vec h;
+    int nr = 0;
+    bool soc = false;
+    Vec q;                // linear cost on node vars
+    Vec pdiag;            // quadratic cost diag on node vars
+    Vec z, s, lam, ssoc, lsoc;
+    bool fixed_u = false;
+};
+
+struct Agent {
+    const scvx_qp_template* T;
+    int n, m, K, pd;
+    std::vector<Node> nd;
+    std::vector<Mat> A, B, C;   // C[t] couples u_{t+1}
+    std::vector<Vec> c;
+    Vec x_init, x_final;
+    Vec y;                       // dynamics multipliers (K-1)*n
+    Vec y_init, y_fin;
+};
+
+static void setup_agent(Agent& ag, const scvx_qp_template* T, const double* disc, double sigma, const double* Xr,
+                        const double* Ur, const double* x_init, const double* x_final, double trv,
+                        const double* crow, const int32_t* ccount) {
+    ag.T = T;
+    int n = T->n_x, m = T->n_u, K = T->K, pd = T->pos_dim;
+    ag.n = n; ag.m = m; ag.K = K; ag.pd = pd;
+    int stride = n * (n + 2 * m + 2);
+    ag.A.assign(K - 1, Mat(n, n));
+    ag.B.assign(K - 1, Mat(n, m));
+    ag.C.assign(K - 1, Mat(n, m));
+    ag.c.assign(K - 1, Vec(n, 0.0));
+    for (int t = 0; t < K - 1; ++t) {
+        const double* d = disc + (size_t)t * stride;
+        for (int j = 0; j < n; ++j)
+            for (int i = 0; i < n; ++i) ag.A[t](i, j) = d[j * n + i];
+        for (int j = 0; j < m; ++j)
+            for (int i = 0; i < n; ++i) {
+                ag.B[t](i, j) = d[n * n + j * n + i];
+                ag.C[t](i, j) = d[n * n + n * m + j * n + i];
+            }
+        for (int i = 0; i < n; ++i) ag.c[t][i] = d[n * n + 2 * n * m + i] * sigma + d[n * n + 2 * n * m + n + i];
+    }
+    ag.x_init.assign(x_init, x_init + n);
+    ag.x_final.assign(n, 0.0);
+    if (T->has_final) ag.x_final.assign(x_final, x_final + n);
+    ag.nd.assign(K, Node());
+    const bool coll = T->j_max > 0;
+    for (int t = 0; t < K; ++t) {
+        Node& N = ag.nd[t];
+        bool ineq = (t < K - 1) || T->ineq_last;
+        N.na = ineq ? (T->n_obs + (coll ? 1 : 0)) : 0;
+        N.nv = n + m + N.na;
+        N.q.assign(N.nv, 0.0);
+        N.pdiag.assign(N.nv, 0.0);
+        double wu = (t < K - 1) ? 1.0 : T->w_last;
+        for (int j = 0; j < m; ++j) N.pdiag[n + j] = 2.0 * wu;
+        N.fixed_u = (t == K - 1) && T->fix_last_input;
+        std::vector<Vec> rows;
+        Vec hs;
+        auto newrow = [&]() { rows.emplace_back(N.nv, 0.0); return (int)rows.size() - 1; };
+        if (ineq) {
+            const double* pb = Xr + (size_t)t * n;
+            const double* ub = Ur + (size_t)t * m;
+            for (int f = 0; f < (1 << m); ++f) {  // L1 ball facets
+                int r = newrow();
+                double hh = trv;
+                for (int j = 0; j < m; ++j) {
+                    double sg = ((f >> j) & 1) ? -1.0 : 1.0;
+                    rows[r][n + j] = sg;
+                    hh += sg * ub[j];
+                }
+                hs.push_back(hh);
+            }
+            for (int b = 0; b < T->n_box; ++b) {
+                int r = newrow(); rows[r][T->box_idx[b]] = 1.0; hs.push_back(T->box_hi[b]);
+                r = newrow(); rows[r][T->box_idx[b]] = -1.0; hs.push_back(-T->box_lo[b]);
+            }
+            for (int o = 0; o < T->n_obs; ++o) {
+                int ai = n + m + o;
+                double diff[3], nr = 0.0;
+                for (int i = 0; i < pd; ++i) { diff[i] = pb[i] - T->obs_center[o][i]; nr += diff[i] * diff[i]; }
+                nr = std::sqrt(nr) + 1e-6;
+                double bo = T->obs_radius[o];
+                int r = newrow();
+                for (int i = 0; i < pd; ++i) {
+                    double a = diff[i] / nr;
+                    rows[r][i] = -a;
+                    bo += a * T->obs_center[o][i];
+                }
+                rows[r][ai] = -1.0;
+                hs.push_back(-bo);
+                r = newrow(); rows[r][ai] = -1.0; hs.push_back(0.0);
+                N.q[ai] = T->w_obs;
+            }
+            if (coll) {
+                int ai = n + m + T->n_obs;
+                int cnt = ccount[t];
+                for (int j = 0; j < cnt; ++j) {
+                    const double* rw = crow + ((size_t)t * T->j_max + j) * (pd + 1);
+                    int r = newrow();
+                    for (int i = 0; i < pd; ++i) rows[r][i] = -rw[i];
+                    rows[r][ai] = -1.0;
+                    hs.push_back(-rw[pd]);
+                }
+                int r = newrow(); rows[r][ai] = -1.0; hs.push_back(0.0);
+                N.q[ai] = T->w_coll;
+            }
+            N.soc = T->has_soc != 0;
+        }
+        N.nr = (int)rows.size();
+        N.G = Mat(N.nr, N.nv);
+        for (int r = 0; r < N.nr; ++r)
+            for (int j = 0; j < N.nv; ++j) N.G(r, j) = rows[r][j];
+        N.h = hs;
+        N.z.assign(N.nv, 0.0);
+        for (int i = 0; i < n; ++i) N.z[i] = Xr[(size_t)t * n + i];
+        for (int j = 0; j < m; ++j) N.z[n + j] = Ur[(size_t)t * m + j];
+        N.s.assign(N.nr, 1.0);
+        N.lam.assign(N.nr, 1.0);
+        if (N.soc) { N.ssoc.assign(m + 1, 0.0); N.lsoc.assign(m + 1, 0.0); }
+    }
+    ag.y.assign((size_t)(K - 1) * n, 0.0);
+    ag.y_init.assign(n, 0.0);
+    ag.y_fin.assign(n, 0.0);
+}
+
+struct NodeLin {   // per-node quantities of one IPM iteration
+    Vec D;          // lam/s
+    Soc soc;
+    Vec lt;         // scaled point (orthant sqrt(s lam); SOC W lam)
+    Mat Hxu;        // reduced (n+m)x(n+m) Hessian after aux elimination
+    Mat Haa_L;      // chol of aux block
+    Mat Hza;        // (n+m) x na coupling
+    Vec rc, rcs;    // ineq residuals
+    Vec rd;         // dual residual over node vars
+};
+
+struct Riccati {
+    std::vector<Mat> P, Kg, L, Pi, kap, Bt;
+    std::vector<Vec> k0, p0;
+    Mat M;
+    bool ok = true;
+};
+
+// factor the Riccati recursion for node Hessians H_t (n+m square, in (x,u) coordinates)
+static void riccati_factor(const Agent& ag, const std::vector<Mat>& H, Riccati& R) {
+    int n = ag.n, m = ag.m, K = ag.K;
+    const bool fin = ag.T->has_final;
+    R.P.assign(K, Mat(n, n));
+    R.Kg.assign(K, Mat(m, n));
+    R.L.assign(K, Mat(m, m));
+    R.Pi.assign(K, Mat(n, n));
+    R.kap.assign(K, Mat(m, n));
+    R.Bt.assign(K, Mat(n, m));
+    R.k0.assign(K, Vec(m));
+    R.p0.assign(K, Vec(n));
+    R.M = Mat(n, n);
+    R.ok = true;
+    for (int t = 0; t < K - 1; ++t) {
+        R.Bt[t] = ag.B[t];
+        if (t > 0) R.Bt[t] = add(ag.B[t], mul(ag.A[t], ag.C[t - 1]));
+    }
+    for (int t = K - 1; t >= 0; --t) {
+        // node Hessian in (xi, v) coordinates: x = xi + C_{t-1} v
+        Mat Hxx(n, n), Hxu(n, m), Huu(m, m);
+        for (int i = 0; i < n; ++i)
+            for (int j = 0; j < n; ++j) Hxx(i, j) = H[t](i, j);
+        for (int i = 0; i < n; ++i)
+            for (int j = 0; j < m; ++j) Hxu(i, j) = H[t](i, n + j);
+        for (int i = 0; i < m; ++i)
+            for (int j = 0; j < m; ++j) Huu(i, j) = H[t](n + i, n + j);
+        Mat Q = Hxx, S = Hxu, Rm = Huu;
+        if (t > 0) {
+            const Mat& Cp = ag.C[t - 1];
+            S = add(mul(Hxx, Cp), Hxu);
+            Rm = add(add(mul(tr(Cp), mul(Hxx, Cp)), mul(tr(Cp), Hxu)), add(mul(tr(Hxu), Cp), Huu));
+        }
+        Mat Qh = Q, Sh = tr(S), Rh = Rm;
+        if (t < K - 1) {
+            const Mat& Pn = R.P[t + 1];
+            Mat PA = mul(Pn, ag.A[t]), PB = mul(Pn, R.Bt[t]);
+            Qh = add(Q, mul(tr(ag.A[t]), PA));
+            Sh = add(tr(S), mul(tr(R.Bt[t]), PA));
+            Rh = add(Rm, mul(tr(R.Bt[t]), PB));
+        }
+        if (ag.nd[t].fixed_u) {
+            for (int i = 0; i < m; ++i) {
+                for (int j = 0; j < m; ++j) Rh(i, j) = (i == j) ? 1.0 : 0.0;
+                for (int j = 0; j < n; ++j) Sh(i, j) = 0.0;
+            }
+        }
+        Mat L = Rh;
+        if (!chol(L)) { R.ok = false; return; }
+        R.L[t] = L;
+        Mat Kg = chol_solve_mat(L, Sh);
+        for (double& v : Kg.a) v = -v;
+        R.Kg[t] = Kg;
+        Mat P = add(Qh, mul(tr(Sh), Kg));
+        for (int i = 0; i < n; ++i)
+            for (int j = 0; j < i; ++j) { double v = 0.5 * (P(i, j) + P(j, i)); P(i, j) = P(j, i) = v; }
+        R.P[t] = P;
+        if (fin) {
+            if (t == K - 1) {
+                Mat rhs(m, n);  // C_{K-2}^T
+                if (K >= 2)
+                    for (int i = 0; i < m; ++i)
+                        for (int j = 0; j < n; ++j) rhs(i, j) = ag.C[K - 2](j, i);
+                if (ag.nd[t].fixed_u) rhs = Mat(m, n);
+                Mat kap = chol_solve_mat(L, rhs);
+                for (double& v : kap.a) v = -v;
+                R.kap[t] = kap;
+                Mat I(n, n);
+                for (int i = 0; i < n; ++i) I(i, i) = 1.0;
+                R.Pi[t] = add(I, mul(tr(Sh), kap));
+                R.M = (K >= 2) ? mul(ag.C[K - 2], kap) : Mat(n, n);
+            } else {
+                const Mat& Pin = R.Pi[t + 1];
+                Mat rhs = mul(tr(R.Bt[t]), Pin);
+                if (ag.nd[t].fixed_u) rhs = Mat(m, n);
+                Mat kap = chol_solve_mat(L, rhs);
+                for (double& v : kap.a) v = -v;
+                R.kap[t] = kap;
+                R.Pi[t] = add(mul(tr(ag.A[t]), Pin), mul(tr(Sh), kap));
+                R.M = add(R.M, mul(tr(Pin), mul(R.Bt[t], kap)));
+            }
+        }
+    }
+}
+
+// Solve  min 1/2 dz'H dz - r1'dz  s.t. A dz = r2  ; returns dz (K*(n+m)), dy (K-1)*n, dyi, dyf
+static bool riccati_solve(const Agent& ag, const std::vector<Mat>& H, Riccati& R, const std::vector<Vec>& r1,
+                          const Vec& xi0, const std::vector<Vec>& e, const Vec& r2fin, std::vector<Vec>& dz,
+                          Vec& dy, Vec& dyi, Vec& dyf) {
+    (void)H;
+    int n = ag.n, m = ag.m, K = ag.K;
+    const bool fin = ag.T->has_final;
+    Vec xacc(n, 0.0);
+    for (int t = K - 1; t >= 0; --t) {
+        Vec q(n), r(m);
+        for (int i = 0; i < n; ++i) q[i] = -r1[t][i];
+        for (int j = 0; j < m; ++j) r[j] = -r1[t][n + j];
+        if (t > 0) {
+            Vec ct = matTvec(ag.C[t - 1], q);
+            for (int j = 0; j < m; ++j) r[j] += ct[j];
+        }
+        Vec qh = q, rh = r;
+        if (t < K - 1) {
+            Vec h = matvec(R.P[t + 1], e[t]);
+            for (int i = 0; i < n; ++i) h[i] += R.p0[t + 1][i];
+            Vec a = matTvec(ag.A[t], h), b = matTvec(R.Bt[t], h);
+            for (int i = 0; i < n; ++i) qh[i] += a[i];
+            for (int j = 0; j < m; ++j) rh[j] += b[j];
+        }
+        if (ag.nd[t].fixed_u)
+            for (int j = 0; j < m; ++j) rh[j] = 0.0;
+        Vec k = rh;
+        chol_solve(R.L[t], k.data());
+        for (double& v : k) v = -v;
+        R.k0[t] = k;
+        Vec p = qh, kt = matTvec(R.Kg[t], rh);
+        for (int i = 0; i < n; ++i) p[i] += kt[i];
+        R.p0[t] = p;
+        if (fin) {
+            if (t == K - 1) {
+                xacc = (K >= 2) ? matvec(ag.C[K - 2], k) : Vec(n, 0.0);
+            } else {
+                Vec bk = matvec(R.Bt[t], k);
+                for (int i = 0; i < n; ++i) bk[i] += e[t][i];
+                Vec g = matTvec(R.Pi[t + 1], bk);
+                for (int i = 0; i < n; ++i) xacc[i] += g[i];
+            }
+        }
+    }
+    Vec mu(n, 0.0);
+    if (fin) {
+        Vec g = matTvec(R.Pi[0], xi0);
+        for (int i = 0; i < n; ++i) mu[i] = r2fin[i] - (xacc[i] + g[i]);
+        if (!lu_solve(R.M, mu)) return false;
+    }
+    Vec xi = xi0;
+    dz.assign(K, Vec(n + m, 0.0));
+    dy.assign((size_t)(K - 1) * n, 0.0);
+    auto pfull = [&](int t) {
+        Vec p = R.p0[t];
+        if (fin) {
+            Vec g = matvec(R.Pi[t], mu);
+            for (int i = 0; i < n; ++i) p[i] += g[i];
+        }
+        return p;
+    };
+    {
+        Vec p = pfull(0), Px = matvec(R.P[0], xi0);
+        dyi.assign(n, 0.0);
+        for (int i = 0; i < n; ++i) dyi[i] = -(Px[i] + p[i]);
+    }
+    for (int t = 0; t < K; ++t) {
+        Vec v = matvec(R.Kg[t], xi);
+        for (int j = 0; j < m; ++j) v[j] += R.k0[t][j];
+        if (fin) {
+            Vec g = matvec(R.kap[t], mu);
+            for (int j = 0; j < m; ++j) v[j] += g[j];
+        }
+        Vec x = xi;
+        if (t > 0) {
+            Vec cv = matvec(ag.C[t - 1], v);
+            for (int i = 0; i < n; ++i) x[i] += cv[i];
+        }
+        for (int i = 0; i < n; ++i) dz[t][i] = x[i];
+        for (int j = 0; j < m; ++j) dz[t][n + j] = v[j];
+        if (t < K - 1) {
+            Vec a = matvec(ag.A[t], xi), b = matvec(R.Bt[t], v);
+            Vec xn(n);
+            for (int i = 0; i < n; ++i) xn[i] = a[i] + b[i] + e[t][i];
+            Vec p = pfull(t + 1), Px = matvec(R.P[t + 1], xn);
+            for (int i = 0; i < n; ++i) dy[(size_t)t * n + i] = -(Px[i] + p[i]);
+            xi = xn;
+        }
+    }
+    dyf = mu;
+    return true;
+}
+
+// CVXOPT-style starting point: from the reference trajectory z_ref (aux = 0) take the minimiser of
+//   1/2 z'Pz + q'z + 1/2 ||Gz - h||^2   s.t.  Az = b
+// (one Riccati solve with unit scaling), then s = h - Gz, lam = Gz - h, each shifted into the
+// cone interior by a common multiple of the identity (oracle/qp_dense.py solve_conic_qp does the same).
+static bool init_point(Agent& ag) {
+    const scvx_qp_template* T = ag.T;
+    int n = ag.n, m = ag.m, K = ag.K;
+    std::vector<Mat> H(K), Hza(K), HaaL(K);
+    std::vector<Vec> r1(K), r1a(K);
+    for (int t = 0; t < K; ++t) {
+        Node& N = ag.nd[t];
+        Mat Hf(N.nv, N.nv);
+        for (int j = 0; j < N.nv; ++j) Hf(j, j) = N.pdiag[j];
+        for (int r = 0; r < N.nr; ++r)
+            for (int i = 0; i < N.nv; ++i)
+                for (int j = 0; j < N.nv; ++j) Hf(i, j) += N.G(r, i) * N.G(r, j);
+        Vec rf(N.nv);
+        for (int j = 0; j < N.nv; ++j) rf[j] = -(N.pdiag[j] * N.z[j] + N.q[j]);
+        for (int r = 0; r < N.nr; ++r) {
+            double v = -N.h[r];
+            for (int j = 0; j < N.nv; ++j) v += N.G(r, j) * N.z[j];
+            for (int j = 0; j < N.nv; ++j) rf[j] -= N.G(r, j) * v;
+        }
+        if (N.soc)
+            for (int j = 0; j < m; ++j) { Hf(n + j, n + j) += 1.0; rf[n + j] -= N.z[n + j]; }
+        if (N.fixed_u)
+            for (int j = 0; j < m; ++j) rf[n + j] = 0.0;
+        int nz = n + m, na = N.na;
+        H[t] = Mat(nz, nz);
+        for (int i = 0; i < nz; ++i)
+            for (int j = 0; j < nz; ++j) H[t](i, j) = Hf(i, j);
+        r1[t].assign(rf.begin(), rf.begin() + nz);
+        if (na > 0) {
+            Mat Haa(na, na);
+            Hza[t] = Mat(nz, na);
+            for (int i = 0; i < na; ++i)
+                for (int j = 0; j < na; ++j) Haa(i, j) = Hf(nz + i, nz + j);
+            for (int i = 0; i < nz; ++i)
+                for (int j = 0; j < na; ++j) Hza[t](i, j) = Hf(i, nz + j);
+            HaaL[t] = Haa;
+            if (!chol(HaaL[t])) return false;
+            Mat X = chol_solve_mat(HaaL[t], tr(Hza[t]));
+            Mat corr = mul(Hza[t], X);
+            for (size_t i = 0; i < H[t].a.size(); ++i) H[t].a[i] -= corr.a[i];
+            r1a[t].assign(rf.begin() + nz, rf.end());
+            Vec ra = r1a[t];
+            chol_solve(HaaL[t], ra.data());
+            Vec c = matvec(Hza[t], ra);
+            for (int i = 0; i < nz; ++i) r1[t][i] -= c[i];
+        }
+    }
+    Riccati R;
+    riccati_factor(ag, H, R);
+    if (!R.ok) return false;
+    Vec xi0(n), r2f(n, 0.0);
+    for (int i = 0; i < n; ++i) xi0[i] = ag.x_init[i] - ag.nd[0].z[i];
+    if (T->has_final)
+        for (int i = 0; i < n; ++i) r2f[i] = ag.x_final[i] - ag.nd[K - 1].z[i];
+    std::vector<Vec> e(K - 1, Vec(n));
+    for (int t = 0; t < K - 1; ++t) {
+        const Vec& z0 = ag.nd[t].z;
+        const Vec& z1 = ag.nd[t + 1].z;
+        for (int i = 0; i < n; ++i) {
+            double v = z1[i] - ag.c[t][i];
+            for (int k = 0; k < n; ++k) v -= ag.A[t](i, k) * z0[k];
+            for (int j = 0; j < m; ++j) v -= ag.B[t](i, j) * z0[n + j] + ag.C[t](i, j) * z1[n + j];
+            e[t][i] = -v;
+        }
+    }
+    std::vector<Vec> dz;
+    Vec dy, dyi, dyf;
+    if (!riccati_solve(ag, H, R, r1, xi0, e, r2f, dz, dy, dyi, dyf)) return false;
+    double smin = 1e300, lmin = 1e300;
+    for (int t = 0; t < K; ++t) {
+        Node& N = ag.nd[t];
+        int nz = n + m;
+        for (int i = 0; i < nz; ++i) N.z[i] += dz[t][i];
+        if (N.na > 0) {
+            Vec ra = r1a[t];
+            Vec c = matTvec(Hza[t], dz[t]);
+            for (int a = 0; a < N.na; ++a) ra[a] -= c[a];
+            chol_solve(HaaL[t], ra.data());
+            for (int a = 0; a < N.na; ++a) N.z[nz + a] += ra[a];
+        }
+        for (int r = 0; r < N.nr; ++r) {
+            double v = N.h[r];
+            for (int j = 0; j < N.nv; ++j) v -= N.G(r, j) * N.z[j];
+            N.s[r] = v;
+            N.lam[r] = -v;
+            smin = std::min(smin, v);
+            lmin = std::min(lmin, -v);
+        }
+        if (N.soc) {
+            N.ssoc[0] = T->u_max;
+            N.lsoc[0] = -T->u_max;
+            double nu = 0.0;
+            for (int j = 0; j < m; ++j) { N.ssoc[1 + j] = N.z[n + j]; N.lsoc[1 + j] = -N.z[n + j]; nu += N.z[n + j] * N.z[n + j]; }
+            smin = std::min(smin, T->u_max - std::sqrt(nu));
+            lmin = std::min(lmin, -T->u_max - std::sqrt(nu));
+        }
+    }
+    double sh_s = std::max(0.0, 1.0 - smin), sh_l = std::max(0.0, 1.0 - lmin);
+    for (int t = 0; t < K; ++t) {
+        Node& N = ag.nd[t];
+        for (int r = 0; r < N.nr; ++r) { N.s[r] += sh_s; N.lam[r] += sh_l; }
+        if (N.soc) { N.ssoc[0] += sh_s; N.lsoc[0] += sh_l; }
+    }
+    return true;
+}
+
+static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
+    const scvx_qp_template* T = ag.T;
+    int n = ag.n, m = ag.m, K = ag.K;
+    int deg = 0;
+    for (int t = 0; t < K; ++t) deg += ag.nd[t].nr + (ag.nd[t].soc ? 1 : 0);
+    std::vector<NodeLin> L(K);
+    std::vector<Mat> H(K);
+    Riccati R;
+    int status = SCVX_STATUS_MAX_ITER;
+    int it = 0;
+    const double tol = T->tol > 0 ? T->tol : 1e-9;
+    if (!init_point(ag)) { iters_out = 0; obj_out = 0.0; return SCVX_STATUS_NUMERICAL; }
+    for (it = 0; it < T->max_iter; ++it) {
+        // ---- residuals
+        double pres = 0.0, dres = 0.0, gap = 0.0, hscale = 1.0, qscale = 1.0;
+        std::vector<Vec> rp(K - 1, Vec(n));
+        Vec rpi(n), rpf(n, 0.0);
+        for (int i = 0; i < n; ++i) rpi[i] = ag.nd[0].z[i] - ag.x_init[i];
+        if (T->has_final)
+            for (int i = 0; i < n; ++i) rpf[i] = ag.nd[K - 1].z[i] - ag.x_final[i];
+        for (int t = 0; t < K - 1; ++t) {
+            const Vec& z0 = ag.nd[t].z;
+            const Vec& z1 = ag.nd[t + 1].z;
+            for (int i = 0; i < n; ++i) {
+                double v = z1[i] - ag.c[t][i];
+                for (int k = 0; k < n; ++k) v -= ag.A[t](i, k) * z0[k];
+                for (int j = 0; j < m; ++j) v -= ag.B[t](i, j) * z0[n + j] + ag.C[t](i, j) * z1[n + j];
+                rp[t][i] = v;
+                pres = std::max(pres, std::fabs(v));
+            }
+        }
+        for (int i = 0; i < n; ++i) pres = std::max({pres, std::fabs(rpi[i]), std::fabs(rpf[i])});
+        for (int t = 0; t < K; ++t) {
+            Node& N = ag.nd[t];
+            NodeLin& l = L[t];
+            l.rc.assign(N.nr, 0.0);
+            for (int r = 0; r < N.nr; ++r) {
+                double v = N.s[r] - N.h[r];
+                for (int j = 0; j < N.nv; ++j) v += N.G(r, j) * N.z[j];
+                l.rc[r] = v;
+                pres = std::max(pres, std::fabs(v));
+                hscale = std::max(hscale, std::fabs(N.h[r]));
+                gap += N.s[r] * N.lam[r];
+            }
+            if (N.soc) {
+                l.rcs.assign(m + 1, 0.0);
+                l.rcs[0] = N.ssoc[0] - T->u_max;
+                for (int j = 0; j < m; ++j) l.rcs[1 + j] = N.ssoc[1 + j] - N.z[n + j];
+                for (int j = 0; j <= m; ++j) { pres = std::max(pres, std::fabs(l.rcs[j])); gap += N.ssoc[j] * N.lsoc[j]; }
+                hscale = std::max(hscale, T->u_max);
+            }
+            l.rd.assign(N.nv, 0.0);
+            for (int j = 0; j < N.nv; ++j) { l.rd[j] = N.pdiag[j] * N.z[j] + N.q[j]; qscale = std::max(qscale, std::fabs(N.q[j])); }
+            for (int r = 0; r < N.nr; ++r)
+                for (int j = 0; j < N.nv; ++j) l.rd[j] += N.G(r, j) * N.lam[r];
+            if (N.soc)
+                for (int j = 0; j < m; ++j) l.rd[n + j] -= N.lsoc[1 + j];
+            // A^T y
+            if (t == 0)
+                for (int i = 0; i < n; ++i) l.rd[i] += ag.y_init[i];
+            if (t == K - 1 && T->has_final)
+                for (int i = 0; i < n; ++i) l.rd[i] += ag.y_fin[i];
+            if (t >= 1) {
+                const double* yp = &ag.y[(size_t)(t - 1) * n];
+                for (int i = 0; i < n; ++i) l.rd[i] += yp[i];
+                for (int j = 0; j < m; ++j)
+                    for (int i = 0; i < n; ++i) l.rd[n + j] -= ag.C[t - 1](i, j) * yp[i];
+            }
+            if (t < K - 1) {
+                const double* yt = &ag.y[(size_t)t * n];
+                for (int k = 0; k < n; ++k)
+                    for (int i = 0; i < n; ++i) l.rd[k] -= ag.A[t](i, k) * yt[i];
+                for (int j = 0; j < m; ++j)
+                    for (int i = 0; i < n; ++i) l.rd[n + j] -= ag.B[t](i, j) * yt[i];
+            }
+            if (N.fixed_u)
+                for (int j = 0; j < m; ++j) l.rd[n + j] = 0.0;
+            for (int j = 0; j < N.nv; ++j) dres = std::max(dres, std::fabs(l.rd[j]));
+        }
+        double mu = gap / std::max(deg, 1);
+        double pobj = 0.0;
+        for (int t = 0; t < K; ++t)
+            for (int j = 0; j < ag.nd[t].nv; ++j) {
+                double zj = ag.nd[t].z[j];
+                pobj += 0.5 * ag.nd[t].pdiag[j] * zj * zj + ag.nd[t].q[j] * zj;
+            }
+        if (std::getenv("SCVX_DEBUG")) std::fprintf(stderr, "it %d pres %.3e dres %.3e mu %.3e pobj %.6e\n", it, pres, dres, mu, pobj);
+        if (!std::isfinite(pres + dres + mu)) { status = SCVX_STATUS_NUMERICAL; break; }
+        if (pres <= tol * hscale && dres <= tol * qscale && gap <= tol * std::max(1.0, std::fabs(pobj))) {
+            status = SCVX_STATUS_OPTIMAL;
+            break;
+        }
+        // ---- scaling and node Hessians (aux eliminated)
+        for (int t = 0; t < K; ++t) {
+            Node& N = ag.nd[t];
+            NodeLin& l = L[t];
+            l.D.assign(N.nr, 0.0);
+            l.lt.assign(N.nr + (N.soc ? m + 1 : 0), 0.0);
+            for (int r = 0; r < N.nr; ++r) { l.D[r] = N.lam[r] / N.s[r]; l.lt[r] = std::sqrt(N.s[r] * N.lam[r]); }
+            Mat Hf(N.nv, N.nv);
+            for (int j = 0; j < N.nv; ++j) Hf(j, j) = N.pdiag[j];
+            for (int r = 0; r < N.nr; ++r)
+                for (int i = 0; i < N.nv; ++i) {
+                    double gi = N.G(r, i);
+                    if (gi == 0.0) continue;
+                    for (int j = 0; j < N.nv; ++j) Hf(i, j) += l.D[r] * gi * N.G(r, j);
+                }
+            if (N.soc) {
+                soc_nt(N.ssoc.data(), N.lsoc.data(), m + 1, l.soc);
+                Vec wl = matvec(l.soc.W, N.lsoc);
+                for (int j = 0; j <= m; ++j) l.lt[N.nr + j] = wl[j];
+                for (int i = 0; i < m; ++i)
+                    for (int j = 0; j < m; ++j) Hf(n + i, n + j) += l.soc.Wi2(1 + i, 1 + j);
+            }
+            int nz = n + m, na = N.na;
+            l.Hxu = Mat(nz, nz);
+            for (int i = 0; i < nz; ++i)
+                for (int j = 0; j < nz; ++j) l.Hxu(i, j) = Hf(i, j);
+            if (na > 0) {
+                Mat Haa(na, na);
+                l.Hza = Mat(nz, na);
+                for (int i = 0; i < na; ++i)
+                    for (int j = 0; j < na; ++j) Haa(i, j) = Hf(nz + i, nz + j);
+                for (int i = 0; i < nz; ++i)
+                    for (int j = 0; j < na; ++j) l.Hza(i, j) = Hf(i, nz + j);
+                l.Haa_L = Haa;
+                if (!chol(l.Haa_L)) { status = SCVX_STATUS_NUMERICAL; goto done; }
+                Mat X = chol_solve_mat(l.Haa_L, tr(l.Hza));  // na x nz
+                Mat corr = mul(l.Hza, X);
+                for (size_t i = 0; i < l.Hxu.a.size(); ++i) l.Hxu.a[i] -= corr.a[i];
+            }
+            H[t] = l.Hxu;
+        }
+        riccati_factor(ag, H, R);
+        if (!R.ok) { status = SCVX_STATUS_NUMERICAL; break; }
+        {
+            // ---- one Newton solve for a given complementarity rhs (orthant rco, SOC rcs2)
+            auto newton = [&](const std::vector<Vec>& rco, const std::vector<Vec>& rcq, std::vector<Vec>& dz,
+                              std::vector<Vec>& ds, std::vector<Vec>& dl, std::vector<Vec>& dsq,
+                              std::vector<Vec>& dlq, Vec& dy, Vec& dyi, Vec& dyf) -> bool {
+                std::vector<Vec> r1(K), r1a(K), tq(K);
+                for (int t = 0; t < K; ++t) {
+                    Node& N = ag.nd[t];
+                    NodeLin& l = L[t];
+                    Vec rf(N.nv);
+                    for (int j = 0; j < N.nv; ++j) rf[j] = -l.rd[j];
+                    for (int r = 0; r < N.nr; ++r) {
+                        double tr_ = (rco[t][r] + N.lam[r] * l.rc[r]) / N.s[r];
+                        for (int j = 0; j < N.nv; ++j) rf[j] -= N.G(r, j) * tr_;
+                    }
+                    if (N.soc) {
+                        Vec rho(m + 1);
+                        jdiv(&l.lt[N.nr], rcq[t].data(), m + 1, rho.data());
+                        Vec t1 = matvec(l.soc.Wi, rho), t2 = matvec(l.soc.Wi2, l.rcs);
+                        tq[t].assign(m + 1, 0.0);
+                        for (int j = 0; j <= m; ++j) tq[t][j] = t1[j] + t2[j];
+                        for (int j = 0; j < m; ++j) rf[n + j] += tq[t][1 + j];  // G^T t, G = [0; -I]
+                    }
+                    if (N.fixed_u)
+                        for (int j = 0; j < m; ++j) rf[n + j] = 0.0;
+                    int nz = n + m;
+                    r1[t].assign(rf.begin(), rf.begin() + nz);
+                    if (N.na > 0) {
+                        Vec ra(rf.begin() + nz, rf.end());
+                        chol_solve(l.Haa_L, ra.data());
+                        Vec c = matvec(l.Hza, ra);
+                        for (int i = 0; i < nz; ++i) r1[t][i] -= c[i];
+                        r1a[t].assign(rf.begin() + nz, rf.end());
+                    }
+                }
+                Vec xi0(n);
+                for (int i = 0; i < n; ++i) xi0[i] = -rpi[i];
+                std::vector<Vec> e(K - 1, Vec(n));
+                for (int t = 0; t < K - 1; ++t)
+                    for (int i = 0; i < n; ++i) e[t][i] = -rp[t][i];
+                Vec r2f(n);
+                for (int i = 0; i < n; ++i) r2f[i] = -rpf[i];
+                std::vector<Vec> dzx;
+                if (!riccati_solve(ag, H, R, r1, xi0, e, r2f, dzx, dy, dyi, dyf)) return false;
+                if (std::getenv("SCVX_DEBUG")) {
+                    double e1 = 0.0, e2 = 0.0;
+                    for (int t = 0; t < K; ++t) {
+                        Vec st = matvec(H[t], dzx[t]);
+                        for (int i = 0; i < n + m; ++i) st[i] -= r1[t][i];
+                        if (t == 0) for (int i = 0; i < n; ++i) st[i] += dyi[i];
+                        if (t == K - 1 && ag.T->has_final) for (int i = 0; i < n; ++i) st[i] += dyf[i];
+                        if (t >= 1) {
+                            const double* yp = &dy[(size_t)(t - 1) * n];
+                            for (int i = 0; i < n; ++i) st[i] += yp[i];
+                            for (int j = 0; j < m; ++j) for (int i = 0; i < n; ++i) st[n + j] -= ag.C[t - 1](i, j) * yp[i];
+                        }
+                        if (t < K - 1) {
+                            const double* yt = &dy[(size_t)t * n];
+                            for (int k = 0; k < n; ++k) for (int i = 0; i < n; ++i) st[k] -= ag.A[t](i, k) * yt[i];
+                            for (int j = 0; j < m; ++j) for (int i = 0; i < n; ++i) st[n + j] -= ag.B[t](i, j) * yt[i];
+                            for (int i = 0; i < n; ++i) {
+                                double v = dzx[t + 1][i] - e[t][i];
+                                for (int k = 0; k < n; ++k) v -= ag.A[t](i, k) * dzx[t][k];
+                                for (int j = 0; j < m; ++j) v -= ag.B[t](i, j) * dzx[t][n + j] + ag.C[t](i, j) * dzx[t + 1][n + j];
+                                e2 = std::max(e2, std::fabs(v));
+                            }
+                        }
+                        int lim = ag.nd[t].fixed_u ? n : n + m;
+                        for (int i = 0; i < lim; ++i) e1 = std::max(e1, std::fabs(st[i]));
+                    }
+                    for (int i = 0; i < n; ++i) e2 = std::max(e2, std::fabs(dzx[0][i] - xi0[i]));
+                    if (ag.T->has_final) for (int i = 0; i < n; ++i) e2 = std::max(e2, std::fabs(dzx[K - 1][i] - r2f[i]));
+                    std::fprintf(stderr, "   kkt check: stationarity %.3e equality %.3e\n", e1, e2);
+                }
+                dz.assign(K, Vec());
+                ds.assign(K, Vec());
+                dl.assign(K, Vec());
+                dsq.assign(K, Vec());
+                dlq.assign(K, Vec());
+                for (int t = 0; t < K; ++t) {
+                    Node& N = ag.nd[t];
+                    NodeLin& l = L[t];
+                    int nz = n + m;
+                    dz[t].assign(N.nv, 0.0);
+                    for (int i = 0; i < nz; ++i) dz[t][i] = dzx[t][i];
+                    if (N.na > 0) {
+                        Vec ra = r1a[t];
+                        Vec c = matTvec(l.Hza, dzx[t]);
+                        for (int a = 0; a < N.na; ++a) ra[a] -= c[a];
+                        chol_solve(l.Haa_L, ra.data());
+                        for (int a = 0; a < N.na; ++a) dz[t][nz + a] = ra[a];
+                    }
+                    ds[t].assign(N.nr, 0.0);
+                    dl[t].assign(N.nr, 0.0);
+                    for (int r = 0; r < N.nr; ++r) {
+                        double g = 0.0;
+                        for (int j = 0; j < N.nv; ++j) g += N.G(r, j) * dz[t][j];
+                        ds[t][r] = -l.rc[r] - g;
+                        dl[t][r] = (rco[t][r] + N.lam[r] * (l.rc[r] + g)) / N.s[r];
+                    }
+                    if (N.soc) {
+                        Vec gq(m + 1, 0.0);
+                        for (int j = 0; j < m; ++j) gq[1 + j] = -dz[t][n + j];
+                        dsq[t].assign(m + 1, 0.0);
+                        for (int j = 0; j <= m; ++j) dsq[t][j] = -l.rcs[j] - gq[j];
+                        Vec rho(m + 1), v(m + 1);
+                        jdiv(&l.lt[N.nr], rcq[t].data(), m + 1, rho.data());
+                        for (int j = 0; j <= m; ++j) v[j] = l.rcs[j] + gq[j];
+                        Vec a = matvec(l.soc.Wi, rho), b = matvec(l.soc.Wi2, v);
+                        dlq[t].assign(m + 1, 0.0);
+                        for (int j = 0; j <= m; ++j) dlq[t][j] = a[j] + b[j];
+                    }
+                }
+                return true;
+            };
+            auto max_step = [&](const std::vector<Vec>& ds, const std::vector<Vec>& dl, const std::vector<Vec>& dsq,
+                                const std::vector<Vec>& dlq) {
+                double a = 1e300;
+                for (int t = 0; t < K; ++t) {
+                    Node& N = ag.nd[t];
+                    for (int r = 0; r < N.nr; ++r) {
+                        if (ds[t][r] < 0) a = std::min(a, -N.s[r] / ds[t][r]);
+                        if (dl[t][r] < 0) a = std::min(a, -N.lam[r] / dl[t][r]);
+                    }
+                    if (N.soc) {
+                        a = std::min(a, soc_step(N.ssoc.data(), dsq[t].data(), m + 1));
+                        a = std::min(a, soc_step(N.lsoc.data(), dlq[t].data(), m + 1));
+                    }
+                }
+                return a;
+            };
+            // predictor
+            std::vector<Vec> rco(K), rcq(K);
+            for (int t = 0; t < K; ++t) {
+                Node& N = ag.nd[t];
+                rco[t].assign(N.nr, 0.0);
+                for (int r = 0; r < N.nr; ++r) rco[t][r] = -N.s[r] * N.lam[r];
+                if (N.soc) {
+                    rcq[t].assign(m + 1, 0.0);
+                    jprod(&L[t].lt[N.nr], &L[t].lt[N.nr], m + 1, rcq[t].data());
+                    for (double& v : rcq[t]) v = -v;
+                }
+            }
+            std::vector<Vec> dz, ds, dl, dsq, dlq;
+            Vec dy, dyi, dyf;
+            if (!newton(rco, rcq, dz, ds, dl, dsq, dlq, dy, dyi, dyf)) { status = SCVX_STATUS_NUMERICAL; break; }
+            double aa = std::min(1.0, max_step(ds, dl, dsq, dlq));
+            double gap_a = 0.0;
+            for (int t = 0; t < K; ++t) {
+                Node& N = ag.nd[t];
+                for (int r = 0; r < N.nr; ++r) gap_a += (N.s[r] + aa * ds[t][r]) * (N.lam[r] + aa * dl[t][r]);
+                if (N.soc)
+                    for (int j = 0; j <= m; ++j) gap_a += (N.ssoc[j] + aa * dsq[t][j]) * (N.lsoc[j] + aa * dlq[t][j]);
+            }
+            double mu_a = gap_a / std::max(deg, 1);
+            double sig = std::pow(std::max(mu_a, 0.0) / mu, 3.0);
+            // corrector
+            for (int t = 0; t < K; ++t) {
+                Node& N = ag.nd[t];
+                for (int r = 0; r < N.nr; ++r) rco[t][r] += -ds[t][r] * dl[t][r] + sig * mu;
+                if (N.soc) {
+                    Vec a = matvec(L[t].soc.Wi, dsq[t]), b = matvec(L[t].soc.W, dlq[t]), c(m + 1);
+                    jprod(a.data(), b.data(), m + 1, c.data());
+                    for (int j = 0; j <= m; ++j) rcq[t][j] -= c[j];
+                    rcq[t][0] += sig * mu;
+                }
+            }
+            if (!newton(rco, rcq, dz, ds, dl, dsq, dlq, dy, dyi, dyf)) { status = SCVX_STATUS_NUMERICAL; break; }
+            double al = std::min(1.0, 0.99 * max_step(ds, dl, dsq, dlq));
+            if (std::getenv("SCVX_DEBUG")) {
+                std::fprintf(stderr, "   alpha_aff %.3e sigma %.3e alpha %.3e\n", aa, sig, al);
+                for (int t = 0; t < K; ++t) { Node& N = ag.nd[t]; for (int r = 0; r < N.nr; ++r) {
+                    double a1 = ds[t][r] < 0 ? -N.s[r]/ds[t][r] : 1e300, a2 = dl[t][r] < 0 ? -N.lam[r]/dl[t][r] : 1e300;
+                    if (std::min(a1,a2) < 1.01*al/0.99) std::fprintf(stderr, "     t %d r %d s %.3e ds %.3e lam %.3e dl %.3e\n", t, r, N.s[r], ds[t][r], N.lam[r], dl[t][r]); } }
+            }
+            for (int t = 0; t < K; ++t) {
+                Node& N = ag.nd[t];
+                for (int j = 0; j < N.nv; ++j) N.z[j] += al * dz[t][j];
+                for (int r = 0; r < N.nr; ++r) { N.s[r] += al * ds[t][r]; N.lam[r] += al * dl[t][r]; }
+                if (N.soc)
+                    for (int j = 0; j <= m; ++j) { N.ssoc[j] += al * dsq[t][j]; N.lsoc[j] += al * dlq[t][j]; }
+            }
+            for (size_t i = 0; i < ag.y.size(); ++i) ag.y[i] += al * dy[i];
+            for (int i = 0; i < n; ++i) { ag.y_init[i] += al * dyi[i]; ag.y_fin[i] += al * dyf[i]; }
+        }
+    }
+done:
+    double pobj = 0.0;
+    for (int t = 0; t < K; ++t)
+        for (int j = 0; j < ag.nd[t].nv; ++j) {
+            double zj = ag.nd[t].z[j];
+            pobj += 0.5 * ag.nd[t].pdiag[j] * zj * zj + ag.nd[t].q[j] * zj;
+        }
+    obj_out = pobj;
+    iters_out = it;
+    return status;
+}
+
+}  // namespace
+
+extern "C" int oracle_qp_solve_batched(const scvx_qp_template* tpl, int N, const double* disc, const double* sigma,
+                                       const double* Xref, const double* Uref, const double* x_init,
+                                       const double* x_final, const double* tr, const double* coll_rows,
+                                       const int32_t* coll_count, double* X, double* U, double* slack_coll,
+                                       double* obj, int32_t* status, int32_t* iters, int nthreads) {
+    const int n = tpl->n_x, m = tpl->n_u, K = tpl->K, pd = tpl->pos_dim;
+    if (n <= 0 || m <= 0 || K < 2 || m > 4 || pd > 3) return -1;
+    const size_t stride = (size_t)(K - 1) * n * (n + 2 * m + 2);
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+    for (int a = 0; a < N; ++a) {
+        Agent ag;
+        const double* cr = tpl->j_max > 0 ? coll_rows + (size_t)a * K * tpl->j_max * (pd + 1) : nullptr;
+        const int32_t* cc = tpl->j_max > 0 ? coll_count + (size_t)a * K : nullptr;
+        setup_agent(ag, tpl, disc + a * stride, sigma[a], Xref + (size_t)a * K * n, Uref + (size_t)a * K * m,
+                    x_init + (size_t)a * n, tpl->has_final ? x_final + (size_t)a * n : nullptr, tr[a], cr, cc);
+        int it = 0;
+        double ob = 0.0;
+        status[a] = solve_agent(ag, it, ob);
+        iters[a] = it;
+        obj[a] = ob;
+        for (int t = 0; t < K; ++t) {
+            for (int i = 0; i < n; ++i) X[((size_t)a * K + t) * n + i] = ag.nd[t].z[i];
+            for (int j = 0; j < m; ++j) U[((size_t)a * K + t) * m + j] = ag.nd[t].z[n + j];
+            slack_coll[(size_t)a * K + t] = (tpl->j_max > 0 && ag.nd[t].na > 0) ? ag.nd[t].z[n + m + tpl->n_obs] : 0.0;
+        }
+    }
+    return 0;
+}
