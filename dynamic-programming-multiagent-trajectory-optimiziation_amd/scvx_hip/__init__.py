@@ -1,0 +1,204 @@
+"""scvx_hip -- MI355X-native batched SCvx inner loop (host side of libscvx_hip.so).
+
+Thin PyTorch-ROCm layer over the C-ABI in include/scvx_hip.h: tensors are device buffers,
+kernels run on torch's current HIP stream, nothing falls back to the CPU.
+
+    foh_batched            FirstOrderHold.calculate_discretization for N agents
+                           (SCvx/discretization/first_order_hold.py:52-87)
+    integrate_nonlinear    FirstOrderHold.integrate_nonlinear_piecewise / _full (:127-155)
+    collision_rows         linearized pairwise collision rows (Distributed_opt/dist_scvx_3d.py:93-107)
+    qp_solve_batched       the per-agent trust-region subproblem (dist_scvx_3d.py:51-111)
+    QPSpec                 problem template of qp_solve_batched
+"""
+import ctypes
+from dataclasses import dataclass, field
+from typing import Optional, Sequence, Tuple
+
+from . import _lib
+from ._lib import MODEL_DIMS, MODEL_IDS, STATUS, QPTemplate, ScvxError, check, lib
+
+# RK4 substeps per FOH interval.  1 is exact for the (linear) integrators; 16 keeps the
+# unicycle / quadrotor within 1e-7 of the reference's LSODA (tests/test_foh_oracle.py).
+DEFAULT_NSUB = {"di": 1, "si": 1, "unicycle": 16, "quad": 16}
+QUAD_PARAMS = (1.0, 9.81, 0.02, 0.02, 0.04)
+
+__all__ = ["foh_batched", "integrate_nonlinear", "collision_rows", "qp_solve_batched", "QPSpec",
+           "disc_stride", "unpack_disc", "ScvxError", "MODEL_DIMS", "DEFAULT_NSUB"]
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _stream(stream=None):
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _dev(t, dtype=None, name="tensor"):
+    torch = _torch()
+    dtype = dtype or torch.float64
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch tensor on the ROCm device")
+    if not t.is_cuda:
+        raise ScvxError(f"{name} must live on the GPU (the HIP path has no CPU fallback)")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def disc_stride(model):
+    n, m = MODEL_DIMS[model]
+    return n * (n + 2 * m + 2)
+
+
+def unpack_disc(disc, model):
+    """[..., K-1, n(n+2m+2)] -> (A_bar, B_bar, C_bar, S_bar, z_bar) in the reference's F-order
+    column layout (..., n*n, K-1) etc. (first_order_hold.py:20-24, 75-85)."""
+    n, m = MODEL_DIMS[model]
+    o = [0, n * n, n * n + n * m, n * n + 2 * n * m, n * n + 2 * n * m + n, n * n + 2 * n * m + 2 * n]
+    return tuple(disc[..., o[i]:o[i + 1]].transpose(-1, -2) for i in range(5))
+
+
+def _params(model, params):
+    torch = _torch()
+    if model != "quad":
+        return None, ctypes.c_void_p(0)
+    p = torch.tensor(params if params is not None else QUAD_PARAMS, dtype=torch.float64)
+    buf = (ctypes.c_double * 5)(*p.tolist())
+    return buf, ctypes.cast(buf, ctypes.c_void_p)
+
+
+def foh_batched(model, X, U, sigma, nsub=None, params=None, out=None, stream=None):
+    """X (N,K,n), U (N,K,m), sigma (N,) float64 device tensors -> disc (N,K-1,n(n+2m+2))."""
+    torch = _torch()
+    N, K, n = X.shape
+    m = U.shape[2]
+    if (n, m) != MODEL_DIMS[model]:
+        raise ValueError(f"{model}: expected n,m={MODEL_DIMS[model]}, got {(n, m)}")
+    if out is None:
+        out = torch.empty((N, K - 1, disc_stride(model)), dtype=torch.float64, device=X.device)
+    keep, pp = _params(model, params)
+    rc = lib().scvx_foh_batched(MODEL_IDS[model], pp, K, N, _dev(X, name="X"), _dev(U, name="U"),
+                                _dev(sigma, name="sigma"), int(nsub or DEFAULT_NSUB[model]),
+                                _dev(out, name="out"), _stream(stream))
+    check(rc, "scvx_foh_batched")
+    return out
+
+
+def integrate_nonlinear(model, X, U, sigma, piecewise, nsub=16, params=None, out=None, stream=None):
+    """Batched FirstOrderHold.integrate_nonlinear_piecewise (piecewise=True) / _full (False)."""
+    torch = _torch()
+    N, K, n = X.shape
+    if out is None:
+        out = torch.empty_like(X)
+    keep, pp = _params(model, params)
+    rc = lib().scvx_integrate_nonlinear_batched(MODEL_IDS[model], pp, K, N, _dev(X, name="X"), _dev(U, name="U"),
+                                                _dev(sigma, name="sigma"), int(nsub), int(bool(piecewise)),
+                                                _dev(out, name="out"), _stream(stream))
+    check(rc, "scvx_integrate_nonlinear_batched")
+    return out
+
+
+def collision_rows(X_all, i0, n_local, R, j_max, pos_dim=3, cull_radius=0.0, rows=None, count=None, stream=None):
+    """Rows (g, b) of dist_scvx_3d.py:93-107 for local agents [i0, i0+n_local) of X_all (N_total,K,n)."""
+    torch = _torch()
+    N_total, K, n = X_all.shape
+    if rows is None:
+        rows = torch.zeros((n_local, K, j_max, pos_dim + 1), dtype=torch.float64, device=X_all.device)
+    if count is None:
+        count = torch.zeros((n_local, K), dtype=torch.int32, device=X_all.device)
+    rc = lib().scvx_collision_rows_batched(K, pos_dim, n, N_total, _dev(X_all, name="X_all"), int(i0), int(n_local),
+                                           float(R), float(cull_radius), int(j_max), _dev(rows, name="rows"),
+                                           _dev(count, torch.int32, "count"), _stream(stream))
+    check(rc, "scvx_collision_rows_batched")
+    return rows, count
+
+
+@dataclass
+class QPSpec:
+    """Template of the batched trust-region subproblem (include/scvx_hip.h scvx_qp_template)."""
+    model: str = "di"
+    K: int = 50
+    pos_dim: int = 3
+    has_final: bool = True
+    fix_last_input: bool = True
+    ineq_last: bool = False
+    w_last: float = 0.0
+    box: Sequence[Tuple[int, float, float]] = ()
+    obs: Sequence[Tuple[Sequence[float], float]] = ()
+    w_obs: float = 1e6
+    j_max: int = 0
+    w_coll: float = 1e4
+    u_max: Optional[float] = None
+    max_iter: int = 60
+    tol: float = 1e-9
+
+    def to_c(self):
+        n, m = MODEL_DIMS[self.model]
+        t = QPTemplate()
+        t.model_id, t.n_x, t.n_u, t.K, t.pos_dim = MODEL_IDS[self.model], n, m, self.K, self.pos_dim
+        t.has_final, t.fix_last_input, t.ineq_last = int(self.has_final), int(self.fix_last_input), int(self.ineq_last)
+        t.w_last = self.w_last
+        if len(self.box) > _lib.SCVX_MAX_BOX or len(self.obs) > _lib.SCVX_MAX_OBS:
+            raise ValueError("too many box constraints / obstacles")
+        t.n_box = len(self.box)
+        for i, (bi, lo, hi) in enumerate(self.box):
+            t.box_idx[i], t.box_lo[i], t.box_hi[i] = int(bi), float(lo), float(hi)
+        t.n_obs = len(self.obs)
+        for o, (c, r) in enumerate(self.obs):
+            for i in range(len(c)):
+                t.obs_center[o][i] = float(c[i])
+            t.obs_radius[o] = float(r)
+        t.w_obs, t.j_max, t.w_coll = float(self.w_obs), int(self.j_max), float(self.w_coll)
+        t.has_soc = int(self.u_max is not None)
+        t.u_max = 0.0 if self.u_max is None else float(self.u_max)
+        t.max_iter, t.tol = int(self.max_iter), float(self.tol)
+        return t
+
+
+class QPSolver:
+    """Reusable batched solver: holds the C template and a device workspace for N agents."""
+
+    def __init__(self, spec: QPSpec, N: int, device="cuda"):
+        torch = _torch()
+        self.spec, self.N = spec, N
+        self.ctpl = spec.to_c()
+        nbytes = lib().scvx_qp_workspace_bytes(ctypes.byref(self.ctpl), N)
+        self.workspace = torch.empty(max(nbytes // 8, 1), dtype=torch.float64, device=device)
+        n, m = MODEL_DIMS[spec.model]
+        K = spec.K
+        self.X = torch.empty((N, K, n), dtype=torch.float64, device=device)
+        self.U = torch.empty((N, K, m), dtype=torch.float64, device=device)
+        self.slack = torch.empty((N, K), dtype=torch.float64, device=device)
+        self.obj = torch.empty(N, dtype=torch.float64, device=device)
+        self.status = torch.empty(N, dtype=torch.int32, device=device)
+        self.iters = torch.empty(N, dtype=torch.int32, device=device)
+        self._dummy = torch.zeros(1, dtype=torch.float64, device=device)
+        self._dummy_i = torch.zeros(1, dtype=torch.int32, device=device)
+
+    def solve(self, disc, sigma, Xref, Uref, x_init, x_final, tr, coll_rows=None, coll_count=None, stream=None):
+        torch = _torch()
+        if coll_rows is None:
+            coll_rows, coll_count = self._dummy, self._dummy_i
+        xf = x_final if x_final is not None else self._dummy
+        rc = lib().scvx_qp_solve_batched(
+            ctypes.byref(self.ctpl), self.N, _dev(disc, name="disc"), _dev(sigma, name="sigma"),
+            _dev(Xref, name="Xref"), _dev(Uref, name="Uref"), _dev(x_init, name="x_init"), _dev(xf, name="x_final"),
+            _dev(tr, name="tr"), _dev(coll_rows, name="coll_rows"), _dev(coll_count, torch.int32, "coll_count"),
+            _dev(self.X), _dev(self.U), _dev(self.slack), _dev(self.obj), _dev(self.status, torch.int32),
+            _dev(self.iters, torch.int32), _dev(self.workspace), ctypes.c_size_t(self.workspace.numel() * 8),
+            _stream(stream))
+        check(rc, "scvx_qp_solve_batched")
+        return dict(X=self.X, U=self.U, slack_coll=self.slack, obj=self.obj, status=self.status, iters=self.iters)
+
+
+def qp_solve_batched(spec: QPSpec, disc, sigma, Xref, Uref, x_init, x_final, tr, coll_rows=None, coll_count=None):
+    """One-shot batched solve (allocates a QPSolver); returns dict of device tensors (copies)."""
+    s = QPSolver(spec, Xref.shape[0], device=Xref.device)
+    out = s.solve(disc, sigma, Xref, Uref, x_init, x_final, tr, coll_rows, coll_count)
+    return {k: v.clone() for k, v in out.items()}

@@ -1,0 +1,72 @@
+"""ctypes binding of libscvx_hip.so (include/scvx_hip.h).
+
+The library is the product: there is no CPU fallback.  Importing works without a GPU (so the
+C-ABI can be checked on a build host); compute calls need a ROCm device and raise otherwise.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libscvx_hip.so")
+
+SCVX_MAX_BOX, SCVX_MAX_OBS = 4, 16
+MODEL_IDS = {"di": 0, "unicycle": 1, "si": 2, "quad": 3}
+MODEL_DIMS = {"di": (6, 3), "unicycle": (3, 2), "si": (3, 3), "quad": (12, 4)}
+STATUS = {0: "optimal", 1: "optimal_inaccurate", 2: "solver_error"}
+
+# every symbol declared in include/scvx_hip.h
+EXPORTS = ("scvx_version", "scvx_last_error", "scvx_foh_batched", "scvx_integrate_nonlinear_batched",
+           "scvx_qp_solve_batched", "scvx_qp_workspace_bytes", "scvx_qp_set_trace",
+           "scvx_collision_rows_batched")
+
+
+class ScvxError(RuntimeError):
+    pass
+
+
+class QPTemplate(ctypes.Structure):
+    """Mirror of scvx_qp_template (include/scvx_hip.h)."""
+    _fields_ = [
+        ("model_id", ctypes.c_int32), ("n_x", ctypes.c_int32), ("n_u", ctypes.c_int32), ("K", ctypes.c_int32),
+        ("pos_dim", ctypes.c_int32), ("has_final", ctypes.c_int32), ("fix_last_input", ctypes.c_int32),
+        ("ineq_last", ctypes.c_int32), ("w_last", ctypes.c_double), ("n_box", ctypes.c_int32),
+        ("box_idx", ctypes.c_int32 * SCVX_MAX_BOX), ("box_lo", ctypes.c_double * SCVX_MAX_BOX),
+        ("box_hi", ctypes.c_double * SCVX_MAX_BOX), ("n_obs", ctypes.c_int32),
+        ("obs_center", (ctypes.c_double * 3) * SCVX_MAX_OBS), ("obs_radius", ctypes.c_double * SCVX_MAX_OBS),
+        ("w_obs", ctypes.c_double), ("j_max", ctypes.c_int32), ("w_coll", ctypes.c_double),
+        ("has_soc", ctypes.c_int32), ("u_max", ctypes.c_double), ("max_iter", ctypes.c_int32),
+        ("tol", ctypes.c_double),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    """Load libscvx_hip.so once; raise loudly if it was not built (no fallback path exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run `make -C {os.path.dirname(HERE)}` "
+                              "or __graft_entry__.build()")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i32, dbl, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_size_t
+        L.scvx_version.restype = i32
+        L.scvx_last_error.restype = ctypes.c_char_p
+        L.scvx_foh_batched.argtypes = [i32, vp, i32, i32, vp, vp, vp, i32, vp, vp]
+        L.scvx_integrate_nonlinear_batched.argtypes = [i32, vp, i32, i32, vp, vp, vp, i32, i32, vp, vp]
+        L.scvx_qp_workspace_bytes.argtypes = [ctypes.POINTER(QPTemplate), i32]
+        L.scvx_qp_workspace_bytes.restype = sz
+        L.scvx_qp_solve_batched.argtypes = [ctypes.POINTER(QPTemplate), i32] + [vp] * 15 + [vp, sz, vp]
+        L.scvx_qp_set_trace.argtypes = [vp, i32, i32]
+        L.scvx_collision_rows_batched.argtypes = [i32, i32, i32, i32, vp, i32, i32, dbl, dbl, vp, vp, vp]
+        for fn in EXPORTS:
+            getattr(L, fn).restype = getattr(L, fn).restype if fn in ("scvx_last_error", "scvx_qp_workspace_bytes") else i32
+        _lib = L
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().scvx_last_error().decode(errors="replace")
+        raise ScvxError(f"{what} failed (code {rc}): {msg}")

@@ -121,12 +121,34 @@ typedef struct scvx_qp_template {
  * Outputs (device):
  *   X [N][K][n], U [N][K][m], slack_coll [N][K] (S_t, zeros if j_max = 0), obj [N],
  *   status [N], iters [N]
+ * workspace: caller-owned device scratch of at least scvx_qp_workspace_bytes(tpl, N) bytes.
+ * Limits: 2 <= K <= 64 (one node per lane), n_u <= 4, <= 64 inequality rows per node.
  */
 int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const double* disc, const double* sigma,
                           const double* Xref, const double* Uref, const double* x_init, const double* x_final,
                           const double* tr, const double* coll_rows, const int32_t* coll_count, double* X,
                           double* U, double* slack_coll, double* obj, int32_t* status, int32_t* iters,
-                          void* stream);
+                          void* workspace, size_t workspace_bytes, void* stream);
+
+/* Bytes of caller-owned device scratch scvx_qp_solve_batched needs for N agents. */
+size_t scvx_qp_workspace_bytes(const scvx_qp_template* tpl, int N);
+
+/* Diagnostics hook: later solves write 8 doubles per IPM iteration of agent `agent`
+ * (pres, dres, gap, pobj, alpha_aff, alpha, sigma, mu) into device buffer `buf` (cap iterations).
+ * buf = NULL disables.  Not needed for normal use. */
+int scvx_qp_set_trace(double* buf, int agent, int cap);
+
+/*
+ * Pairwise collision linearization for the Jacobi coupling (Distributed_opt/dist_scvx_3d.py:93-107):
+ * for local agents i0..i0+N_local-1 of the all-gathered states X_all [N_total][K][n_x] and nodes
+ * t < K-1, rows (g, b) with g = (p_i - p_j)/|p_i - p_j|, b = 2R - |p_i - p_j| + g' p_i, i.e.
+ * b - g' p_t <= S_t.  cull_radius <= 0 keeps every neighbour; otherwise only |p_i - p_j| < cull_radius.
+ * At most j_max rows per node (largest 2R - |.| kept).  rows [N_local][K][j_max][pos_dim+1],
+ * count [N_local][K].
+ */
+int scvx_collision_rows_batched(int K, int pos_dim, int n_x, int N_total, const double* X_all, int i0,
+                                int N_local, double R, double cull_radius, int j_max, double* rows,
+                                int32_t* count, void* stream);
 
 #ifdef __cplusplus
 }

@@ -923,6 +923,12 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
             std::vector<Vec> dz, ds, dl, dsq, dlq;
             Vec dy, dyi, dyf;
             if (!newton(rco, rcq, dz, ds, dl, dsq, dlq, dy, dyi, dyf)) { status = SCVX_STATUS_NUMERICAL; break; }
+            if (it == 0 && std::getenv("SCVX_DUMP")) {
+                FILE* fp = std::fopen(std::getenv("SCVX_DUMP"), "wb");
+                for (int t = 0; t < K; ++t) { double buf[40] = {0}; for (int j = 0; j < ag.nd[t].nv && j < 40; ++j) buf[j] = dz[t][j]; std::fwrite(buf, sizeof(double), 40, fp); }
+                std::fwrite(dyi.data(), sizeof(double), n, fp);
+                std::fclose(fp);
+            }
             double aa = std::min(1.0, max_step(ds, dl, dsq, dlq));
             double gap_a = 0.0;
             for (int t = 0; t < K; ++t) {

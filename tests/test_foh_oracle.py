@@ -1,0 +1,52 @@
+"""CPU: the C FOH restatement (oracle/foh_ref.c) against golden vectors produced by the reference
+FirstOrderHold (tests/golden/make_foh_goldens.py; first_order_hold.py:52-155, LSODA)."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from oracle import foh_oracle
+
+GOLD = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "foh_*.npz")))
+NSUB = {"di": 1, "si": 1, "unicycle": 16, "quad": 16}
+
+
+def rel(a, b):
+    return np.max(np.abs(a - b)) / max(1.0, np.max(np.abs(b)))
+
+
+@pytest.mark.parametrize("path", GOLD, ids=[os.path.basename(p) for p in GOLD])
+def test_oracle_foh_matches_reference_goldens(path):
+    d = np.load(path)
+    model = str(d["model"])
+    outs = foh_oracle.foh(model, d["X"], d["U"], float(d["sigma"]), nsub=NSUB[model])
+    for name, o in zip(["A_bar", "B_bar", "C_bar", "S_bar", "z_bar"], outs):
+        assert o.shape == d[name].shape  # (n*n, K-1), ... as test_disc.py:22-26
+        # tolerance: LSODA (rtol=atol=1.49e-8) is itself only ~1e-8 accurate
+        assert rel(o, d[name]) < 1e-7, name
+
+
+@pytest.mark.parametrize("path", GOLD, ids=[os.path.basename(p) for p in GOLD])
+def test_oracle_nonlinear_rollouts(path):
+    d = np.load(path)
+    model = str(d["model"])
+    pw = foh_oracle.integrate_nonlinear(model, d["X"], d["U"], float(d["sigma_nl"]), True, nsub=16)
+    full = foh_oracle.integrate_nonlinear(model, d["X"], d["U"], float(d["sigma_nl"]), False, nsub=16)
+    assert rel(pw, d["X_piecewise"]) < 1e-7
+    assert rel(full, d["X_full"]) < 1e-6
+
+
+def test_double_integrator_foh_is_exact_zoh_sum():
+    """For the DI, Phi = expm(A sigma dt) and B_k + C_k = ZOH Bd."""
+    K, sigma = 51, 30.0
+    rng = np.random.default_rng(0)
+    X, U = rng.normal(size=(6, K)), rng.normal(size=(3, K))
+    A, B, C, S, z = foh_oracle.foh("di", X, U, sigma)
+    h = sigma / (K - 1)
+    Ad = np.eye(6); Ad[0:3, 3:6] = h * np.eye(3)
+    Bd = np.zeros((6, 3)); Bd[0:3] = 0.5 * h * h * np.eye(3); Bd[3:6] = h * np.eye(3)
+    for k in range(K - 1):
+        np.testing.assert_allclose(A[:, k].reshape(6, 6, order="F"), Ad, atol=1e-13)
+        np.testing.assert_allclose((B[:, k] + C[:, k]).reshape(6, 3, order="F"), Bd, atol=1e-13)
+    np.testing.assert_allclose(S * sigma + z, 0.0, atol=1e-12)

@@ -1,0 +1,117 @@
+"""GPU parity: the HIP batched trust-region solve (scvx_qp_solve_batched through the C-ABI)
+against the dense reference-formulation oracle (oracle/qp_dense.py: dist_scvx_3d.py:51-111 as
+written, generic dense IPM + KKT certificate) and the CPU restatement (oracle/scvx_cpu.cpp).
+
+Tolerances (float64): trajectories 1e-6 absolute, objective 1e-8 relative, feasibility 1e-8."""
+import numpy as np
+import pytest
+
+import scvx_hip
+from oracle import foh_oracle, problems as pb, qp_cpu, qp_dense as qd
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(x, cuda, dtype=None):
+    import torch
+    return torch.tensor(np.ascontiguousarray(x), device=cuda, dtype=dtype or torch.float64)
+
+
+def test_dist_scvx_3d_first_iteration_matches_dense_oracle(cuda):
+    sc = pb.dist3_scenario()
+    T = sc["T"]
+    A = np.repeat(sc["Ad"][None], T - 1, 0)
+    B = np.repeat(sc["Bd"][None], T - 1, 0)
+    disc = np.stack([pb.pack_disc(A, B)] * 3)
+    Xref = np.stack([x[:, 0:6] for x in sc["X_traj"]])
+    Uref = np.stack([x[:, 6:9] for x in sc["X_traj"]])
+    xdes = np.stack([x[0:6] for x in sc["x_des"]])
+    J = 2
+    rows = np.zeros((3, T, J, 4))
+    cnt = np.zeros((3, T), np.int32)
+    dense_rows = [pb.collision_rows(sc["X_traj"], i, sc["R"]) for i in range(3)]
+    for i in range(3):
+        for t in range(T - 1):
+            rows[i, t] = dense_rows[i][t]
+            cnt[i, t] = 2
+    box = [(0, -1, 22), (1, -1, 20)]
+    spec = scvx_hip.QPSpec(model="di", K=T, box=box, j_max=J, w_coll=1e4, tol=1e-10, max_iter=80)
+    import torch
+    out = scvx_hip.qp_solve_batched(spec, _t(disc, cuda), _t(np.zeros(3), cuda), _t(Xref, cuda), _t(Uref, cuda),
+                                    _t(Xref[:, 0], cuda), _t(xdes, cuda), _t(np.full(3, sc["tr"]), cuda),
+                                    _t(rows, cuda), _t(cnt, cuda, torch.int32))
+    st = out["status"].cpu().numpy()
+    assert (st == 0).all(), st
+    for i in range(3):
+        prob = pb.dense_prob_from_rows(A, B, Xref[i], Uref[i], xdes[i], sc["tr"], dense_rows[i], box=box,
+                                       w_coll=1e4, fix_last_input=True)
+        Xd, Ud, objd, info = qd.solve_agent(prob, tol=1e-11, maxit=120)
+        assert info["status"] == "optimal"
+        X = out["X"][i].cpu().numpy()
+        U = out["U"][i].cpu().numpy()
+        S = out["slack_coll"][i].cpu().numpy()
+        viol = qd.constraint_violation(prob, X, U, S)
+        assert max(viol.values()) < 1e-8, viol
+        obj = out["obj"][i].item()
+        assert abs(obj - objd) <= 1e-8 * max(1.0, abs(objd))
+        if objd < 1e3:  # slack-free agents: the quadratic part pins the trajectory
+            assert np.abs(X - Xd).max() < 1e-6
+            assert np.abs(U - Ud).max() < 1e-6
+
+
+@pytest.mark.parametrize("umax,nobs", [(None, 0), (1.0, 8), (0.12, 8)])
+def test_c3_family_matches_cpu_and_dense(cuda, umax, nobs):
+    N, K = 12, 50
+    sc = pb.synthetic_di(N, K=K, seed=1, obstacles=nobs)
+    import torch
+    X, U, sig = _t(sc["X"], cuda), _t(sc["U"], cuda), _t(sc["sigma"], cuda)
+    disc = scvx_hip.foh_batched("di", X, U, sig)
+    box = [(0, -12, 12), (1, -12, 12)]
+    spec = scvx_hip.QPSpec(model="di", K=K, box=box, obs=sc["obs"], w_obs=1e6, u_max=umax, tol=1e-10, max_iter=80)
+    tr = np.full(N, 0.25)
+    out = scvx_hip.qp_solve_batched(spec, disc, sig, X, U, _t(sc["x_init"], cuda), _t(sc["x_final"], cuda), _t(tr, cuda))
+    tpl = qp_cpu.make_template(6, 3, K, box=box, obs=sc["obs"], w_obs=1e6, u_max=umax, tol=1e-10, max_iter=80)
+    dn = disc.cpu().numpy()
+    cpu = qp_cpu.solve_batched(tpl, dn, sc["sigma"], sc["X"], sc["U"], sc["x_init"], sc["x_final"], tr)
+    st = out["status"].cpu().numpy()
+    ok = cpu["status"] == 0
+    assert ok.sum() >= N // 2
+    assert (st[ok] == 0).all()
+    Xg, Ug, og = out["X"].cpu().numpy(), out["U"].cpu().numpy(), out["obj"].cpu().numpy()
+    for a in np.nonzero(ok)[0]:
+        assert abs(og[a] - cpu["obj"][a]) <= 1e-8 * max(1.0, abs(cpu["obj"][a]))
+        assert np.abs(Xg[a] - cpu["X"][a]).max() < 1e-6
+        assert np.abs(Ug[a] - cpu["U"][a]).max() < 1e-6
+    compared = 0
+    for a in np.nonzero(ok)[0][:4]:
+        if compared == 2:
+            break
+        A, B, C, S, z = pb.unpack_disc(dn[a], 6, 3)
+        prob = dict(A=A, B=B, C=C, c=S * sc["sigma"][a] + z, Xref=sc["X"][a], Uref=sc["U"][a],
+                    x_final=sc["x_final"][a], tr=0.25, box=box, obs=sc["obs"], w_obs=1e6, umax=umax,
+                    fix_last_input=True)
+        with np.errstate(all="ignore"):
+            Xd, Ud, objd, info = qd.solve_agent(prob, tol=1e-11, maxit=120)
+        if info["status"] != "optimal":  # the dense checker itself failed on this agent
+            continue
+        compared += 1
+        assert abs(og[a] - objd) <= 1e-7 * max(1.0, abs(objd))
+        viol = qd.constraint_violation(prob, Xg[a], Ug[a])
+        assert max(viol.values()) < 1e-7, viol
+    assert compared >= 1
+
+
+def test_collision_rows_match_reference_formula(cuda):
+    rng = np.random.default_rng(3)
+    N, K = 9, 20
+    Xall = rng.normal(0, 3.0, (N, K, 6))
+    rows, cnt = scvx_hip.collision_rows(_t(Xall, cuda), 2, 4, 2.3, j_max=N - 1)
+    rows, cnt = rows.cpu().numpy(), cnt.cpu().numpy()
+    trajs = [Xall[i] for i in range(N)]
+    for a in range(4):
+        ref = pb.collision_rows(trajs, 2 + a, 2.3)
+        for t in range(K - 1):
+            assert cnt[a, t] == N - 1
+            got = rows[a, t, :cnt[a, t]]
+            np.testing.assert_allclose(got[np.lexsort(got.T)], ref[t][np.lexsort(ref[t].T)], rtol=1e-13, atol=1e-13)
+        assert cnt[a, K - 1] == 0
