@@ -1,0 +1,190 @@
+"""Benchmark: SCvx-iterations/sec of the batched SCvx inner loop on MI355X.
+
+Workload (BASELINE.json metric, config C3 of SURVEY §8(d)): per GPU, N=1024 agents, 3-D double
+integrator (n=6, m=3), K=50 nodes, sigma=30 s (h=0.6 s as Distributed_opt/dist_scvx_3d.py:200-204),
+trust region 0.25 (:207), 8 static spherical obstacles as linearized soft halfspaces
+(single_integrator_model.py:113-126 semantics, weight 1e6), per-node SOC ||u_t|| <= 1.0
+(:103-104 semantics), box |x|,|y| <= 12 (dist_scvx_3d.py:87-90 widened), straight-line warm start.
+
+One SCvx iteration (= one "step") = batched FOH discretization (scvx_foh_batched) + batched
+trust-region QP/SOCP solve to tolerance (scvx_qp_solve_batched) + trust-region bookkeeping, all
+on device; inputs resident in HBM.  Multi-GPU (--gpus N under torch.distributed.run): weak scaling,
+each rank owns its own 1024 agents (C3 has no inter-agent coupling, so there is no data-path
+collective); `value` counts the N_gpus * 1024-agent SCvx iterations completed per second.
+
+Also reported: roofline of the dominant kernel (qp_ipm_kernel, FP64 FLOP rate vs the FP64 peak,
+timed with HIP events on the launch stream) and a CPU baseline (the C++ restatement of the same
+algorithm, oracle/scvx_cpu.cpp + oracle/foh_ref.c, on a bounded agent sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "dynamic-programming-multiagent-trajectory-optimiziation_amd"))
+sys.path.insert(0, REPO)
+
+N_AGENTS = 1024
+K = 50
+SIGMA = 30.0
+TR0 = 0.25
+U_MAX = 1.0
+N_OBS = 8
+BOX = [(0, -12.0, 12.0), (1, -12.0, 12.0)]
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) dense peak, spec
+HBM_PEAK_GBS = 8000.0
+
+
+def qp_flops_per_ipm_iter(n, m, K, rows):
+    """Algorithmic FP64 FLOPs of one IPM iteration of one agent:
+    Riccati factor (with terminal sensitivities) + 2 solves + node-local work."""
+    factor = 2 * (3 * n ** 3 + 5 * n * n * m + 3 * n * m * m + m ** 3 / 3)
+    solve = 2 * (6 * n * n + 7 * n * m + 2 * m * m)
+    node = 2 * (8 * 12 * rows + n * n * m + n * m * m)
+    return K * (factor + 2 * solve + node)
+
+
+def make_workload(N, seed, device):
+    import torch
+    from oracle import problems as pb
+    sc = pb.synthetic_di(N, K=K, seed=seed, sigma=SIGMA, obstacles=N_OBS)
+    t = {k: torch.tensor(sc[k], device=device) for k in ("X", "U", "x_init", "x_final", "sigma")}
+    return sc, t
+
+
+def cpu_baseline(sc, n_sample, threads):
+    """Time the CPU restatement (oracle) on n_sample agents: FOH + QP for one SCvx iteration."""
+    import numpy as np
+    from oracle import foh_oracle, qp_cpu
+    tpl = qp_cpu.make_template(6, 3, K, box=BOX, obs=sc["obs"], w_obs=1e6, u_max=U_MAX, tol=1e-9, max_iter=60)
+    t0 = time.perf_counter()
+    disc = np.zeros((n_sample, K - 1, 6 * (6 + 6 + 2)))
+    for a in range(n_sample):
+        outs = foh_oracle.foh("di", sc["X"][a].T, sc["U"][a].T, sc["sigma"][a])
+        disc[a] = np.hstack([o.T for o in outs])
+    qp_cpu.solve_batched(tpl, disc, sc["sigma"][:n_sample], sc["X"][:n_sample], sc["U"][:n_sample],
+                         sc["x_init"][:n_sample], sc["x_final"][:n_sample], np.full(n_sample, TR0),
+                         nthreads=threads)
+    el = time.perf_counter() - t0
+    return dict(value=(n_sample / N_AGENTS) / el, unit="SCvx-iterations/s (N=1024-agent equivalent)",
+                cores=threads, kind="port",
+                sample=f"{n_sample} of the {N_AGENTS} agents, one SCvx iteration (FOH C + structured IPM C++), "
+                       f"{el:.2f} s wall, -O3 x86-64-v3, OpenMP over agents")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--agents", type=int, default=N_AGENTS)
+    ap.add_argument("--cpu-sample", type=int, default=1024)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import scvx_hip
+    from scvx_hip.scvx import JacobiSCvx
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    N = args.agents
+    sc, w = make_workload(N, seed=1 + rank, device=device)
+    spec = scvx_hip.QPSpec(model="di", K=K, box=BOX, obs=sc["obs"], w_obs=1e6, u_max=U_MAX, tol=1e-9, max_iter=60)
+    drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, tr_rule="per_agent")
+    X, U = w["X"].clone(), w["U"].clone()
+
+    stream = torch.cuda.current_stream()
+    iters_total = 0
+
+    def step(X, U):
+        Xn, Un, out = drv.step(X, U)
+        X.copy_(Xn)
+        U.copy_(Un)
+        return out
+
+    for _ in range(args.warmup):
+        step(X, U)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    # timed region: K steps; QP kernel bracketed by HIP events on the launch stream
+    qp_ms = []
+    iters = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        drv.disc = scvx_hip.foh_batched("di", X, U, w["sigma"], out=drv.disc)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        out = drv.solver.solve(drv.disc, w["sigma"], X, U, w["x_init"], w["x_final"], drv.tr)
+        e1.record(stream)
+        cost = (out["U"][:, :-1, :] ** 2).sum(dim=(1, 2))
+        shrink = (cost > drv.prev_cost).to(torch.float64)
+        drv.tr.mul_(1.0 - 0.5 * shrink)
+        drv.prev_cost.copy_(cost)
+        X.copy_(out["X"])
+        U.copy_(out["U"])
+        qp_ms.append((e0, e1))
+        iters.append(out["iters"].sum())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    el_t = torch.tensor([el], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    el = el_t.item()
+    qp_avg_ms = sum(a.elapsed_time(b) for a, b in qp_ms) / len(qp_ms)
+    ipm_iters = float(torch.stack(iters).sum().item())
+    status = out["status"].cpu()
+    rows = (1 << 3) + 2 * len(BOX) + 2 * N_OBS
+    flops = qp_flops_per_ipm_iter(6, 3, K, rows) * ipm_iters / args.steps
+    achieved = flops / (qp_avg_ms * 1e-3) / 1e12
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu:
+            cpu = cpu_baseline(sc, min(args.cpu_sample, N), threads=min(16, os.cpu_count() or 1))
+        value = world * args.steps / el
+        line = {
+            "metric": "SCvx-iterations/sec, N agents x K=50 nodes (N=1024 per GPU)",
+            "value": value,
+            "unit": "SCvx-iterations/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * el / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (C3 construction, SURVEY §8d: seeded random starts/goals, 8 spheres)",
+            "config": {"workload": "C3: N=1024 agents/GPU, 3-D double integrator n=6 m=3, K=50, FOH sigma=30, "
+                                   "tr=0.25, 8 obstacles (soft), SOC ||u||<=1, box |x|,|y|<=12",
+                       "agents_per_gpu": N, "K": K, "parallelism": f"agents sharded x{world}"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                         "kernel": "qp_ipm_kernel", "kernel_ms": qp_avg_ms,
+                         "note": "FP64 VALU-bound small dense linear algebra; peak = FP64 dense peak; "
+                                 "algorithmic FLOPs per DESIGN.md §4 x executed IPM iterations"},
+            "ipm_iters_per_agent": ipm_iters / (args.steps * N),
+            "status_counts": {str(k): int((status == k).sum()) for k in (0, 1, 2)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

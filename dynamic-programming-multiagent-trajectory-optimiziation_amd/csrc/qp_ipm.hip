@@ -144,6 +144,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     __shared__ int spiv[NX];
     __shared__ double sz[WAVE][NZ], sy[WAVE][NX], sdz[WAVE][NZ], sdy[WAVE][NX];
     __shared__ double syi[NX], syf[NX], sdyi[NX], sdyf[NX], sflag[4];
+    __shared__ double sRing[3 * (StageLayout<NX, NU>::size + NX * NX + NX * NU)];
 
     // ------------------------------------------------------------------ node constants
     double xb[NX], ub[NU], Cp[NX * NU];  // reference point, C_{t-1} (column-major as disc)
@@ -158,7 +159,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 
     // soft rows (g, b): obstacle linearisations (single_integrator_model.py:113-126), then the
     // collision rows of dist_scvx_3d.py:93-107 supplied by the caller
-    auto softp = [&](int q, int i) -> double& { return soft[((long long)q * (pd + 1) + i) * WAVE + lane]; };
+    auto softp = [&](int q, int i) __attribute__((always_inline)) -> double& { return soft[((long long)q * (pd + 1) + i) * WAVE + lane]; };
     if (ineq) {
         for (int o = 0; o < T.n_obs; ++o) {
             double d[3] = {0, 0, 0}, nr = 0.0, bo = T.obs_radius[o];
@@ -172,14 +173,15 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             for (int i = 0; i <= pd; ++i) softp(T.n_obs + j, i) = src[i];
         }
     }
-    auto soft_row = [&](int q, double* g, double& b) {
+    auto soft_row = [&](int q, double* g, double& b) __attribute__((always_inline)) {
+#pragma unroll
         for (int i = 0; i < 3; ++i) g[i] = (i < pd) ? softp(q, i) : 0.0;
         b = softp(q, pd);
     };
-    auto group_of = [&](int q) { return q < T.n_obs ? q : T.n_obs; };
+    auto group_of = [&](int q) __attribute__((always_inline)) { return q < T.n_obs ? q : T.n_obs; };
 
     // G_r [z; aux] and h_r of orthant row r at this node (aux: a group column pointer)
-    auto row_eval = [&](int r, const double* z, const double* auxc, double& gz, double& h) {
+    auto row_eval = [&](int r, const double* z, const double* auxc, double& gz, double& h) __attribute__((always_inline)) {
         if (r < NTR) {
             gz = 0.0; h = trv;
 #pragma unroll
@@ -204,7 +206,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
     };
     // gzv += c * G_r'|_z ; gav column += c * G_r'|_aux
-    auto row_accT = [&](int r, double c, double* gzv, double* gav) {
+    auto row_accT = [&](int r, double c, double* gzv, double* gav) __attribute__((always_inline)) {
         if (r < NTR) {
 #pragma unroll
             for (int j = 0; j < NU; ++j) gzv[NX + j] += (((r >> j) & 1) ? -c : c);
@@ -243,22 +245,52 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     double W[NQ * NQ], Wi[NQ * NQ], ltq[NQ];  // SOC NT scaling, scaled point
 
     // ---------------------------------------------------------------- Riccati machinery
-    auto ld_stage_dyn = [&](int ts) {  // A_ts, Bt_ts into LDS (row-major)
-        const double* d = disc + (long long)ts * DSTR;
-        for (int e = lane; e < NX * NX; e += WAVE) { const int i = e / NX, j = e % NX; sA[e] = d[j * NX + i]; }
-        for (int e = lane; e < NX * NU; e += WAVE) sBt[e] = stage[(long long)ts * SL::size + SL::Bt + e];
+    // Stage packets: [stage block (SL) | A_t (disc, col-major) | C_{t-1} (disc, col-major)], streamed
+    // from the agent workspace into a 3-slot LDS ring one stage ahead of the sweep, so the
+    // sequential chain only ever waits on LDS (the global loads of stage t-+1 fly during stage t).
+    constexpr int PKT = SL::size + NX * NX + NX * NU;
+    constexpr int PFN = (PKT + WAVE - 1) / WAVE;
+    constexpr int OA = SL::size, OC = SL::size + NX * NX;
+    auto slot = [&](int ts) __attribute__((always_inline)) -> double* { return sRing + (ts % 3) * PKT; };
+    auto pf_issue = [&](int ts, double* r) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < PFN; ++k) {
+            const int e = lane + WAVE * k;
+            double v = 0.0;
+            if (e < SL::size) v = stage[(long long)ts * SL::size + e];
+            else if (e < OC) v = (ts < K - 1) ? disc[(long long)ts * DSTR + (e - OA)] : 0.0;
+            else if (e < PKT) v = (ts > 0) ? disc[(long long)(ts - 1) * DSTR + NX * NX + NX * NU + (e - OC)] : 0.0;
+            r[k] = v;
+        }
+    };
+    auto pf_commit = [&](int ts, const double* r) __attribute__((always_inline)) {
+        double* d = slot(ts);
+#pragma unroll
+        for (int k = 0; k < PFN; ++k) {
+            const int e = lane + WAVE * k;
+            if (e < PKT) d[e] = r[k];
+        }
+    };
+    auto ld_stage_dyn = [&](const double* pk) __attribute__((always_inline)) {  // A_t, Bt_t into LDS (row-major)
+        for (int e = lane; e < NX * NX; e += WAVE) { const int i = e / NX, j = e % NX; sA[e] = pk[OA + j * NX + i]; }
+        for (int e = lane; e < NX * NU; e += WAVE) sBt[e] = pk[SL::Bt + e];
     };
     // factor: node Hessians (Q,S,R) of all stages already in the stage buffers
-    auto factor = [&]() -> bool {
+    auto factor = [&]() __attribute__((always_inline)) -> bool {
+        double pf[PFN];
         for (int e = lane; e < NX * NX; e += WAVE) { sM[e] = 0.0; sPp[e] = 0.0; sPip[e] = 0.0; }
         if (lane == 0) sflag[0] = 0.0;
+        pf_issue(K - 1, pf);
+        pf_commit(K - 1, pf);
         __syncthreads();
         for (int ts = K - 1; ts >= 0; --ts) {
-            double* st = stage + (long long)ts * SL::size;
-            for (int e = lane; e < NX * NX; e += WAVE) sQ[e] = st[SL::Q + e];
-            for (int e = lane; e < NX * NU; e += WAVE) sS[e] = st[SL::S + e];
-            for (int e = lane; e < NU * NU; e += WAVE) sR[e] = st[SL::R + e];
-            if (ts < K - 1) ld_stage_dyn(ts);
+            if (ts > 0) pf_issue(ts - 1, pf);
+            const double* pk = slot(ts);
+            double* stg = stage + (long long)ts * SL::size;  // global outputs
+            for (int e = lane; e < NX * NX; e += WAVE) sQ[e] = pk[SL::Q + e];
+            for (int e = lane; e < NX * NU; e += WAVE) sS[e] = pk[SL::S + e];
+            for (int e = lane; e < NU * NU; e += WAVE) sR[e] = pk[SL::R + e];
+            if (ts < K - 1) ld_stage_dyn(pk);
             __syncthreads();
             if (ts < K - 1) {
                 mm<NX, NX, NX, false, false>(sT1, sPp, sA, nullptr, 1.0, lane);    // P'A
@@ -279,7 +311,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                     const int i = e / NX, j = e % NX;
                     sSh[e] = sS[j * NU + i];
                     // W2 at the last stage = C_{K-2}' (so that M += W2' kappa gives C_{K-2} kappa_{K-1})
-                    sW2[e] = (K >= 2) ? disc[(long long)(K - 2) * DSTR + NX * NX + NX * NU + i * NX + j] : 0.0;
+                    sW2[e] = (K >= 2) ? pk[OC + i * NX + j] : 0.0;
                 }
                 for (int e = lane; e < NU * NU; e += WAVE) sRh[e] = sR[e];
             }
@@ -328,10 +360,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                 for (int i = 0; i < NU; ++i) sKk[i * 2 * NX + c] = -col[i];
             }
+            __syncthreads();
             if (fx) {
                 for (int e = lane; e < NU * NX; e += WAVE) sSh[e] = 0.0;
+                __syncthreads();
             }
-            __syncthreads();
             // P = Qh + Sh' K ; Pi = W1 + Sh' kappa ; M += W2' kappa
             for (int e = lane; e < NX * NX; e += WAVE) {
                 const int i = e / NX, j = e % NX;
@@ -352,16 +385,17 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 const double p = 0.5 * (sT1[i * NX + j] + sT1[j * NX + i]);
                 sPp[e] = p;
                 sPip[e] = sW1[e];
-                st[SL::P + e] = p;
-                st[SL::Pi + e] = sW1[e];
+                stg[SL::P + e] = p;
+                stg[SL::Pi + e] = sW1[e];
             }
             for (int e = lane; e < NU * NX; e += WAVE) {
                 const int i = e / NX, j = e % NX;
-                st[SL::Kg + e] = sKk[i * 2 * NX + j];
-                st[SL::kap + e] = sKk[i * 2 * NX + NX + j];
-                st[SL::W2 + e] = sW2[e];
+                stg[SL::Kg + e] = sKk[i * 2 * NX + j];
+                stg[SL::kap + e] = sKk[i * 2 * NX + NX + j];
+                stg[SL::W2 + e] = sW2[e];
             }
-            for (int e = lane; e < NU * NU; e += WAVE) st[SL::L + e] = sRh[e];
+            for (int e = lane; e < NU * NU; e += WAVE) stg[SL::L + e] = sRh[e];
+            if (ts > 0) pf_commit(ts - 1, pf);
             __syncthreads();
         }
         // LU with partial pivoting of M (lane 0; NX <= 12)
@@ -388,135 +422,156 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 
     // solve: stage q,r,e buffers filled; xi0 = sv[0], r2f = sv[1] (LDS).  Outputs sdz, sdy, sdyi, sdyf.
     // LDS vector slots: sv[0] xi0, sv[1] r2f, sv[2] h, sv[3] pe, sv[4] qh/rh, sv[5] p', sv[6] xacc, sv[7] mu
-    auto solve = [&]() {
+    auto solve = [&]() __attribute__((always_inline)) {
         double* h = sv[2]; double* pe = sv[3]; double* qr = sv[4]; double* pp = sv[5];
         double* xacc = sv[6]; double* mu = sv[7];
+        double pf[PFN];
         if (lane < NX) { pp[lane] = 0.0; xacc[lane] = 0.0; }
+        pf_issue(K - 1, pf);
+        pf_commit(K - 1, pf);
         __syncthreads();
         for (int ts = K - 1; ts >= 0; --ts) {
-            double* st = stage + (long long)ts * SL::size;
+            if (ts > 0) pf_issue(ts - 1, pf);
+            const double* pk = slot(ts);
+            double* stg = stage + (long long)ts * SL::size;
             if (ts < K - 1) {
-                const double* stn = stage + (long long)(ts + 1) * SL::size;
+                const double* pkn = slot(ts + 1);
                 if (lane < NX) {
                     double hv = pp[lane], pv = 0.0;
 #pragma unroll
                     for (int k = 0; k < NX; ++k) {
-                        const double ek = st[SL::e + k];
-                        hv = fma(stn[SL::P + lane * NX + k], ek, hv);
-                        pv = fma(stn[SL::Pi + k * NX + lane], ek, pv);
+                        const double ek = pk[SL::e + k];
+                        hv = fma(pkn[SL::P + lane * NX + k], ek, hv);
+                        pv = fma(pkn[SL::Pi + k * NX + lane], ek, pv);
                     }
                     h[lane] = hv; pe[lane] = pv;
                 }
-                ld_stage_dyn(ts);
                 __syncthreads();
                 // qh = q + A'h (lanes 0..NX-1), rh = r + Bt'h (lanes NX..NX+NU-1)
                 if (lane < NX) {
-                    double v = st[SL::q + lane];
+                    double v = pk[SL::q + lane];
 #pragma unroll
-                    for (int k = 0; k < NX; ++k) v = fma(sA[k * NX + lane], h[k], v);
+                    for (int k = 0; k < NX; ++k) v = fma(pk[OA + lane * NX + k], h[k], v);  // A(k,lane), col-major
                     qr[lane] = v;
                 } else if (lane < NX + NU) {
                     const int j = lane - NX;
-                    double v = st[SL::r + j];
+                    double v = pk[SL::r + j];
 #pragma unroll
-                    for (int k = 0; k < NX; ++k) v = fma(sBt[k * NU + j], h[k], v);
+                    for (int k = 0; k < NX; ++k) v = fma(pk[SL::Bt + k * NU + j], h[k], v);
                     qr[lane] = v;
                 }
             } else {
-                if (lane < NX) { qr[lane] = st[SL::q + lane]; pe[lane] = 0.0; }
-                else if (lane < NX + NU) qr[lane] = st[SL::r + lane - NX];
+                if (lane < NX) { qr[lane] = pk[SL::q + lane]; pe[lane] = 0.0; }
+                else if (lane < NX + NU) qr[lane] = pk[SL::r + lane - NX];
             }
             __syncthreads();
             const bool fx = (ts == K - 1) && T.fix_last_input;
-            // k = -Rhat^{-1} rh  (every lane redundantly: NU <= 4)
-            double kv[NU], rh[NU];
+            // k = -Rhat^{-1} rh  (every lane redundantly: NU <= 4; L from the fresh factor in global)
+            double kv[NU], rh[NU], Lr[NU * NU];
+#pragma unroll
+            for (int e = 0; e < NU * NU; ++e) Lr[e] = pk[SL::L + e];
 #pragma unroll
             for (int i = 0; i < NU; ++i) { rh[i] = fx ? 0.0 : qr[NX + i]; kv[i] = rh[i]; }
 #pragma unroll
             for (int i = 0; i < NU; ++i) {
                 double v = kv[i];
 #pragma unroll
-                for (int k = 0; k < i; ++k) v -= st[SL::L + i * NU + k] * kv[k];
-                kv[i] = v / st[SL::L + i * NU + i];
+                for (int k = 0; k < i; ++k) v -= Lr[i * NU + k] * kv[k];
+                kv[i] = v / Lr[i * NU + i];
             }
 #pragma unroll
             for (int i = NU - 1; i >= 0; --i) {
                 double v = kv[i];
 #pragma unroll
-                for (int k = i + 1; k < NU; ++k) v -= st[SL::L + k * NU + i] * kv[k];
-                kv[i] = v / st[SL::L + i * NU + i];
+                for (int k = i + 1; k < NU; ++k) v -= Lr[k * NU + i] * kv[k];
+                kv[i] = v / Lr[i * NU + i];
             }
             if (lane < NX) {
                 double p = qr[lane], xa = pe[lane];
 #pragma unroll
                 for (int k = 0; k < NU; ++k) {
-                    p = fma(st[SL::Kg + k * NX + lane], rh[k], p);
-                    xa = fma(st[SL::W2 + k * NX + lane], -kv[k], xa);
+                    p = fma(pk[SL::Kg + k * NX + lane], rh[k], p);
+                    xa = fma(pk[SL::W2 + k * NX + lane], -kv[k], xa);
                 }
-                st[SL::p0 + lane] = p;
+                stg[SL::p0 + lane] = p;
+                pp[lane] = p;   // read by stage ts-1 after the barrier below
                 xacc[lane] += xa;
-                if (lane < NU) st[SL::k0 + lane] = -kv[lane];
+                if (lane < NU) stg[SL::k0 + lane] = -kv[lane];
             }
-            __syncthreads();
-            if (lane < NX) pp[lane] = st[SL::p0 + lane];
+            if (ts > 0) pf_commit(ts - 1, pf);
             __syncthreads();
         }
-        // terminal multiplier mu = M^{-1} (r2f - xacc - Pi_0' xi0)
+        // terminal multiplier mu = M^{-1} (r2f - xacc - Pi_0' xi0)   (Pi_0 from slot(0))
         if (lane == 0) {
+            const double* pk0 = slot(0);
             double b[NX];
+#pragma unroll
             for (int i = 0; i < NX; ++i) {
                 double v = sv[1][i] - xacc[i];
-                for (int k = 0; k < NX; ++k) v -= stage[SL::Pi + k * NX + i] * sv[0][k];
+#pragma unroll
+                for (int k = 0; k < NX; ++k) v -= pk0[SL::Pi + k * NX + i] * sv[0][k];
                 b[i] = fin ? v : 0.0;
             }
             if (fin) {
                 // getrf storage: apply every row interchange first, then unit-lower substitution
+#pragma unroll
                 for (int k = 0; k < NX; ++k) {
                     const int p = spiv[k];
-                    if (p != k) { double tmp = b[k]; b[k] = b[p]; b[p] = tmp; }
+#pragma unroll
+                    for (int i = 0; i < NX; ++i)
+                        if (i == p && p != k) { const double tmp = b[k]; b[k] = b[i]; b[i] = tmp; }
                 }
+#pragma unroll
                 for (int k = 0; k < NX; ++k)
+#pragma unroll
                     for (int i = k + 1; i < NX; ++i) b[i] -= sM[i * NX + k] * b[k];
+#pragma unroll
                 for (int i = NX - 1; i >= 0; --i) {
                     double v = b[i];
+#pragma unroll
                     for (int j = i + 1; j < NX; ++j) v -= sM[i * NX + j] * b[j];
                     b[i] = v / sM[i * NX + i];
                 }
             }
+#pragma unroll
             for (int i = 0; i < NX; ++i) mu[i] = b[i];
         }
+        // forward sweep (slots t, t+1 ring-buffered; k0/p0 were just written by the backward sweep)
+        pf_issue(0, pf);
+        pf_commit(0, pf);
+        if (K > 1) { pf_issue(1, pf); pf_commit(1, pf); }
         __syncthreads();
-        // forward sweep; h holds xi_t
         if (lane < NX) {
+            const double* pk0 = slot(0);
             h[lane] = sv[0][lane];
-            double v = stage[SL::p0 + lane];
+            double v = pk0[SL::p0 + lane];
 #pragma unroll
-            for (int k = 0; k < NX; ++k) v += stage[SL::P + lane * NX + k] * sv[0][k] + stage[SL::Pi + lane * NX + k] * mu[k];
+            for (int k = 0; k < NX; ++k) v += pk0[SL::P + lane * NX + k] * sv[0][k] + pk0[SL::Pi + lane * NX + k] * mu[k];
             sdyi[lane] = -v;
             sdyf[lane] = mu[lane];
         }
         __syncthreads();
         for (int ts = 0; ts < K; ++ts) {
-            double* st = stage + (long long)ts * SL::size;
+            if (ts + 2 < K) pf_issue(ts + 2, pf);
+            const double* pk = slot(ts);
             if (lane < NU) {  // v = K xi + k0 + kappa mu
-                double v = st[SL::k0 + lane];
+                double v = pk[SL::k0 + lane];
 #pragma unroll
-                for (int k = 0; k < NX; ++k) v += st[SL::Kg + lane * NX + k] * h[k] + st[SL::kap + lane * NX + k] * mu[k];
+                for (int k = 0; k < NX; ++k) v += pk[SL::Kg + lane * NX + k] * h[k] + pk[SL::kap + lane * NX + k] * mu[k];
                 qr[lane] = v;
             }
-            if (ts < K - 1) ld_stage_dyn(ts);
             __syncthreads();
             if (lane < NX) {
                 double dx = h[lane];
 #pragma unroll
-                for (int j = 0; j < NU; ++j) dx += (ts > 0 ? disc[(long long)(ts - 1) * DSTR + NX * NX + NX * NU + j * NX + lane] : 0.0) * qr[j];
+                for (int j = 0; j < NU; ++j) dx += pk[OC + j * NX + lane] * qr[j];  // C_{t-1} (zero at t = 0)
                 sdz[ts][lane] = dx;
                 if (ts < K - 1) {
-                    double xn = st[SL::e + lane];
+                    double xn = pk[SL::e + lane];
 #pragma unroll
-                    for (int k = 0; k < NX; ++k) xn += sA[lane * NX + k] * h[k];
+                    for (int k = 0; k < NX; ++k) xn += pk[OA + k * NX + lane] * h[k];
 #pragma unroll
-                    for (int j = 0; j < NU; ++j) xn += sBt[lane * NU + j] * qr[j];
+                    for (int j = 0; j < NU; ++j) xn += pk[SL::Bt + lane * NU + j] * qr[j];
                     pe[lane] = xn;
                 }
             } else if (lane < NX + NU) {
@@ -524,21 +579,22 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             }
             __syncthreads();
             if (ts < K - 1) {
-                const double* stn = stage + (long long)(ts + 1) * SL::size;
+                const double* pkn = slot(ts + 1);
                 if (lane < NX) {
                     h[lane] = pe[lane];
-                    double v = stn[SL::p0 + lane];
+                    double v = pkn[SL::p0 + lane];
 #pragma unroll
-                    for (int k = 0; k < NX; ++k) v += stn[SL::P + lane * NX + k] * pe[k] + stn[SL::Pi + lane * NX + k] * mu[k];
+                    for (int k = 0; k < NX; ++k) v += pkn[SL::P + lane * NX + k] * pe[k] + pkn[SL::Pi + lane * NX + k] * mu[k];
                     sdy[ts][lane] = -v;
                 }
-                __syncthreads();
             }
+            if (ts + 2 < K) pf_commit(ts + 2, pf);
+            __syncthreads();
         }
     };
 
     // ------------------------------------------------------------------ node phase helpers
-    auto exchange_z = [&]() {
+    auto exchange_z = [&]() __attribute__((always_inline)) {
         if (act) {
 #pragma unroll
             for (int i = 0; i < NZ; ++i) sz[t][i] = z[i];
@@ -547,10 +603,12 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     };
     // write node Hessian blocks (Q, S, R in xi/v coordinates): Hxx = diag(dbox) + embed(Hpp),
     // Huu dense, H_xu = 0.
-    auto write_hessian = [&](const double* dbox, double (*Hpp)[3], const double* Huu) {
+    auto write_hessian = [&](const double* dbox, double (*Hpp)[3], const double* Huu) __attribute__((always_inline)) {
         if (!act) return;
         double* st = stage + (long long)t * SL::size;
+#pragma unroll
         for (int i = 0; i < NX; ++i)
+#pragma unroll
             for (int j = 0; j < NX; ++j) {
                 double v = (i == j) ? dbox[i] : 0.0;
                 if (i < pd && j < pd) v += Hpp[i][j];
@@ -562,8 +620,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
             for (int j = 0; j < NU; ++j) {
                 double v = dbox[i] * Cp[j * NX + i];
-                if (i < pd)
-                    for (int k = 0; k < pd; ++k) v += Hpp[i][k] * Cp[j * NX + k];
+#pragma unroll
+                for (int k = 0; k < 3; ++k)
+                    if (i < pd && k < pd) v += Hpp[i < 3 ? i : 0][k] * Cp[j * NX + k];
                 Sx[i * NU + j] = v;
                 st[SL::S + i * NU + j] = v;
             }
@@ -578,7 +637,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             }
     };
     // linear terms q = -r1x, r = -(Cp' r1x + r1u), e = -rp for this node
-    auto write_rhs = [&](const double* r1) {
+    auto write_rhs = [&](const double* r1) __attribute__((always_inline)) {
         if (!act) return;
         double* st = stage + (long long)t * SL::size;
 #pragma unroll
@@ -596,42 +655,51 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
     };
     // Bt_t = B_t + A_t C_{t-1}
-    auto write_Bt = [&]() {
+    auto write_Bt = [&]() __attribute__((always_inline)) {
         if (!(act && t < K - 1)) return;
         const double* d = disc + (long long)t * DSTR;
         double* st = stage + (long long)t * SL::size;
+#pragma unroll
         for (int i = 0; i < NX; ++i)
+#pragma unroll
             for (int j = 0; j < NU; ++j) {
                 double v = d[NX * NX + j * NX + i];
+#pragma unroll
                 for (int k = 0; k < NX; ++k) v += d[k * NX + i] * Cp[j * NX + k];
                 st[SL::Bt + i * NU + j] = v;
             }
     };
     // dynamics residual rp_t = x_{t+1} - A x_t - B u_t - C u_{t+1} - c_t (needs sz filled)
-    auto dyn_residual = [&]() {
+    auto dyn_residual = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < NX; ++i) rp[i] = 0.0;
         if (!(act && t < K - 1)) return;
         const double* d = disc + (long long)t * DSTR;
+#pragma unroll
         for (int i = 0; i < NX; ++i) {
             double v = sz[t + 1][i] - (d[NX * NX + 2 * NX * NU + i] * sig + d[NX * NX + 2 * NX * NU + NX + i]);
+#pragma unroll
             for (int k = 0; k < NX; ++k) v -= d[k * NX + i] * z[k];
+#pragma unroll
             for (int j = 0; j < NU; ++j) v -= d[NX * NX + j * NX + i] * z[NX + j] + d[NX * NX + NX * NU + j * NX + i] * sz[t + 1][NX + j];
             rp[i] = v;
         }
     };
     // r1 (position part) -= sum_g Hpa[g] r1a[g] / Haa[g]
-    auto eliminate_rhs = [&](double* r1) {
+    auto eliminate_rhs = [&](double* r1) __attribute__((always_inline)) {
         for (int g = 0; g < na; ++g) {
             const double f = gR1[g * WAVE] / gHaa[g * WAVE];
-            for (int i = 0; i < pd; ++i) r1[i] -= gH0[(3 * g + i) * WAVE] * f;
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                if (i < pd) r1[i] -= gH0[(3 * g + i) * WAVE] * f;
         }
     };
     // node Hessian for scaling D_r (unit = true: D = 1, W = I) ; fills group columns Haa, Hpa
-    auto assemble_hessian = [&](bool unit, const double* Wi2uu) {
+    auto assemble_hessian = [&](bool unit, const double* Wi2uu) __attribute__((always_inline)) {
         double dbox[NX], Hpp[3][3], Huu[NU * NU];
 #pragma unroll
         for (int i = 0; i < NX; ++i) dbox[i] = 0.0;
+#pragma unroll
         for (int i = 0; i < 3; ++i) Hpp[i][0] = Hpp[i][1] = Hpp[i][2] = 0.0;
 #pragma unroll
         for (int i = 0; i < NU; ++i)
@@ -639,6 +707,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             for (int j = 0; j < NU; ++j) Huu[i * NU + j] = (i == j ? 2.0 * wu : 0.0) + (soc ? Wi2uu[i * NU + j] : 0.0);
         for (int g = 0; g < na; ++g) {
             gHaa[g * WAVE] = 0.0;
+#pragma unroll
             for (int i = 0; i < 3; ++i) gH0[(3 * g + i) * WAVE] = 0.0;
         }
         for (int r = 0; r < nrows; ++r) {
@@ -659,9 +728,12 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 double g[3], b;
                 const int q = r - r_soft0, gr = group_of(q);
                 soft_row(q, g, b);
+#pragma unroll
                 for (int i = 0; i < 3; ++i)
+#pragma unroll
                     for (int j = 0; j < 3; ++j) Hpp[i][j] += Dr * g[i] * g[j];
                 gHaa[gr * WAVE] += Dr;
+#pragma unroll
                 for (int i = 0; i < 3; ++i) gH0[(3 * gr + i) * WAVE] += Dr * g[i];
             } else {
                 gHaa[(r - r_grp0) * WAVE] += Dr;
@@ -670,25 +742,30 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         for (int g = 0; g < na; ++g) {
             const double ih = 1.0 / gHaa[g * WAVE];
             double hp[3];
+#pragma unroll
             for (int i = 0; i < 3; ++i) hp[i] = gH0[(3 * g + i) * WAVE];
+#pragma unroll
             for (int i = 0; i < 3; ++i)
+#pragma unroll
                 for (int j = 0; j < 3; ++j) Hpp[i][j] -= hp[i] * hp[j] * ih;
         }
         write_hessian(dbox, Hpp, Huu);
     };
     // aux direction from the position direction: da_g = (r1a_g - Hpa_g' dp) / Haa_g
-    auto recover_aux = [&](const double* dzl) {
+    auto recover_aux = [&](const double* dzl) __attribute__((always_inline)) {
         for (int g = 0; g < a.gmax; ++g) {
             double v = 0.0;
             if (g < na) {
                 v = gR1[g * WAVE];
-                for (int i = 0; i < pd; ++i) v -= gH0[(3 * g + i) * WAVE] * dzl[i];
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+                    if (i < pd) v -= gH0[(3 * g + i) * WAVE] * dzl[i];
                 v /= gHaa[g * WAVE];
             }
             gDa[g * WAVE] = v;
         }
     };
-    auto set_boundary_rhs = [&]() {
+    auto set_boundary_rhs = [&]() __attribute__((always_inline)) {
         if (lane < NX) {
             sv[0][lane] = a.x_init[agent * NX + lane] - sz[0][lane];
             sv[1][lane] = fin ? a.x_final[agent * NX + lane] - sz[K - 1][lane] : 0.0;
@@ -762,7 +839,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     deg = (int)wave_sum((double)deg);
     const double tol = T.tol > 0 ? T.tol : 1e-9;
 
-    auto soc_step = [&](const double* x, const double* dx) {
+    auto soc_step = [&](const double* x, const double* dx) __attribute__((always_inline)) {
         double qa = dx[0] * dx[0], qb = x[0] * dx[0], qc = x[0] * x[0];
 #pragma unroll
         for (int j = 1; j < NQ; ++j) { qa -= dx[j] * dx[j]; qb -= x[j] * dx[j]; qc -= x[j] * x[j]; }
@@ -783,6 +860,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     };
 
     // ------------------------------------------------------------------ IPM iterations
+    long long cyc_factor = 0, cyc_solve = 0, cyc_all0 = __builtin_amdgcn_s_memtime();
     for (it = 0; it < T.max_iter && status != SCVX_STATUS_NUMERICAL; ++it) {
         exchange_z();
         dyn_residual();
@@ -836,15 +914,22 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 for (int i = 0; i < NX; ++i) rd[i] += syf[i];
             }
             if (t >= 1) {
+#pragma unroll
                 for (int i = 0; i < NX; ++i) rd[i] += sy[t - 1][i];
+#pragma unroll
                 for (int j = 0; j < NU; ++j)
+#pragma unroll
                     for (int i = 0; i < NX; ++i) rd[NX + j] -= Cp[j * NX + i] * sy[t - 1][i];
             }
             if (t < K - 1) {
                 const double* d = disc + (long long)t * DSTR;
+#pragma unroll
                 for (int k = 0; k < NX; ++k)
+#pragma unroll
                     for (int i = 0; i < NX; ++i) rd[k] -= d[k * NX + i] * sy[t][i];
+#pragma unroll
                 for (int j = 0; j < NU; ++j)
+#pragma unroll
                     for (int i = 0; i < NX; ++i) rd[NX + j] -= d[NX * NX + j * NX + i] * sy[t][i];
             }
             if (fixed_u) {
@@ -917,18 +1002,20 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
         assemble_hessian(false, Wi2uu);
         __syncthreads();
+        long long st0 = __builtin_amdgcn_s_memtime();
         if (!factor()) { status = SCVX_STATUS_NUMERICAL; break; }
+        cyc_factor += __builtin_amdgcn_s_memtime() - st0;
 
         // complementarity rhs of row r: predictor -s l ; corrector -s l - ds_a dl_a + sig mu
         double sgmu = 0.0;
         bool corr = false;
-        auto rco_of = [&](int r) {
+        auto rco_of = [&](int r) __attribute__((always_inline)) {
             const double v = -cS[r * WAVE] * cL[r * WAVE];
             return corr ? v - cP[r * WAVE] + sgmu : v;
         };
         // Newton direction: dz, dy -> LDS; aux -> gDa; SOC pieces -> dsq/dlq.  Returns dzl.
         double dzl[NZ], dsq[NQ], dlq[NQ], rho[NQ];
-        auto newton = [&](const double* rcq2) {
+        auto newton = [&](const double* rcq2) __attribute__((always_inline)) {
             double r1[NZ];
 #pragma unroll
             for (int i = 0; i < NZ; ++i) r1[i] = -rd[i];
@@ -968,7 +1055,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             eliminate_rhs(r1);
             write_rhs(r1);
             set_boundary_rhs();
+            long long st1 = __builtin_amdgcn_s_memtime();
             solve();
+            cyc_solve += __builtin_amdgcn_s_memtime() - st1;
 #pragma unroll
             for (int i = 0; i < NZ; ++i) dzl[i] = act ? sdz[t][i] : 0.0;
             recover_aux(dzl);
@@ -998,14 +1087,14 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             }
         };
         // row directions ds = -rc - G d, dl = (rco + l (rc + G d)) / s
-        auto row_dir = [&](int r, double& dsr, double& dlr) {
+        auto row_dir = [&](int r, double& dsr, double& dlr) __attribute__((always_inline)) {
             double gz, h;
             row_eval(r, dzl, gDa, gz, h);
             const double rcr = cR[r * WAVE];
             dsr = -rcr - gz;
             dlr = (rco_of(r) + cL[r * WAVE] * (rcr + gz)) / cS[r * WAVE];
         };
-        auto max_step = [&]() {
+        auto max_step = [&]() __attribute__((always_inline)) {
             double am = 1e300;
             for (int r = 0; r < nrows; ++r) {
                 double dsr, dlr;
@@ -1033,6 +1122,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         newton(rcq2);
         if (a.trace && agent == a.trace_agent && it == 0 && act) {  // predictor direction dump
             double* dd = a.trace + 8 * a.trace_cap + (long long)t * 40;
+#pragma unroll
             for (int i = 0; i < NZ; ++i) dd[i] = dzl[i];
             for (int g = 0; g < na && g < 17; ++g) dd[NZ + g] = gDa[g * WAVE];
             if (lane < NX) a.trace[8 * a.trace_cap + 64 * 40 + lane] = sdyi[lane];
@@ -1103,6 +1193,10 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     }
 
     // ------------------------------------------------------------------ outputs
+    if (a.trace && agent == a.trace_agent && lane == 0) {
+        double* dd = a.trace + 8 * a.trace_cap + 64 * 40 + 16;
+        dd[0] = (double)cyc_factor; dd[1] = (double)cyc_solve; dd[2] = (double)(__builtin_amdgcn_s_memtime() - cyc_all0);
+    }
     double pobj = 0.0;
     if (act) {
 #pragma unroll

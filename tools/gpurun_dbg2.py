@@ -1,6 +1,6 @@
 import sys, os, ctypes
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "dynamic-programming-multiagent-trajectory-optimiziation_amd"))
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dynamic-programming-multiagent-trajectory-optimiziation_amd"))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 import scvx_hip
 from oracle import problems as pb
@@ -25,7 +25,7 @@ torch.cuda.synchronize()
 b = buf.cpu().numpy()
 gd = b[8 * cap: 8 * cap + 64 * 40].reshape(64, 40)[:T]
 gyi = b[8 * cap + 64 * 40: 8 * cap + 64 * 40 + 6]
-cd = np.fromfile("dbg/cpu_dz1.bin", dtype=np.float64)
+cd = np.fromfile(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dbg/cpu_dz1.bin"), dtype=np.float64)
 cyi = cd[T * 40: T * 40 + 6]
 cd = cd[:T * 40].reshape(T, 40)
 np.set_printoptions(linewidth=200, precision=4)

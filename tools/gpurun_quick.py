@@ -1,6 +1,6 @@
 import time, sys, os
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "dynamic-programming-multiagent-trajectory-optimiziation_amd"))
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dynamic-programming-multiagent-trajectory-optimiziation_amd"))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 import scvx_hip
 from oracle import problems as pb
