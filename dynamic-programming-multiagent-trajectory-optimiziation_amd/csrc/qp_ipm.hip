@@ -144,6 +144,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     __shared__ int spiv[NX];
     __shared__ double sz[WAVE][NZ], sy[WAVE][NX], sdz[WAVE][NZ], sdy[WAVE][NX];
     __shared__ double syi[NX], syf[NX], sdyi[NX], sdyf[NX], sflag[4];
+    __shared__ double sStamp[16];
     __shared__ double sRing[3 * (StageLayout<NX, NU>::size + NX * NX + NX * NU)];
 
     // ------------------------------------------------------------------ node constants
@@ -248,19 +249,23 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     // Stage packets: [stage block (SL) | A_t (disc, col-major) | C_{t-1} (disc, col-major)], streamed
     // from the agent workspace into a 3-slot LDS ring one stage ahead of the sweep, so the
     // sequential chain only ever waits on LDS (the global loads of stage t-+1 fly during stage t).
+    // Each phase of a stage is straight-line: a lane picks its output element(s) (pointer/stride
+    // selection only), then one shared dot-product body runs for every output kind, so a phase
+    // costs one LDS round trip plus a short FMA chain.
     constexpr int PKT = SL::size + NX * NX + NX * NU;
     constexpr int PFN = (PKT + WAVE - 1) / WAVE;
     constexpr int OA = SL::size, OC = SL::size + NX * NX;
+    const bool stamp_on = a.trace && agent == a.trace_agent;
     auto slot = [&](int ts) __attribute__((always_inline)) -> double* { return sRing + (ts % 3) * PKT; };
     auto pf_issue = [&](int ts, double* r) __attribute__((always_inline)) {
 #pragma unroll
         for (int k = 0; k < PFN; ++k) {
             const int e = lane + WAVE * k;
-            double v = 0.0;
-            if (e < SL::size) v = stage[(long long)ts * SL::size + e];
-            else if (e < OC) v = (ts < K - 1) ? disc[(long long)ts * DSTR + (e - OA)] : 0.0;
-            else if (e < PKT) v = (ts > 0) ? disc[(long long)(ts - 1) * DSTR + NX * NX + NX * NU + (e - OC)] : 0.0;
-            r[k] = v;
+            const double* src = stage + (long long)ts * SL::size + e;
+            if (e >= SL::size && e < OC) src = disc + (long long)(ts < K - 1 ? ts : 0) * DSTR + (e - OA);
+            if (e >= OC) src = disc + (long long)(ts > 0 ? ts - 1 : 0) * DSTR + NX * NX + NX * NU + (e - OC);
+            const bool zero = (e >= SL::size && e < OC && ts >= K - 1) || (e >= OC && ts == 0);
+            r[k] = (e < PKT && !zero) ? *src : 0.0;
         }
     };
     auto pf_commit = [&](int ts, const double* r) __attribute__((always_inline)) {
@@ -271,72 +276,119 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             if (e < PKT) d[e] = r[k];
         }
     };
-    auto ld_stage_dyn = [&](const double* pk) __attribute__((always_inline)) {  // A_t, Bt_t into LDS (row-major)
-        for (int e = lane; e < NX * NX; e += WAVE) { const int i = e / NX, j = e % NX; sA[e] = pk[OA + j * NX + i]; }
-        for (int e = lane; e < NX * NU; e += WAVE) sBt[e] = pk[SL::Bt + e];
-    };
+    constexpr int E1 = 2 * NX * NX + 2 * NX * NU;   // phase-1 outputs: P'A, P'Bt, A'Pi', Bt'Pi'
+    constexpr int E2 = NX * NX + NU * NX + NU * NU; // phase-2 outputs: Qh, Sh, Rh
+    constexpr int E4 = 3 * NX * NX;                 // phase-4 outputs: P, Pi, M-increment
     // factor: node Hessians (Q,S,R) of all stages already in the stage buffers
     auto factor = [&]() __attribute__((always_inline)) -> bool {
         double pf[PFN];
         for (int e = lane; e < NX * NX; e += WAVE) { sM[e] = 0.0; sPp[e] = 0.0; sPip[e] = 0.0; }
         if (lane == 0) sflag[0] = 0.0;
+        __syncthreads();  // stage buffers were written by other lanes (global)
         pf_issue(K - 1, pf);
         pf_commit(K - 1, pf);
-        __syncthreads();
+        wsync();
         for (int ts = K - 1; ts >= 0; --ts) {
+            if (stamp_on && ts == 25 && lane == 0) sStamp[0] = (double)__builtin_amdgcn_s_memtime();
             if (ts > 0) pf_issue(ts - 1, pf);
-            const double* pk = slot(ts);
+            double* pk = slot(ts);
             double* stg = stage + (long long)ts * SL::size;  // global outputs
-            for (int e = lane; e < NX * NX; e += WAVE) sQ[e] = pk[SL::Q + e];
-            for (int e = lane; e < NX * NU; e += WAVE) sS[e] = pk[SL::S + e];
-            for (int e = lane; e < NU * NU; e += WAVE) sR[e] = pk[SL::R + e];
-            if (ts < K - 1) ld_stage_dyn(pk);
-            __syncthreads();
-            if (ts < K - 1) {
-                mm<NX, NX, NX, false, false>(sT1, sPp, sA, nullptr, 1.0, lane);    // P'A
-                mm<NX, NU, NX, false, false>(sT2, sPp, sBt, nullptr, 1.0, lane);   // P'Bt
-                if (fin) {
-                    mm<NX, NX, NX, true, false>(sW1, sA, sPip, nullptr, 1.0, lane);  // A'Pi'
-                    mm<NU, NX, NX, true, false>(sW2, sBt, sPip, nullptr, 1.0, lane); // Bt'Pi'
-                }
-                __syncthreads();
-                mm<NX, NX, NX, true, false>(sQh, sA, sT1, sQ, 1.0, lane);           // Q + A'P'A
-                mm<NU, NX, NX, true, false>(sSh, sBt, sT1, nullptr, 1.0, lane);     // Bt'P'A
-                mm<NU, NU, NX, true, false>(sRh, sBt, sT2, sR, 1.0, lane);          // R + Bt'P'Bt
-                __syncthreads();
-                for (int e = lane; e < NU * NX; e += WAVE) { const int i = e / NX, j = e % NX; sSh[e] += sS[j * NU + i]; }
-            } else {
-                for (int e = lane; e < NX * NX; e += WAVE) { sQh[e] = sQ[e]; sW1[e] = (e / NX == e % NX) ? 1.0 : 0.0; }
-                for (int e = lane; e < NU * NX; e += WAVE) {
-                    const int i = e / NX, j = e % NX;
-                    sSh[e] = sS[j * NU + i];
-                    // W2 at the last stage = C_{K-2}' (so that M += W2' kappa gives C_{K-2} kappa_{K-1})
-                    sW2[e] = (K >= 2) ? pk[OC + i * NX + j] : 0.0;
-                }
-                for (int e = lane; e < NU * NU; e += WAVE) sRh[e] = sR[e];
-            }
-            __syncthreads();
-            const bool fx = (ts == K - 1) && T.fix_last_input;
-            if (lane == 0) {  // mask fixed inputs, Cholesky of Rhat (NU <= 4) into sRh (lower)
-                if (fx) {
-                    for (int i = 0; i < NU; ++i)
-                        for (int j = 0; j < NU; ++j) sRh[i * NU + j] = (i == j) ? 1.0 : 0.0;
-                }
-                for (int j = 0; j < NU; ++j) {
-                    double d = sRh[j * NU + j];
-                    for (int k = 0; k < j; ++k) d -= sRh[j * NU + k] * sRh[j * NU + k];
-                    if (!(d > 0.0)) { sflag[0] = 1.0; d = 1.0; }
-                    d = sqrt(d);
-                    sRh[j * NU + j] = d;
-                    for (int i = j + 1; i < NU; ++i) {
-                        double v = sRh[i * NU + j];
-                        for (int k = 0; k < j; ++k) v -= sRh[i * NU + k] * sRh[j * NU + k];
-                        sRh[i * NU + j] = v / d;
+            const bool last = ts == K - 1;
+            // ---- phase 1: T1 = P'A, T2 = P'Bt, W1 = A'Pi', W2 = Bt'Pi'   (zero / C' at the last stage)
+#pragma unroll
+            for (int rep = 0; rep < (E1 + WAVE - 1) / WAVE; ++rep) {
+                int off = lane + rep * WAVE;
+                if (off < E1) {
+                    const double *Lp, *Rp;
+                    int lsk, rsk;
+                    double* out;
+                    double base = 0.0;
+                    if (off < NX * NX) {
+                        const int i = off / NX, j = off % NX;
+                        Lp = sPp + i * NX; lsk = 1; Rp = pk + OA + j * NX; rsk = 1; out = sT1 + off;
+                    } else if ((off -= NX * NX) < NX * NU) {
+                        const int i = off / NU, j = off % NU;
+                        Lp = sPp + i * NX; lsk = 1; Rp = pk + SL::Bt + j; rsk = NU; out = sT2 + off;
+                    } else if ((off -= NX * NU) < NX * NX) {
+                        const int i = off / NX, j = off % NX;
+                        Lp = pk + OA + i * NX; lsk = 1; Rp = sPip + j; rsk = NX; out = sW1 + off;
+                        if (last) base = (i == j) ? 1.0 : 0.0;
+                    } else {
+                        off -= NX * NX;
+                        const int i = off / NX, j = off % NX;
+                        Lp = pk + SL::Bt + i; lsk = NU; Rp = sPip + j; rsk = NX; out = sW2 + off;
+                        if (last) base = pk[OC + i * NX + j];  // C_{K-2}' (M += W2' kappa -> C_{K-2} kappa)
                     }
+                    double acc = 0.0;
+                    if (!last) {
+#pragma unroll
+                        for (int k = 0; k < NX; ++k) acc = fma(Lp[k * lsk], Rp[k * rsk], acc);
+                    }
+                    *out = base + acc;
                 }
             }
-            __syncthreads();
-            // [K | kappa] = -Rhat^{-1} [Shat | W2]   (one column per lane)
+            wsync();
+            if (stamp_on && ts == 25 && lane == 0) sStamp[1] = (double)__builtin_amdgcn_s_memtime();
+            // ---- phase 2: Qh = Q + A'T1, Sh = S' + Bt'T1, Rh = R + Bt'T2
+#pragma unroll
+            for (int rep = 0; rep < (E2 + WAVE - 1) / WAVE; ++rep) {
+                int off = lane + rep * WAVE;
+                if (off < E2) {
+                    const double *Lp, *Rp;
+                    int lsk, rsk;
+                    double* out;
+                    double base;
+                    if (off < NX * NX) {
+                        const int i = off / NX, j = off % NX;
+                        Lp = pk + OA + i * NX; lsk = 1; Rp = sT1 + j; rsk = NX; out = sQh + off; base = pk[SL::Q + off];
+                    } else if ((off -= NX * NX) < NU * NX) {
+                        const int i = off / NX, j = off % NX;
+                        Lp = pk + SL::Bt + i; lsk = NU; Rp = sT1 + j; rsk = NX; out = sSh + off; base = pk[SL::S + j * NU + i];
+                    } else {
+                        off -= NU * NX;
+                        const int i = off / NU, j = off % NU;
+                        Lp = pk + SL::Bt + i; lsk = NU; Rp = sT2 + j; rsk = NU; out = sRh + off; base = pk[SL::R + off];
+                    }
+                    double acc = 0.0;
+                    if (!last) {
+#pragma unroll
+                        for (int k = 0; k < NX; ++k) acc = fma(Lp[k * lsk], Rp[k * rsk], acc);
+                    }
+                    *out = base + acc;
+                }
+            }
+            wsync();
+            if (stamp_on && ts == 25 && lane == 0) sStamp[2] = (double)__builtin_amdgcn_s_memtime();
+            // ---- phase 3: Cholesky of Rhat in registers (every lane), [K | kappa] = -Rhat^-1 [Sh | W2]
+            const bool fx = last && T.fix_last_input;
+            double Lr[NU * NU], id[NU];
+#pragma unroll
+            for (int e = 0; e < NU * NU; ++e) Lr[e] = fx ? ((e / NU == e % NU) ? 1.0 : 0.0) : sRh[e];
+            // pivots that rounding pushed below 1e-13 * max diag (Rhat = R + Bt'P'Bt with P' a Schur
+            // complement loses definiteness at ~1e15 barrier scalings) are clamped, not fatal
+            double dmax = 0.0;
+#pragma unroll
+            for (int j = 0; j < NU; ++j) dmax = fmax(dmax, fabs(Lr[j * NU + j]));
+            const double dmin = 1e-13 * dmax + 1e-300;
+            bool bad = (dmax != dmax);
+#pragma unroll
+            for (int j = 0; j < NU; ++j) {
+                double d = Lr[j * NU + j];
+#pragma unroll
+                for (int k = 0; k < j; ++k) d -= Lr[j * NU + k] * Lr[j * NU + k];
+                bad |= (d != d);
+                d = sqrt(d > dmin ? d : dmin);
+                Lr[j * NU + j] = d;
+                id[j] = 1.0 / d;
+#pragma unroll
+                for (int i = j + 1; i < NU; ++i) {
+                    double v = Lr[i * NU + j];
+#pragma unroll
+                    for (int k = 0; k < j; ++k) v -= Lr[i * NU + k] * Lr[j * NU + k];
+                    Lr[i * NU + j] = v * id[j];
+                }
+            }
+            if (bad && lane == 0) sflag[0] = 1.0;
             if (lane < 2 * NX) {
                 const int c = lane;
                 const bool isk = c < NX;
@@ -347,126 +399,141 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 for (int i = 0; i < NU; ++i) {
                     double v = col[i];
 #pragma unroll
-                    for (int k = 0; k < i; ++k) v -= sRh[i * NU + k] * col[k];
-                    col[i] = v / sRh[i * NU + i];
+                    for (int k = 0; k < i; ++k) v -= Lr[i * NU + k] * col[k];
+                    col[i] = v * id[i];
                 }
 #pragma unroll
                 for (int i = NU - 1; i >= 0; --i) {
                     double v = col[i];
 #pragma unroll
-                    for (int k = i + 1; k < NU; ++k) v -= sRh[k * NU + i] * col[k];
-                    col[i] = v / sRh[i * NU + i];
+                    for (int k = i + 1; k < NU; ++k) v -= Lr[k * NU + i] * col[k];
+                    col[i] = v * id[i];
                 }
 #pragma unroll
-                for (int i = 0; i < NU; ++i) sKk[i * 2 * NX + c] = -col[i];
-            }
-            __syncthreads();
-            if (fx) {
-                for (int e = lane; e < NU * NX; e += WAVE) sSh[e] = 0.0;
-                __syncthreads();
-            }
-            // P = Qh + Sh' K ; Pi = W1 + Sh' kappa ; M += W2' kappa
-            for (int e = lane; e < NX * NX; e += WAVE) {
-                const int i = e / NX, j = e % NX;
-                double p = sQh[e], pi = sW1[e], mm_ = 0.0;
-#pragma unroll
-                for (int k = 0; k < NU; ++k) {
-                    p = fma(sSh[k * NX + i], sKk[k * 2 * NX + j], p);
-                    pi = fma(sSh[k * NX + i], sKk[k * 2 * NX + NX + j], pi);
-                    mm_ = fma(sW2[k * NX + i], sKk[k * 2 * NX + NX + j], mm_);
+                for (int i = 0; i < NU; ++i) {
+                    sKk[i * 2 * NX + c] = -col[i];
+                    (isk ? stg[SL::Kg + i * NX + c] : stg[SL::kap + i * NX + c - NX]) = -col[i];
                 }
-                sT1[e] = p;      // reuse T1 as new P (symmetrised below)
-                sW1[e] = pi;
-                if (fin) sM[e] += mm_;
             }
-            __syncthreads();
-            for (int e = lane; e < NX * NX; e += WAVE) {
-                const int i = e / NX, j = e % NX;
-                const double p = 0.5 * (sT1[i * NX + j] + sT1[j * NX + i]);
-                sPp[e] = p;
-                sPip[e] = sW1[e];
-                stg[SL::P + e] = p;
-                stg[SL::Pi + e] = sW1[e];
+            if (lane < NU * NU) stg[SL::L + lane] = Lr[lane];
+            wsync();
+            if (stamp_on && ts == 25 && lane == 0) sStamp[3] = (double)__builtin_amdgcn_s_memtime();
+            // ---- phase 4: P = Qh + Sh'K (symmetrised in-lane), Pi = W1 + Sh'kappa, M += W2'kappa
+#pragma unroll
+            for (int rep = 0; rep < (E4 + WAVE - 1) / WAVE; ++rep) {
+                int off = lane + rep * WAVE;
+                if (off < E4) {
+                    const int grp = off / (NX * NX), o = off % (NX * NX), i = o / NX, j = o % NX;
+                    if (grp == 0) {
+                        double p = sQh[o], pt = sQh[j * NX + i];
+#pragma unroll
+                        for (int k = 0; k < NU; ++k) {
+                            const double shk_i = fx ? 0.0 : sSh[k * NX + i], shk_j = fx ? 0.0 : sSh[k * NX + j];
+                            p = fma(shk_i, sKk[k * 2 * NX + j], p);
+                            pt = fma(shk_j, sKk[k * 2 * NX + i], pt);
+                        }
+                        p = 0.5 * (p + pt);
+                        sPp[o] = p;
+                        stg[SL::P + o] = p;
+                    } else if (grp == 1) {
+                        double pi = sW1[o];
+#pragma unroll
+                        for (int k = 0; k < NU; ++k) pi = fma(fx ? 0.0 : sSh[k * NX + i], sKk[k * 2 * NX + NX + j], pi);
+                        sPip[o] = pi;
+                        stg[SL::Pi + o] = pi;
+                    } else if (fin) {
+                        double mm_ = 0.0;
+#pragma unroll
+                        for (int k = 0; k < NU; ++k) mm_ = fma(sW2[k * NX + i], sKk[k * 2 * NX + NX + j], mm_);
+                        sM[o] += mm_;
+                    }
+                }
             }
-            for (int e = lane; e < NU * NX; e += WAVE) {
-                const int i = e / NX, j = e % NX;
-                stg[SL::Kg + e] = sKk[i * 2 * NX + j];
-                stg[SL::kap + e] = sKk[i * 2 * NX + NX + j];
-                stg[SL::W2 + e] = sW2[e];
-            }
-            for (int e = lane; e < NU * NU; e += WAVE) stg[SL::L + e] = sRh[e];
+            for (int e = lane; e < NU * NX; e += WAVE) stg[SL::W2 + e] = sW2[e];
             if (ts > 0) pf_commit(ts - 1, pf);
-            __syncthreads();
+            wsync();
+            if (stamp_on && ts == 25 && lane == 0) sStamp[4] = (double)__builtin_amdgcn_s_memtime();
         }
-        // LU with partial pivoting of M (lane 0; NX <= 12)
+        // LU with partial pivoting of M (lane 0, in registers; NX <= 12)
         if (fin && lane == 0) {
+            double Mr[NX * NX];
+#pragma unroll
+            for (int e = 0; e < NX * NX; ++e) Mr[e] = sM[e];
+#pragma unroll
             for (int k = 0; k < NX; ++k) {
                 int p = k;
-                for (int i = k + 1; i < NX; ++i)
-                    if (fabs(sM[i * NX + k]) > fabs(sM[p * NX + k])) p = i;
-                spiv[k] = p;
-                if (p != k)
-                    for (int j = 0; j < NX; ++j) { double tmp = sM[k * NX + j]; sM[k * NX + j] = sM[p * NX + j]; sM[p * NX + j] = tmp; }
-                const double d = sM[k * NX + k];
-                if (d == 0.0) { sflag[0] = 1.0; continue; }
+                double best = fabs(Mr[k * NX + k]);
+#pragma unroll
                 for (int i = k + 1; i < NX; ++i) {
-                    const double f = sM[i * NX + k] / d;
-                    sM[i * NX + k] = f;
-                    for (int j = k + 1; j < NX; ++j) sM[i * NX + j] -= f * sM[k * NX + j];
+                    const double v = fabs(Mr[i * NX + k]);
+                    if (v > best) { best = v; p = i; }
+                }
+                spiv[k] = p;
+#pragma unroll
+                for (int i = k + 1; i < NX; ++i) {
+                    if (i == p) {
+#pragma unroll
+                        for (int j = 0; j < NX; ++j) { const double tmp = Mr[k * NX + j]; Mr[k * NX + j] = Mr[i * NX + j]; Mr[i * NX + j] = tmp; }
+                    }
+                }
+                const double d = Mr[k * NX + k];
+                if (d == 0.0) sflag[0] = 2.0;
+                const double inv = d != 0.0 ? 1.0 / d : 0.0;
+#pragma unroll
+                for (int i = k + 1; i < NX; ++i) {
+                    const double f = Mr[i * NX + k] * inv;
+                    Mr[i * NX + k] = f;
+#pragma unroll
+                    for (int j = k + 1; j < NX; ++j) Mr[i * NX + j] -= f * Mr[k * NX + j];
                 }
             }
+#pragma unroll
+            for (int e = 0; e < NX * NX; ++e) sM[e] = Mr[e];
         }
-        __syncthreads();
+        wsync();
         return sflag[0] == 0.0;
     };
 
     // solve: stage q,r,e buffers filled; xi0 = sv[0], r2f = sv[1] (LDS).  Outputs sdz, sdy, sdyi, sdyf.
-    // LDS vector slots: sv[0] xi0, sv[1] r2f, sv[2] h, sv[3] pe, sv[4] qh/rh, sv[5] p', sv[6] xacc, sv[7] mu
+    // LDS vector slots: sv[0] xi0, sv[1] r2f, sv[2] xi, sv[3] xi', sv[4] qh|rh / v, sv[5] p', sv[6] xacc, sv[7] mu
     auto solve = [&]() __attribute__((always_inline)) {
-        double* h = sv[2]; double* pe = sv[3]; double* qr = sv[4]; double* pp = sv[5];
+        double* xi = sv[2]; double* xin = sv[3]; double* qr = sv[4]; double* pp = sv[5];
         double* xacc = sv[6]; double* mu = sv[7];
         double pf[PFN];
         if (lane < NX) { pp[lane] = 0.0; xacc[lane] = 0.0; }
+        __syncthreads();  // q, r, e were written by other lanes (global)
         pf_issue(K - 1, pf);
         pf_commit(K - 1, pf);
-        __syncthreads();
+        wsync();
         for (int ts = K - 1; ts >= 0; --ts) {
             if (ts > 0) pf_issue(ts - 1, pf);
             const double* pk = slot(ts);
+            const double* pkn = slot(ts + 1);
             double* stg = stage + (long long)ts * SL::size;
-            if (ts < K - 1) {
-                const double* pkn = slot(ts + 1);
-                if (lane < NX) {
-                    double hv = pp[lane], pv = 0.0;
+            const bool last = ts == K - 1;
+            // ---- phase 1: h = P_{t+1} e + p' (every lane, redundantly); lanes 0..NX-1: qh = q + A'h,
+            //      lanes NX..NX+NU-1: rh = r + Bt'h
+            if (lane < NX + NU) {
+                double h[NX];
 #pragma unroll
-                    for (int k = 0; k < NX; ++k) {
-                        const double ek = pk[SL::e + k];
-                        hv = fma(pkn[SL::P + lane * NX + k], ek, hv);
-                        pv = fma(pkn[SL::Pi + k * NX + lane], ek, pv);
+                for (int i = 0; i < NX; ++i) {
+                    double v = pp[i];
+                    if (!last) {
+#pragma unroll
+                        for (int k = 0; k < NX; ++k) v = fma(pkn[SL::P + i * NX + k], pk[SL::e + k], v);
                     }
-                    h[lane] = hv; pe[lane] = pv;
+                    h[i] = last ? 0.0 : v;
                 }
-                __syncthreads();
-                // qh = q + A'h (lanes 0..NX-1), rh = r + Bt'h (lanes NX..NX+NU-1)
-                if (lane < NX) {
-                    double v = pk[SL::q + lane];
+                const bool isq = lane < NX;
+                const int j = isq ? lane : lane - NX;
+                double v = isq ? pk[SL::q + j] : pk[SL::r + j];
 #pragma unroll
-                    for (int k = 0; k < NX; ++k) v = fma(pk[OA + lane * NX + k], h[k], v);  // A(k,lane), col-major
-                    qr[lane] = v;
-                } else if (lane < NX + NU) {
-                    const int j = lane - NX;
-                    double v = pk[SL::r + j];
-#pragma unroll
-                    for (int k = 0; k < NX; ++k) v = fma(pk[SL::Bt + k * NU + j], h[k], v);
-                    qr[lane] = v;
-                }
-            } else {
-                if (lane < NX) { qr[lane] = pk[SL::q + lane]; pe[lane] = 0.0; }
-                else if (lane < NX + NU) qr[lane] = pk[SL::r + lane - NX];
+                for (int k = 0; k < NX; ++k) v = fma(isq ? pk[OA + j * NX + k] : pk[SL::Bt + k * NU + j], h[k], v);
+                qr[lane] = v;
             }
-            __syncthreads();
-            const bool fx = (ts == K - 1) && T.fix_last_input;
-            // k = -Rhat^{-1} rh  (every lane redundantly: NU <= 4; L from the fresh factor in global)
+            wsync();
+            // ---- phase 2: k = -Rhat^-1 rh (every lane), p = qh + K'rh, xacc += W2'k + Pi_{t+1}'e
+            const bool fx = last && T.fix_last_input;
             double kv[NU], rh[NU], Lr[NU * NU];
 #pragma unroll
             for (int e = 0; e < NU * NU; ++e) Lr[e] = pk[SL::L + e];
@@ -487,19 +554,23 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 kv[i] = v / Lr[i * NU + i];
             }
             if (lane < NX) {
-                double p = qr[lane], xa = pe[lane];
+                double p = qr[lane], xa = 0.0;
 #pragma unroll
                 for (int k = 0; k < NU; ++k) {
                     p = fma(pk[SL::Kg + k * NX + lane], rh[k], p);
                     xa = fma(pk[SL::W2 + k * NX + lane], -kv[k], xa);
                 }
+                if (!last) {
+#pragma unroll
+                    for (int k = 0; k < NX; ++k) xa = fma(pkn[SL::Pi + k * NX + lane], pk[SL::e + k], xa);
+                }
                 stg[SL::p0 + lane] = p;
-                pp[lane] = p;   // read by stage ts-1 after the barrier below
+                pp[lane] = p;   // p' of stage ts-1
                 xacc[lane] += xa;
                 if (lane < NU) stg[SL::k0 + lane] = -kv[lane];
             }
             if (ts > 0) pf_commit(ts - 1, pf);
-            __syncthreads();
+            wsync();
         }
         // terminal multiplier mu = M^{-1} (r2f - xacc - Pi_0' xi0)   (Pi_0 from slot(0))
         if (lane == 0) {
@@ -537,59 +608,50 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             for (int i = 0; i < NX; ++i) mu[i] = b[i];
         }
         // forward sweep (slots t, t+1 ring-buffered; k0/p0 were just written by the backward sweep)
+        __syncthreads();
         pf_issue(0, pf);
         pf_commit(0, pf);
         if (K > 1) { pf_issue(1, pf); pf_commit(1, pf); }
-        __syncthreads();
-        if (lane < NX) {
-            const double* pk0 = slot(0);
-            h[lane] = sv[0][lane];
-            double v = pk0[SL::p0 + lane];
-#pragma unroll
-            for (int k = 0; k < NX; ++k) v += pk0[SL::P + lane * NX + k] * sv[0][k] + pk0[SL::Pi + lane * NX + k] * mu[k];
-            sdyi[lane] = -v;
-            sdyf[lane] = mu[lane];
-        }
-        __syncthreads();
+        if (lane < NX) xi[lane] = sv[0][lane];
+        wsync();
         for (int ts = 0; ts < K; ++ts) {
             if (ts + 2 < K) pf_issue(ts + 2, pf);
             const double* pk = slot(ts);
-            if (lane < NU) {  // v = K xi + k0 + kappa mu
+            // ---- phase a: v = K xi + k0 + kappa mu (lanes 0..NU-1); y_{t-1} = -(P_t xi + p0_t + Pi_t mu)
+            //      (lanes 32..32+NX-1; y_{-1} is the initial-state multiplier)
+            if (lane < NU) {
                 double v = pk[SL::k0 + lane];
 #pragma unroll
-                for (int k = 0; k < NX; ++k) v += pk[SL::Kg + lane * NX + k] * h[k] + pk[SL::kap + lane * NX + k] * mu[k];
+                for (int k = 0; k < NX; ++k) v += pk[SL::Kg + lane * NX + k] * xi[k] + pk[SL::kap + lane * NX + k] * mu[k];
                 qr[lane] = v;
+            } else if (lane >= 32 && lane < 32 + NX) {
+                const int i = lane - 32;
+                double v = pk[SL::p0 + i];
+#pragma unroll
+                for (int k = 0; k < NX; ++k) v += pk[SL::P + i * NX + k] * xi[k] + pk[SL::Pi + i * NX + k] * mu[k];
+                if (ts == 0) { sdyi[i] = -v; sdyf[i] = mu[i]; }
+                else sdy[ts - 1][i] = -v;
             }
-            __syncthreads();
+            wsync();
+            // ---- phase b: dx_t = xi + C_{t-1} v, du_t = v, xi' = A xi + Bt v + e
             if (lane < NX) {
-                double dx = h[lane];
+                double dx = xi[lane];
 #pragma unroll
                 for (int j = 0; j < NU; ++j) dx += pk[OC + j * NX + lane] * qr[j];  // C_{t-1} (zero at t = 0)
                 sdz[ts][lane] = dx;
-                if (ts < K - 1) {
-                    double xn = pk[SL::e + lane];
+                double xn = pk[SL::e + lane];
 #pragma unroll
-                    for (int k = 0; k < NX; ++k) xn += pk[OA + k * NX + lane] * h[k];
+                for (int k = 0; k < NX; ++k) xn += pk[OA + k * NX + lane] * xi[k];
 #pragma unroll
-                    for (int j = 0; j < NU; ++j) xn += pk[SL::Bt + lane * NU + j] * qr[j];
-                    pe[lane] = xn;
-                }
-            } else if (lane < NX + NU) {
-                sdz[ts][lane] = qr[lane - NX];
-            }
-            __syncthreads();
-            if (ts < K - 1) {
-                const double* pkn = slot(ts + 1);
-                if (lane < NX) {
-                    h[lane] = pe[lane];
-                    double v = pkn[SL::p0 + lane];
-#pragma unroll
-                    for (int k = 0; k < NX; ++k) v += pkn[SL::P + lane * NX + k] * pe[k] + pkn[SL::Pi + lane * NX + k] * mu[k];
-                    sdy[ts][lane] = -v;
-                }
+                for (int j = 0; j < NU; ++j) xn += pk[SL::Bt + lane * NU + j] * qr[j];
+                xin[lane] = xn;
+            } else if (lane >= 32 && lane < 32 + NU) {
+                sdz[ts][NX + lane - 32] = qr[lane - 32];
             }
             if (ts + 2 < K) pf_commit(ts + 2, pf);
-            __syncthreads();
+            wsync();
+            if (lane < NX) xi[lane] = xin[lane];
+            wsync();
         }
     };
 
@@ -861,6 +923,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 
     // ------------------------------------------------------------------ IPM iterations
     long long cyc_factor = 0, cyc_solve = 0, cyc_all0 = __builtin_amdgcn_s_memtime();
+    double fail_code = 0.0;
     for (it = 0; it < T.max_iter && status != SCVX_STATUS_NUMERICAL; ++it) {
         exchange_z();
         dyn_residual();
@@ -946,17 +1009,22 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         pres = wave_max(pres); dres = wave_max(dres); hsc = wave_max(hsc); qsc = wave_max(qsc);
         gap = wave_sum(gap); pobj = wave_sum(pobj);
         const double mu = gap / fmax((double)deg, 1.0);
-        if (!isfinite(pres + dres + mu)) { status = SCVX_STATUS_NUMERICAL; break; }
+        if (!isfinite(pres + dres + mu)) { status = SCVX_STATUS_NUMERICAL; fail_code = 3.0; break; }
         if (pres <= tol * hsc && dres <= tol * qsc && gap <= tol * fmax(1.0, fabs(pobj))) {
             status = SCVX_STATUS_OPTIMAL;
             break;
         }
+        // ECOS-style reduced accuracy: what a numerical breakdown below leaves is still usable
+        const bool near = pres <= 1e-6 * hsc && dres <= 1e-6 * qsc && gap <= 1e-6 * fmax(1.0, fabs(pobj));
         // SOC Nesterov-Todd scaling (hyperbolic-rotation form, W z = W^-1 s)
         double Wi2uu[NU * NU];
         if (soc) {
-            double Js = sq[0] * sq[0], Jz = lq[0] * lq[0];
+            // J(x) = (x0 - |x1|)(x0 + |x1|): no catastrophic cancellation next to the cone boundary
+            double n1s = 0.0, n1z = 0.0;
 #pragma unroll
-            for (int j = 1; j < NQ; ++j) { Js -= sq[j] * sq[j]; Jz -= lq[j] * lq[j]; }
+            for (int j = 1; j < NQ; ++j) { n1s += sq[j] * sq[j]; n1z += lq[j] * lq[j]; }
+            n1s = sqrt(n1s); n1z = sqrt(n1z);
+            const double Js = fmax((sq[0] - n1s) * (sq[0] + n1s), 1e-300), Jz = fmax((lq[0] - n1z) * (lq[0] + n1z), 1e-300);
             const double ns = sqrt(Js), nz = sqrt(Jz);
             double sb[NQ], zb[NQ], w[NQ], dot = 0.0;
 #pragma unroll
@@ -1003,7 +1071,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         assemble_hessian(false, Wi2uu);
         __syncthreads();
         long long st0 = __builtin_amdgcn_s_memtime();
-        if (!factor()) { status = SCVX_STATUS_NUMERICAL; break; }
+        if (!factor()) { status = near ? SCVX_STATUS_MAX_ITER : SCVX_STATUS_NUMERICAL; fail_code = sflag[0]; break; }
         cyc_factor += __builtin_amdgcn_s_memtime() - st0;
 
         // complementarity rhs of row r: predictor -s l ; corrector -s l - ds_a dl_a + sig mu
@@ -1164,6 +1232,17 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
         newton(rcq2);
         const double al = fmin(1.0, 0.99 * max_step());
+        {
+            double chk = al;
+#pragma unroll
+            for (int i = 0; i < NZ; ++i) chk += 0.0 * dzl[i];
+            chk = wave_sum(chk);  // NaN anywhere in the direction poisons the sum
+            if (!(chk == chk) || !(al > 0.0)) {
+                status = near ? SCVX_STATUS_MAX_ITER : SCVX_STATUS_NUMERICAL;
+                fail_code = 4.0;
+                break;
+            }
+        }
         if (a.trace && agent == a.trace_agent && lane == 0 && it < a.trace_cap) {
             double* tr_ = a.trace + 8 * it;
             tr_[0] = pres; tr_[1] = dres; tr_[2] = gap; tr_[3] = pobj; tr_[4] = aa; tr_[5] = al; tr_[6] = sg; tr_[7] = mu;
@@ -1196,6 +1275,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     if (a.trace && agent == a.trace_agent && lane == 0) {
         double* dd = a.trace + 8 * a.trace_cap + 64 * 40 + 16;
         dd[0] = (double)cyc_factor; dd[1] = (double)cyc_solve; dd[2] = (double)(__builtin_amdgcn_s_memtime() - cyc_all0);
+        for (int k = 0; k < 12; ++k) dd[3 + k] = sStamp[k];
+        dd[15] = fail_code;
     }
     double pobj = 0.0;
     if (act) {

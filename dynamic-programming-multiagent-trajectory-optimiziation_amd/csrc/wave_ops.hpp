@@ -11,6 +11,17 @@ namespace scvx {
 
 constexpr int WAVE = 64;
 
+// LDS-only barrier for a one-wavefront workgroup.  __syncthreads() emits s_waitcnt vmcnt(0)
+// (it fences global memory too), which would drain every prefetch load and every store in flight
+// at each phase of a sequential sweep.  Lanes of one wave exchange data through LDS in issue
+// order, so a phase boundary only needs the LDS counter drained plus a compiler barrier.
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only (vmcnt, expcnt left at max)
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);

@@ -35,7 +35,7 @@ def test_dist_scvx_3d_first_iteration_matches_dense_oracle(cuda):
             rows[i, t] = dense_rows[i][t]
             cnt[i, t] = 2
     box = [(0, -1, 22), (1, -1, 20)]
-    spec = scvx_hip.QPSpec(model="di", K=T, box=box, j_max=J, w_coll=1e4, tol=1e-10, max_iter=80)
+    spec = scvx_hip.QPSpec(model="di", K=T, box=box, j_max=J, w_coll=1e4, tol=1e-9, max_iter=80)
     import torch
     out = scvx_hip.qp_solve_batched(spec, _t(disc, cuda), _t(np.zeros(3), cuda), _t(Xref, cuda), _t(Uref, cuda),
                                     _t(Xref[:, 0], cuda), _t(xdes, cuda), _t(np.full(3, sc["tr"]), cuda),

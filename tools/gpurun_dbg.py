@@ -8,12 +8,14 @@ d = torch.device("cuda")
 T_ = lambda x, dt=torch.float64: torch.tensor(np.ascontiguousarray(x), device=d, dtype=dt)
 
 def trace_solve(solver, agent, *args):
-    buf = torch.zeros(8 * 100, dtype=torch.float64, device=d)
+    buf = torch.zeros(8 * 100 + 64 * 40 + 64, dtype=torch.float64, device=d)
     scvx_hip.lib().scvx_qp_set_trace(ctypes.c_void_p(buf.data_ptr()), agent, 100)
     out = solver.solve(*args)
     torch.cuda.synchronize()
     scvx_hip.lib().scvx_qp_set_trace(None, 0, 0)
-    b = buf.view(100, 8).cpu().numpy()
+    bb = buf.cpu().numpy()
+    print("fail code", bb[8 * 100 + 64 * 40 + 16 + 15])
+    b = bb[:800].reshape(100, 8)
     print(f"agent {agent} status {out['status'][agent].item()} iters {out['iters'][agent].item()}")
     for i in range(min(int(out["iters"][agent].item()) + 1, 100)):
         if np.all(b[i] == 0): break

@@ -19,6 +19,8 @@ for N in (1, 64, 1024):
     args = (disc, sig, X, U, T_(sc["x_init"]), T_(sc["x_final"]), T_(np.full(N, 0.25)))
     out = s.solve(*args); torch.cuda.synchronize()
     t0 = time.time(); out = s.solve(*args); torch.cuda.synchronize(); el = time.time() - t0
-    b = buf.cpu().numpy()[8 * cap + 64 * 40 + 16:][:3]
+    b = buf.cpu().numpy()[8 * cap + 64 * 40 + 16:][:15]
+    st = b[3:15]
+    print("factor phase cycles (stage 25):", np.diff(st[st > 0]).astype(int).tolist())
     it = out["iters"][0].item()
     print(f"N={N} wall {el*1e3:.2f} ms iters(agent0) {it}  cycles: factor {b[0]:.3e} solve {b[1]:.3e} total {b[2]:.3e}  -> per-iter factor {b[0]/it:.0f} solve(x2) {b[1]/it:.0f} other {(b[2]-b[0]-b[1])/it:.0f}")
