@@ -1,0 +1,152 @@
+"""CPU tests of the drop-in SCvx surface and the C-ABI (no GPU needed).
+
+Known-answer tests restated from the reference suite:
+  SCvx/multi_agent_tests/test_admm_utils.py:7-45, test_multi_agent_model.py:9-59,
+  SCvx/tests/test_unicycle_model.py:10-64 (numpy parts)."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from oracle import models_np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+# ---------------------------------------------------------------- admm_utils KATs
+def test_primal_residual_zero():
+    from SCvx.optimization.admm_utils import primal_residual
+    assert primal_residual(np.zeros((2, 5)), np.zeros((2, 5))) == 0.0
+
+
+def test_primal_residual_nonzero():
+    from SCvx.optimization.admm_utils import primal_residual
+    p = np.array([[1, 2, 3, 4, 5], [0, 0, 0, 0, 0]], dtype=float)
+    assert primal_residual(p, np.zeros_like(p)) == pytest.approx(np.linalg.norm(p), rel=1e-6)
+
+
+def test_dual_residual():
+    from SCvx.optimization.admm_utils import dual_residual
+    Y_new = np.array([[1, 1, 1, 1], [2, 2, 2, 2]], dtype=float)
+    assert dual_residual(Y_new, np.zeros((2, 4))) == pytest.approx(np.linalg.norm(Y_new), rel=1e-6)
+
+
+@pytest.mark.parametrize("rho0,pr,du,mu,ti,td,exp", [(1.0, 100.0, 1.0, 10.0, 3.0, 2.0, 3.0),
+                                                     (10.0, 1.0, 100.0, 10.0, 3.0, 5.0, 2.0),
+                                                     (2.0, 10.0, 1.0, 100.0, 4.0, 4.0, 2.0)])
+def test_update_rho_admm(rho0, pr, du, mu, ti, td, exp):
+    from SCvx.optimization.admm_utils import update_rho_admm
+    assert update_rho_admm(rho0, primal_res=pr, dual_res=du, mu=mu, tau_inc=ti, tau_dec=td) == exp
+
+
+# ---------------------------------------------------------------- multi-agent model KATs
+def test_multi_agent_model_initialization():
+    from SCvx.models.multi_agent_model import MultiAgentModel
+    from SCvx.models.unicycle_model import UnicycleModel
+    mam = MultiAgentModel([{"r_init": np.array([0.0, 0.0, 0.0]), "r_final": np.array([1.0, 1.0, 0.0])},
+                           {"r_init": np.array([2.0, 2.0, 0.0]), "r_final": np.array([3.0, 3.0, 0.0])}], d_min=1.5)
+    assert mam.N == 2 and mam.d_min == 1.5 and all(isinstance(m, UnicycleModel) for m in mam.models)
+
+
+def test_linearize_collision_correctness():
+    from SCvx.global_parameters import K
+    from SCvx.models.multi_agent_model import MultiAgentModel
+    d_min = 2.0
+    mam = MultiAgentModel([{"r_init": np.array([0, d_min, 0]), "r_final": np.array([0, d_min, 0])},
+                           {"r_init": np.array([0, 0, 0]), "r_final": np.array([0, 0, 0])}], d_min=d_min)
+    X_i = np.tile(np.array([[0.0], [d_min], [0.0]]), (1, K))
+    X_j = np.tile(np.array([[0.0], [0.0], [0.0]]), (1, K))
+    A_ij, b_ij = mam.linearize_collision(0, 1, X_i, X_j)
+    for k in range(K):
+        assert np.allclose(A_ij[:, k], [0.0, 1.0], atol=1e-6)
+        assert b_ij[k] == pytest.approx(d_min, rel=1e-6)
+
+
+def test_si_linearize_matches_loop_form():
+    from SCvx.models.SI_multi_agent_model import SI_MultiAgentModel
+    rng = np.random.default_rng(0)
+    mam = SI_MultiAgentModel([{}, {}], d_min=0.7)
+    Xi, Xj = rng.normal(size=(3, 12)), rng.normal(size=(3, 12))
+    A, b = mam.linearize_inter_agent_collision(0, 1, Xi, Xj)
+    for k in range(12):  # SI_multi_agent_model.py:62-73 loop form
+        diff = Xi[:, k] - Xj[:, k]
+        a = diff / (np.linalg.norm(diff) + 1e-6)
+        assert np.allclose(A[:, k], a) and b[k] == pytest.approx(0.7 + a @ Xj[:, k])
+
+
+# ---------------------------------------------------------------- models
+def test_unicycle_equation_shapes_and_values():
+    from SCvx.global_parameters import K
+    from SCvx.models.base_model import BaseModel
+    from SCvx.models.unicycle_model import UnicycleModel
+    model = UnicycleModel()
+    assert isinstance(model, BaseModel)
+    f, A, B = model.get_equations()
+    x0, u0 = np.array([0.1, -0.2, 0.3]), np.array([0.5, -0.1])
+    assert f(x0, u0).shape in [(3, 1), (3,)] and A(x0, u0).shape == (3, 3) and B(x0, u0).shape == (3, 2)
+    fr, Ar, Br = models_np.unicycle_equations()
+    assert np.allclose(f(x0, u0), fr(x0, u0)) and np.allclose(A(x0, u0), Ar(x0, u0)) and np.allclose(B(x0, u0), Br(x0, u0))
+    X, U = model.initialize_trajectory(np.zeros((3, K)), np.zeros((2, K)))
+    np.testing.assert_allclose(X[:, 0], model.x_init)
+    np.testing.assert_allclose(X[:, -1], model.x_final)
+    assert np.all(U == 0)
+
+
+def test_quadrotor_jacobians_match_finite_differences():
+    f, A, B = models_np.quad_equations()
+    rng = np.random.default_rng(1)
+    for _ in range(5):
+        x = rng.normal(0, 0.3, 12)
+        u = np.array([9.81, 0.01, -0.02, 0.005]) + rng.normal(0, 0.1, 4)
+        Jx = np.stack([(f(x + e, u) - f(x - e, u)) / 2e-6 for e in np.eye(12) * 1e-6], axis=1)
+        Ju = np.stack([(f(x, u + e) - f(x, u - e)) / 2e-6 for e in np.eye(4) * 1e-6], axis=1)
+        assert np.abs(A(x, u) - Jx).max() < 1e-6 and np.abs(B(x, u) - Ju).max() < 1e-6
+    from SCvx.models.quadrotor_model import QuadrotorModel
+    q = QuadrotorModel()
+    x = rng.normal(0, 0.3, 12)
+    u = np.array([9.5, 0.01, 0.0, -0.01])
+    assert np.allclose(q.f(x, u), f(x, u), atol=1e-12)
+
+
+def test_dist_scvx_3d_zoh_matches_scipy():
+    from scipy import signal
+    from Distributed_opt import dist_scvx_3d as d
+    A = np.zeros((6, 6)); A[0:3, 3:6] = np.eye(3)
+    B = np.zeros((6, 3)); B[3:6] = np.eye(3)
+    sysd = signal.StateSpace(A, B, np.eye(6), np.zeros((6, 3))).to_discrete(d.dt)
+    assert np.abs(sysd.A - d.Ad).max() < 1e-12 and np.abs(sysd.B - d.Bd).max() < 1e-12
+    assert d.T == 51 and d.R == 2.3 and d.trust_region == 0.25 and len(d.robots_name) == 3
+
+
+# ---------------------------------------------------------------- C-ABI
+def test_library_exports_every_header_symbol():
+    import ctypes
+    from scvx_hip import _lib
+    hdr = open(os.path.join(REPO, "include", "scvx_hip.h")).read()
+    declared = set(re.findall(r"^\w[\w\s\*]*?\b(scvx_\w+)\(", hdr, flags=re.M))
+    assert {"scvx_foh_batched", "scvx_qp_solve_batched", "scvx_collision_rows_batched"} <= declared
+    L = _lib.lib()
+    for name in declared:
+        assert hasattr(L, name), name
+    assert set(_lib.EXPORTS) == declared
+    assert L.scvx_version() >= 1
+    # bad arguments are rejected without touching the GPU
+    rc = L.scvx_foh_batched(0, None, 1, 4, None, None, None, 1, None, None)
+    assert rc == -1 and b"bad args" in L.scvx_last_error()
+    t = _lib.QPTemplate()
+    t.K = 100
+    assert L.scvx_qp_solve_batched(ctypes.byref(t), 1, *([None] * 15), None, 0, None) == -2
+
+
+def test_first_order_hold_rejects_models_without_device_dynamics():
+    from SCvx.discretization.first_order_hold import FirstOrderHold
+
+    class Custom:
+        n_x, n_u = 2, 1
+
+        def get_equations(self):
+            return None, None, None
+
+    with pytest.raises(ValueError):
+        FirstOrderHold(Custom(), 10)

@@ -1,0 +1,105 @@
+"""GPU: the drop-in surfaces run unmodified-style against the MI355X backend.
+
+  * SCvx.discretization.first_order_hold.FirstOrderHold vs the reference goldens (LSODA) and the
+    reference test_disc.py shape contract (SCvx/tests/test_disc.py:9-49);
+  * Distributed_opt.dist_scvx_3d.x_traj_opt: one Jacobi sweep of the 3-robot scenario vs the dense
+    reference-formulation oracle per robot, then several sweeps of the reference outer loop."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from oracle import qp_dense as qd
+
+pytestmark = pytest.mark.gpu
+GOLD = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "foh_*.npz")))
+
+
+def _model(name):
+    from SCvx.models.double_integrator_model import DoubleIntegratorModel
+    from SCvx.models.quadrotor_model import QuadrotorModel
+    from SCvx.models.single_integrator_model import SingleIntegratorModel
+    from SCvx.models.unicycle_model import UnicycleModel
+    return {"di": DoubleIntegratorModel, "unicycle": UnicycleModel, "si": SingleIntegratorModel,
+            "quad": QuadrotorModel}[name]()
+
+
+@pytest.mark.parametrize("path", GOLD, ids=[os.path.basename(p) for p in GOLD])
+def test_first_order_hold_dropin(cuda, path):
+    from SCvx.discretization.first_order_hold import FirstOrderHold
+    d = np.load(path)
+    model = _model(str(d["model"]))
+    K = int(d["K"])
+    foh = FirstOrderHold(model, K)
+    outs = foh.calculate_discretization(d["X"], d["U"], float(d["sigma"]))
+    shapes = [(model.n_x * model.n_x, K - 1), (model.n_x * model.n_u, K - 1), (model.n_x * model.n_u, K - 1),
+              (model.n_x, K - 1), (model.n_x, K - 1)]
+    for o, name, shp in zip(outs, ["A_bar", "B_bar", "C_bar", "S_bar", "z_bar"], shapes):
+        assert o.shape == shp
+        assert np.abs(o - d[name]).max() / max(1.0, np.abs(d[name]).max()) < 1e-7, name
+    assert outs[0] is foh.A_bar  # reference aliasing: buffers owned by the object
+    Xp = foh.integrate_nonlinear_piecewise(d["X"], d["U"], float(d["sigma_nl"]))
+    Xf = foh.integrate_nonlinear_full(d["X"][:, 0], d["U"], float(d["sigma_nl"]))
+    assert Xp.shape == (model.n_x, K) and Xf.shape == (model.n_x, K)
+    assert np.abs(Xp - d["X_piecewise"]).max() / max(1, np.abs(d["X_piecewise"]).max()) < 1e-7
+    assert np.abs(Xf - d["X_full"]).max() / max(1, np.abs(d["X_full"]).max()) < 1e-6
+
+
+def _dense_reference_sweep(d, X_traj):
+    """x_traj_opt restated with the dense oracle, robot by robot (dist_scvx_3d.py:51-118)."""
+    names = d.robots_name
+    new = {}
+    for nm in names:
+        Xr = X_traj[nm][:, 0:6]
+        Ur = X_traj[nm][:, 6:9]
+        coll = []
+        for t in range(d.T - 1):
+            rows = []
+            for o in names:
+                if o == nm:
+                    continue
+                diff = X_traj[nm][t, 0:3] - X_traj[o][t, 0:3]
+                nr = np.linalg.norm(diff)
+                rows.append(np.concatenate([diff / nr, [2 * d.R - nr]]))
+            coll.append(np.array(rows))
+        prob = dict(A=np.repeat(d.Ad[None], d.T - 1, 0), B=np.repeat(d.Bd[None], d.T - 1, 0), Xref=Xr, Uref=Ur,
+                    x_final=d.x_des[nm][0:6], tr=d.trust_region, box=[(0, -1, 22), (1, -1, 20)], coll=coll,
+                    w_coll=1e4, fix_last_input=True)
+        Xn, Un, obj, info = qd.solve_agent(prob, tol=1e-10, maxit=150)
+        assert info["status"] == "optimal"
+        new[nm] = (Xn, Un, obj, prob)
+    return new
+
+
+def test_dist_scvx_3d_jacobi_sweep_matches_dense_oracle(cuda):
+    from Distributed_opt import dist_scvx_3d as d
+    X0 = d.x_initial(d.x_ini, d.x_des)
+    ref = _dense_reference_sweep(d, X0)
+    X1 = d.x_traj_opt({k: v.copy() for k, v in X0.items()}, d.trust_region)
+    for nm in d.robots_name:
+        Xn, Un, obj, prob = ref[nm]
+        got_X, got_U = X1[nm][:, 0:6], X1[nm][:, 6:9]
+        viol = qd.constraint_violation(prob, got_X, got_U, np.full(d.T, 1e9))
+        assert max(v for k, v in viol.items() if k != "coll") < 1e-8, viol
+        u_cost = np.sum(got_U[:-1] ** 2)
+        if obj < 1e3:  # no active collision slack: the minimum-energy trajectory is unique
+            assert abs(u_cost - obj) <= 1e-8 * max(1.0, obj)
+            assert np.abs(got_X - Xn).max() < 1e-6 and np.abs(got_U - Un).max() < 1e-6
+        np.testing.assert_array_equal(X1[nm][-1, 6:9], X0[nm][-1, 6:9])  # pinned unused row
+
+
+def test_dist_scvx_3d_outer_loop_runs(cuda):
+    from Distributed_opt import dist_scvx_3d as d
+    X = d.x_initial(d.x_ini, d.x_des)
+    tr = d.trust_region
+    costs = []
+    for it in range(6):
+        X = d.x_traj_opt(X, tr)
+        costs.append(d.cost_fcn(X))
+        if it >= 1 and costs[-1] > costs[-2]:
+            tr /= 2
+    for nm in d.robots_name:
+        np.testing.assert_allclose(X[nm][-1, 0:6], d.x_des[nm][0:6], atol=1e-7)
+        np.testing.assert_allclose(X[nm][0, 0:6], d.x_ini[nm][0:6], atol=1e-12)
+    assert all(np.isfinite(costs))
