@@ -17,6 +17,19 @@ from typing import Optional
 from . import (DEFAULT_NSUB, MODEL_DIMS, QPSolver, QPSpec, collision_rows, foh_batched)
 
 
+class HipBackend:
+    """The product compute path: the libscvx_hip.so kernels (no CPU fallback)."""
+
+    def foh(self, model, X, U, sigma, nsub, out):
+        return foh_batched(model, X, U, sigma, nsub=nsub, out=out)
+
+    def collision_rows(self, X_all, i0, n_local, R, j_max, pos_dim, cull, rows, count):
+        return collision_rows(X_all, i0, n_local, R, j_max, pos_dim, cull, rows, count)
+
+    def qp_solver(self, spec, N, device):
+        return QPSolver(spec, N, device=device)
+
+
 @dataclass
 class CouplingSpec:
     R: float = 2.3              # agent radius (dist_scvx_3d.py:211); rows use 2R
@@ -32,9 +45,10 @@ class JacobiSCvx:
     """
 
     def __init__(self, spec: QPSpec, x_init, x_final, sigma, tr0: float, coupling: Optional[CouplingSpec] = None,
-                 tr_rule: str = "per_agent", group=None, nsub: Optional[int] = None):
+                 tr_rule: str = "per_agent", group=None, nsub: Optional[int] = None, backend=None):
         import torch
         self.torch = torch
+        self.backend = backend or HipBackend()
         self.spec = spec
         self.N = x_init.shape[0]
         self.device = x_init.device
@@ -43,7 +57,7 @@ class JacobiSCvx:
         self.tr_rule = tr_rule
         self.group = group
         self.nsub = nsub or DEFAULT_NSUB[spec.model]
-        self.solver = QPSolver(spec, self.N, device=self.device)
+        self.solver = self.backend.qp_solver(spec, self.N, self.device)
         self.tr = torch.full((self.N,), float(tr0), dtype=torch.float64, device=self.device)
         self.prev_cost = torch.full((self.N,), float("inf"), dtype=torch.float64, device=self.device)
         self.prev_total = torch.full((1,), float("inf"), dtype=torch.float64, device=self.device)
@@ -74,12 +88,12 @@ class JacobiSCvx:
         """One SCvx iteration; returns the new (X, U) (device tensors owned by the solver)."""
         torch = self.torch
         spec = self.spec
-        self.disc = foh_batched(spec.model, X, U, self.sigma, nsub=self.nsub, out=self.disc)
+        self.disc = self.backend.foh(spec.model, X, U, self.sigma, self.nsub, self.disc)
         rows = count = None
         if self.coupling is not None:
             X_all = self.gather_states(X)
-            rows, count = collision_rows(X_all, self.i0, self.N, self.coupling.R, spec.j_max, spec.pos_dim,
-                                         self.coupling.cull_radius, self.rows, self.count)
+            rows, count = self.backend.collision_rows(X_all, self.i0, self.N, self.coupling.R, spec.j_max,
+                                                      spec.pos_dim, self.coupling.cull_radius, self.rows, self.count)
         out = self.solver.solve(self.disc, self.sigma, X, U, self.x_init, self.x_final, self.tr, rows, count)
         Xn, Un = out["X"], out["U"]
         # cost_fcn (dist_scvx_3d.py:131-138) and the trust-region halving rule (:250-252)
