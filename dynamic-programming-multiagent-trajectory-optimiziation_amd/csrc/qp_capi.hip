@@ -1,0 +1,117 @@
+// C-ABI of the batched trust-region QP (include/scvx_hip.h): argument checks, row-capacity class
+// selection (qp_caps.hpp), workspace sizing and the launch of the matching qp_ipm_kernel
+// instantiation (qp_inst_*.hip).
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+#include "qp_caps.hpp"
+#include "qp_ipm.hpp"
+#include "scvx_hip.h"
+
+namespace scvx {
+int qp_launch_di(int idx, const QPArgs& a, hipStream_t st);
+int qp_launch_unicycle(int idx, const QPArgs& a, hipStream_t st);
+int qp_launch_si(int idx, const QPArgs& a, hipStream_t st);
+int qp_launch_quad(int idx, const QPArgs& a, hipStream_t st);
+}  // namespace scvx
+
+using namespace scvx;
+
+namespace {
+double* g_trace = nullptr;
+int g_trace_agent = 0, g_trace_cap = 0;
+
+constexpr int kCapsDI[] = {SCVX_CAPS_DI};
+constexpr int kCapsUni[] = {SCVX_CAPS_UNICYCLE};
+constexpr int kCapsSI[] = {SCVX_CAPS_SI};
+constexpr int kCapsQuad[] = {SCVX_CAPS_QUAD};
+
+struct ModelTable {
+    int nx, nu;
+    const int* caps;
+    int ncaps;
+    int (*launch)(int, const QPArgs&, hipStream_t);
+};
+
+// model table entry for the template (nullptr: unknown model / dimensions)
+const ModelTable* model_of(const scvx_qp_template& T) {
+    static const ModelTable tab[] = {
+        {6, 3, kCapsDI, (int)(sizeof(kCapsDI) / sizeof(int) / 3), qp_launch_di},
+        {3, 2, kCapsUni, (int)(sizeof(kCapsUni) / sizeof(int) / 3), qp_launch_unicycle},
+        {3, 3, kCapsSI, (int)(sizeof(kCapsSI) / sizeof(int) / 3), qp_launch_si},
+        {12, 4, kCapsQuad, (int)(sizeof(kCapsQuad) / sizeof(int) / 3), qp_launch_quad},
+    };
+    const int ids[] = {SCVX_MODEL_DOUBLE_INTEGRATOR, SCVX_MODEL_UNICYCLE, SCVX_MODEL_SINGLE_INTEGRATOR, SCVX_MODEL_QUADROTOR};
+    for (int i = 0; i < 4; ++i)
+        if (T.model_id == ids[i] && T.n_x == tab[i].nx && T.n_u == tab[i].nu) return &tab[i];
+    return nullptr;
+}
+
+// validates the template; on success sets the model entry and the capacity class
+int qp_check(const scvx_qp_template* T, int N, const ModelTable*& mt, int& cls) {
+    if (!T || N < 0) return set_error(SCVX_EINVAL, "qp: null template");
+    if (T->K < 2 || T->K > WAVE) return set_error(SCVX_EUNSUPPORTED, "qp: K must be in [2, 64]");
+    if (T->pos_dim < 1 || T->pos_dim > 3 || T->pos_dim > T->n_x) return set_error(SCVX_EINVAL, "qp: pos_dim");
+    if (T->n_box < 0 || T->n_box > SCVX_MAX_BOX || T->n_obs < 0 || T->n_obs > SCVX_MAX_OBS || T->j_max < 0)
+        return set_error(SCVX_EINVAL, "qp: box/obstacle/collision counts");
+    for (int b = 0; b < T->n_box; ++b)
+        if (T->box_idx[b] < 0 || T->box_idx[b] >= T->n_x) return set_error(SCVX_EINVAL, "qp: box index");
+    if (T->max_iter < 1) return set_error(SCVX_EINVAL, "qp: max_iter");
+    mt = model_of(*T);
+    if (!mt) return set_error(SCVX_EUNSUPPORTED, "qp: model id / dimensions");
+    cls = qp_pick_caps(mt->caps, mt->ncaps, *T);
+    if (cls < 0) return set_error(SCVX_EUNSUPPORTED, "qp: more box / obstacle / collision rows than the largest capacity class (j_max <= 32, n_obs <= 16)");
+    return SCVX_OK;
+}
+
+size_t ws_bytes(const ModelTable& mt, int cls, int N) {
+    const int nb = mt.caps[3 * cls], no = mt.caps[3 * cls + 1], nc = mt.caps[3 * cls + 2];
+    (void)nb;
+    const int ns = no + nc, ng = no + (nc > 0 ? 1 : 0);
+    return sizeof(double) * (size_t)N * (size_t)qp_ws_doubles(mt.nx, mt.nu, ns, ng);
+}
+}  // namespace
+
+// Diagnostics hook (not part of the solve contract): subsequent scvx_qp_solve_batched launches write
+// 8 doubles per IPM iteration of agent `agent` into the device buffer (pres, dres, gap, pobj,
+// alpha_aff, alpha, sigma, mu), then 4 doubles (factor cycles, solve cycles, total cycles, fail code).
+extern "C" int scvx_qp_set_trace(double* buf, int agent, int cap) {
+    g_trace = buf; g_trace_agent = agent; g_trace_cap = buf ? cap : 0;
+    return SCVX_OK;
+}
+
+extern "C" size_t scvx_qp_workspace_bytes(const scvx_qp_template* tpl, int N) {
+    const ModelTable* mt = nullptr;
+    int cls = -1;
+    if (N <= 0 || qp_check(tpl, N, mt, cls) != SCVX_OK) return 0;
+    return ws_bytes(*mt, cls, N);
+}
+
+extern "C" int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const double* disc, const double* sigma,
+                                     const double* Xref, const double* Uref, const double* x_init,
+                                     const double* x_final, const double* tr, const double* coll_rows,
+                                     const int32_t* coll_count, double* X, double* U, double* slack_coll,
+                                     double* obj, int32_t* status, int32_t* iters, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+    const ModelTable* mt = nullptr;
+    int cls = -1;
+    int rc = qp_check(tpl, N, mt, cls);
+    if (rc != SCVX_OK) return rc;
+    if (N == 0) return SCVX_OK;
+    if (!disc || !sigma || !Xref || !Uref || !x_init || !tr || !X || !U || !slack_coll || !obj || !status || !iters)
+        return set_error(SCVX_EINVAL, "qp: null buffer");
+    if (tpl->has_final && !x_final) return set_error(SCVX_EINVAL, "qp: x_final required");
+    if (tpl->j_max > 0 && (!coll_rows || !coll_count)) return set_error(SCVX_EINVAL, "qp: collision rows required");
+    const size_t need = ws_bytes(*mt, cls, N);
+    if (!workspace || workspace_bytes < need) return set_error(SCVX_EWORKSPACE, "qp: workspace too small");
+    QPArgs a{};
+    a.T = *tpl;
+    a.N = N;
+    a.disc = disc; a.sigma = sigma; a.Xref = Xref; a.Uref = Uref; a.x_init = x_init; a.x_final = x_final;
+    a.tr = tr; a.coll_rows = coll_rows; a.coll_count = coll_count;
+    a.X = X; a.U = U; a.slack_coll = slack_coll; a.obj = obj; a.status = status; a.iters = iters;
+    a.ws = (double*)workspace;
+    a.ws_agent = (long long)(need / sizeof(double) / (size_t)N);
+    a.trace = g_trace; a.trace_agent = g_trace_agent; a.trace_cap = g_trace_cap;
+    return mt->launch(cls, a, (hipStream_t)stream);
+}

@@ -1,0 +1,1475 @@
+// Batched trust-region QP/SOCP solve for the SCvx inner loop (MI355X / gfx950, float64).
+//
+// Replaces the per-agent CVXPY+Clarabel solve of Distributed_opt/dist_scvx_3d.py:51-111
+// (x_traj_opt), batched over N agents; the problem is stated in include/scvx_hip.h.
+//
+// Algorithm: primal-dual interior point, Mehrotra predictor-corrector, Nesterov-Todd scaling for
+// the per-node second-order cone ||u_t|| <= u_max, CVXOPT-style starting point.  Each Newton
+// system is solved by a Riccati recursion over the K nodes in the FOH-transformed state
+// xi_t = x_t - C_{t-1} u_t (x_{t+1} = A x_t + B u_t + C u_{t+1} + c  becomes
+// xi_{t+1} = A xi_t + Bt u_t + c with Bt = B + A C_{t-1}); the terminal equality is handled by an
+// n x n Schur complement M on its multiplier mu, accumulated in the factor sweep.  Soft-constraint
+// slacks (obstacle slacks, the shared collision slack S_t of dist_scvx_3d.py:93-107) are
+// eliminated per node.
+//
+// Mapping (one agent per 64-lane wavefront = one workgroup; lane t = node t):
+//   * node phases  -- lane-parallel over the nodes.  The inequality-row state (slacks s,
+//                     duals lambda) lives in registers: rows have compile-time capacities
+//                     (QPCfg: 2^m trust-region facets, NB boxes, NO obstacles, NC collision
+//                     rows, their slack groups), so every row loop is unrolled with the row
+//                     kind resolved at compile time;
+//   * factor sweep -- sequential over stages, element-parallel over lanes: 4 straight-line
+//                     phases per stage, each lane's output element picked by a packed
+//                     descriptor computed once (no per-stage branching), stage inputs
+//                     streamed through a 2-slot LDS ring one stage ahead;
+//   * solves       -- closed-loop form.  With Acl_t = A_t + Bt_t K_t the backward pass is the
+//                     chain p_t = Acl_t' p_{t+1} + g_t and the forward pass the chain
+//                     xi_{t+1} = Acl_t xi_t + f_t: g_t, f_t and every output that does not sit on
+//                     the chain (feed-forward k0, inputs, multipliers) are computed
+//                     lane-parallel before/after the chain, so each chain step is one
+//                     n-term dot product per lane.
+// Factor outputs are kept in an agent-private workspace in stage-minor columns
+// (ws[col * 64 + t]): lane-parallel passes read them coalesced.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+#include "scvx_hip.h"
+#include "wave_ops.hpp"
+
+namespace scvx {
+
+struct QPArgs {
+    scvx_qp_template T;
+    int N;
+    const double* disc;
+    const double* sigma;
+    const double* Xref;
+    const double* Uref;
+    const double* x_init;
+    const double* x_final;
+    const double* tr;
+    const double* coll_rows;
+    const int32_t* coll_count;
+    double* X;
+    double* U;
+    double* slack_coll;
+    double* obj;
+    int32_t* status;
+    int32_t* iters;
+    double* ws;          // workspace
+    long long ws_agent;  // doubles per agent
+    double* trace;       // optional per-iteration diagnostics of agent `trace_agent` (or nullptr)
+    int trace_agent, trace_cap;
+};
+
+// ---- sizes shared by host (workspace / LDS bytes) and device
+constexpr int qp_dstr(int nx, int nu) { return nx * (nx + 2 * nu + 2); }
+constexpr int qp_pkt(int nx, int nu) { return 2 * nx * nx + 3 * nx * nu + nu * nu + nx; }
+constexpr int qp_ncol(int nx, int nu, int ns, int ng) {
+    return qp_dstr(nx, nu) + 3 * nu * nx + nu * nu + 3 * nx * nx + nx + nx * nu + 4 * ns + 4 * ng + nx + nu + ng;
+}
+constexpr long long qp_ws_doubles(int nx, int nu, int ns, int ng) {
+    return (long long)qp_ncol(nx, nu, ns, ng) * 64 + 64LL * qp_pkt(nx, nu);
+}
+constexpr int qp_even(int x) { return (x + 1) & ~1; }
+constexpr int qp_lds_factor(int nx, int nu) {
+    return qp_even(2 * qp_pkt(nx, nu) + 5 * nx * nx + 2 * nx * nu + nu * nx + nu * nu + 2 * nu * nx + 8);
+}
+constexpr int qp_lds_doubles(int nx, int nu, int K, int nr) {
+    // max(factor region, solve packets) + persistent vectors + predictor row products [nr][64]
+    return (qp_lds_factor(nx, nu) > K * (nx * nx + nx) ? qp_lds_factor(nx, nu) : qp_even(K * (nx * nx + nx))) +
+           2 * nx * nx + (K + 1) * nx + 10 * nx + 8 + 64 * nr;
+}
+
+template <int NX_, int NU_, int NB_, int NO_, int NC_>
+struct QPCfg {
+    static constexpr int NX = NX_, NU = NU_, NB = NB_, NO = NO_, NC = NC_;
+    static constexpr int NZ = NX + NU, NQ = NU + 1, NTR = 1 << NU;
+    static constexpr int NS = NO + NC;                // soft halfspace rows
+    static constexpr int NG = NO + (NC > 0 ? 1 : 0);  // slack groups (one per obstacle, one shared)
+    static constexpr int R_BOX = NTR, R_OBS = NTR + 2 * NB, R_COL = R_OBS + NO, R_GRP = R_COL + NC;
+    static constexpr int NR = R_GRP + NG;
+    static constexpr int DSTR = qp_dstr(NX, NU);
+    // factor packet [t][PKT]: node Hessian Q|S|R, e, then the constant A | Bt | C_{t-1}
+    static constexpr int P_Q = 0, P_S = P_Q + NX * NX, P_R = P_S + NX * NU, P_E = P_R + NU * NU,
+                         P_A = P_E + NX, P_BT = P_A + NX * NX, P_C = P_BT + NX * NU, PKT = P_C + NX * NU;
+    static_assert(PKT == qp_pkt(NX, NU), "packet size");
+    // stage-minor workspace columns
+    static constexpr int C_DT = 0;                // disc, transposed: A (col-major) | B | C | S | z
+    static constexpr int C_K = C_DT + DSTR;       // K      NU x NX
+    static constexpr int C_KAP = C_K + NU * NX;   // kappa  NU x NX
+    static constexpr int C_LD = C_KAP + NU * NX;  // LDL' of Rhat: L[i][j] (i > j), 1/d_i on the diagonal
+    static constexpr int C_W2 = C_LD + NU * NU;   // W2 = Bt' Pi_{t+1}  NU x NX
+    static constexpr int C_P = C_W2 + NU * NX;    // P_t
+    static constexpr int C_PI = C_P + NX * NX;    // Pi_t
+    static constexpr int C_ACL = C_PI + NX * NX;  // Acl_t = A_t + Bt_t K_t (row-major)
+    static constexpr int C_U = C_ACL + NX * NX;   // P_{t+1} e_t
+    static constexpr int C_BT = C_U + NX;         // Bt_t (row-major)
+    static constexpr int C_SOFT = C_BT + NX * NU; // soft rows (g0, g1, g2, b)
+    static constexpr int C_GRP = C_SOFT + 4 * NS; // per group: Hpa/Haa (3), 1/Haa
+    static constexpr int C_RD = C_GRP + 4 * NG;   // dual residual (x, u part)
+    static constexpr int C_R1A = C_RD + NZ;       // group part of the current Newton rhs
+    static constexpr int NCOL = C_R1A + NG;
+    static_assert(NCOL == qp_ncol(NX, NU, NS, NG), "column count");
+    // LDS (doubles): factor region (aliased by the solve packets), then persistent vectors
+    static constexpr int F_RING = 0, F_PP = 2 * PKT, F_PIP = F_PP + NX * NX, F_T1 = F_PIP + NX * NX,
+                         F_T2 = F_T1 + NX * NX, F_W1 = F_T2 + NX * NU, F_W2 = F_W1 + NX * NX,
+                         F_QH = F_W2 + NU * NX, F_SH = F_QH + NX * NX, F_RH = F_SH + NU * NX,
+                         F_KK = F_RH + NU * NU, F_SINK = F_KK + 2 * NU * NX, F_END = F_SINK + 8;
+    static_assert(qp_even(F_END) == qp_lds_factor(NX, NU), "factor LDS");
+    static constexpr int PKS = NX * NX + NX;  // solve packet per stage: Acl | g or f
+};
+
+// packed phase descriptors: operand = LDS offset (14 bits) | ring-slot relative << 14 | stride << 15
+__host__ __device__ constexpr int qp_dpk(int off, int slot, int stride) { return off | (slot << 14) | (stride << 15); }
+// output = LDS offset | accumulate << 14 | (global column + 1) << 15 ; base = offset | slot << 14 | kind << 15
+// (kind 0: none, 1: always, 2: last stage only)
+
+// Agent workspace accessor: raw buffer loads/stores with the lane part of the address in one
+// VGPR (voffset) and the column part as an SGPR/immediate (soffset), so no per-column 64-bit
+// address is ever materialised (or hoisted) in vector registers.
+typedef unsigned int qp_u2 __attribute__((ext_vector_type(2)));
+struct QPBuf {
+    __amdgpu_buffer_rsrc_t rs;
+    __device__ __forceinline__ double ld(int voff, int soff) const {
+        soff = __builtin_amdgcn_readfirstlane(soff);  // uniform by construction
+        asm volatile("" : "+s"(soff));
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
+    }
+    __device__ __forceinline__ void st(int voff, int soff, double v) const {
+        soff = __builtin_amdgcn_readfirstlane(soff);
+        asm volatile("" : "+s"(soff));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(qp_u2, v), rs, voff, soff, 0);
+    }
+};
+// keep a value opaque to loop-invariant code motion (re-derive it at the point of use)
+__device__ __forceinline__ int qp_opaque(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+// 1.0 if a == b else 0.0, opaque to the optimiser: selecting an array element by a runtime
+// index with this mask stays arithmetic (a compare/select chain is turned back into a
+// dynamically indexed private array, i.e. scratch memory)
+__device__ __forceinline__ double qp_mask(int a, int b) {
+    int m = a == b ? 1 : 0;
+    asm volatile("" : "+v"(m));
+    return (double)m;
+}
+
+template <int KK>
+__device__ __forceinline__ double qp_dot(const double* lds, int L, int R, int soff) {
+    L = qp_opaque(L);
+    R = qp_opaque(R);
+    const int lo = (L & 0x3FFF) + ((L >> 14) & 1) * soff, ls = L >> 15;
+    const int ro = (R & 0x3FFF) + ((R >> 14) & 1) * soff, rs = R >> 15;
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < KK; ++k) acc = fma(lds[lo + k * ls], lds[ro + k * rs], acc);
+    return acc;
+}
+
+template <class C>
+__global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
+    constexpr int NX = C::NX, NU = C::NU, NZ = C::NZ, NQ = C::NQ, NR = C::NR, NG = C::NG,
+                  NS = C::NS, NO = C::NO, NC = C::NC, PKT = C::PKT, PKS = C::PKS;
+    constexpr int NGA = NG > 0 ? NG : 1, NSA = NS > 0 ? NS : 1;
+    extern __shared__ double lds[];
+    const scvx_qp_template& T = a.T;
+    const int K = T.K, lane = threadIdx.x, t = lane;
+    const long long agent = blockIdx.x;
+    const bool act = t < K;
+    const bool ineq = act && ((t < K - 1) || T.ineq_last);
+    const bool fin = T.has_final != 0;
+    const bool soc = ineq && T.has_soc;
+    const bool has_coll = NC > 0 && T.j_max > 0;
+    const int nobs = T.n_obs, nbox = T.n_box;
+    const int ccount = (ineq && has_coll) ? min((int)a.coll_count[agent * K + t], min(T.j_max, NC)) : 0;
+    const double trv = a.tr[agent];
+    const double sig = a.sigma[agent];
+    const double wu = (t < K - 1) ? 1.0 : T.w_last;
+    const bool fixed_u = act && (t == K - 1) && T.fix_last_input;
+    const double* disc = a.disc + agent * (long long)(K - 1) * C::DSTR;
+    double* ws = a.ws + agent * a.ws_agent;
+    QPBuf wb;
+    wb.rs = __builtin_amdgcn_make_buffer_rsrc(ws, (short)0, 0x7fffffff, 0x00020000);
+    const int vt = t * 8;  // this lane's element of a stage-minor column
+    constexpr int PKB = C::NCOL * WAVE * 8;  // byte offset of the packets [t][PKT]
+    const int vpk = t * PKT * 8;
+    // column c at this lane's stage
+    auto cld = [&](int c) __attribute__((always_inline)) -> double { return wb.ld(vt, c * WAVE * 8); };
+    auto cst = [&](int c, double v) __attribute__((always_inline)) { wb.st(vt, c * WAVE * 8, v); };
+    auto pst = [&](int e, double v) __attribute__((always_inline)) { wb.st(vpk, PKB + e * 8, v); };
+
+    // persistent LDS vectors
+    const int R0 = qp_lds_factor(NX, NU) > K * PKS ? qp_lds_factor(NX, NU) : qp_even(K * PKS);
+    const int V_M = R0, V_PI0 = V_M + NX * NX, V_CH = V_PI0 + NX * NX, V_XE = V_CH + (K + 1) * NX,
+              V_XI0 = V_XE + NX, V_R2F = V_XI0 + NX, V_YI = V_R2F + NX, V_YF = V_YI + NX, V_DYI = V_YF + NX, V_DYF = V_DYI + NX, V_PIV = V_DYF + NX,
+              V_ONE = V_PIV + NX, V_FLAG = V_ONE + 1, V_CP = qp_even(V_FLAG + 4);
+    constexpr int S_PK = 0;
+
+    // ------------------------------------------------------------------ setup (once per solve)
+    double ub[NU];  // reference input
+#pragma unroll
+    for (int j = 0; j < NU; ++j) ub[j] = act ? a.Uref[(agent * K + t) * NU + j] : 0.0;
+    // C_{t-1} (column-major as disc) of this node, from the transposed disc at stage t-1
+    auto load_cp = [&](double* Cp) __attribute__((always_inline)) {
+#pragma unroll
+        for (int e = 0; e < NX * NU; ++e) {
+            const double v = wb.ld(vt - 8, (C::C_DT + NX * NX + NX * NU + e) * WAVE * 8);
+            Cp[e] = (t > 0) ? v : 0.0;
+        }
+    };
+    {
+        double Cp[NX * NU];
+#pragma unroll
+        for (int e = 0; e < NX * NU; ++e)
+            Cp[e] = (act && t > 0) ? disc[(long long)(t - 1) * C::DSTR + NX * NX + NX * NU + e] : 0.0;
+        // transposed disc (zero for t >= K-1), Bt = B + A C_{t-1}, the constant part of the packets
+        double Ad[NX * NX], Bd[NX * NU];
+        const bool dyn = t < K - 1;
+        for (int e = 0; e < C::DSTR; ++e) {
+            const double v = dyn ? disc[(long long)t * C::DSTR + e] : 0.0;
+            cst(C::C_DT + e, v);
+        }
+#pragma unroll
+        for (int e = 0; e < NX * NX; ++e) Ad[e] = dyn ? disc[(long long)t * C::DSTR + e] : 0.0;
+#pragma unroll
+        for (int e = 0; e < NX * NU; ++e) Bd[e] = dyn ? disc[(long long)t * C::DSTR + NX * NX + e] : 0.0;
+        if (act) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i)
+#pragma unroll
+                for (int j = 0; j < NU; ++j) {
+                    double v = Bd[j * NX + i];
+#pragma unroll
+                    for (int k = 0; k < NX; ++k) v = fma(Ad[k * NX + i], Cp[j * NX + k], v);
+                    cst(C::C_BT + i * NU + j, v);
+                    pst(C::P_BT + i * NU + j, v);
+                }
+#pragma unroll
+            for (int e = 0; e < NX * NX; ++e) pst(C::P_A + e, Ad[e]);
+#pragma unroll
+            for (int e = 0; e < NX * NU; ++e) pst(C::P_C + e, Cp[e]);
+        }
+        // soft rows: obstacle linearisations (single_integrator_model.py:113-126) from Xref, then
+        // the caller's collision rows (dist_scvx_3d.py:93-107)
+        const int pd = T.pos_dim;
+        double xb[3] = {0, 0, 0};
+        for (int i = 0; i < pd; ++i) xb[i] = act ? a.Xref[(agent * K + t) * NX + i] : 0.0;
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+            double d[3] = {0, 0, 0}, nr = 0.0, bo = 0.0;
+            if (o < nobs) {
+                bo = T.obs_radius[o];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    d[i] = i < pd ? xb[i] - T.obs_center[o][i] : 0.0;
+                    nr += d[i] * d[i];
+                }
+                nr = sqrt(nr) + 1e-6;
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    d[i] = d[i] / nr;
+                    bo += i < pd ? d[i] * T.obs_center[o][i] : 0.0;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 3; ++i) cst(C::C_SOFT + o * 4 + i, d[i]);
+            cst(C::C_SOFT + o * 4 + 3, bo);
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            double g[4] = {0, 0, 0, 0};
+            if (c < ccount) {
+                const double* src = a.coll_rows + ((agent * K + t) * T.j_max + c) * (pd + 1);
+                for (int i = 0; i < pd; ++i) g[i] = src[i];
+                g[3] = src[pd];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) cst(C::C_SOFT + (NO + c) * 4 + i, g[i]);
+        }
+        if (lane == 0) lds[V_ONE] = 1.0;
+    }
+
+    // ------------------------------------------------------------------ phase descriptors
+    constexpr int E1 = 2 * NX * NX + 2 * NX * NU + 2 * NX, E2 = NX * NX + NU * NX + NU * NU, E4 = 4 * NX * NX;
+    constexpr int R1 = (E1 + WAVE - 1) / WAVE, R2 = (E2 + WAVE - 1) / WAVE, R4 = (E4 + WAVE - 1) / WAVE;
+    int d1[R1][4], d2[R2][4], d4[R4][4];
+    {
+        const int sink = C::F_SINK;
+#pragma unroll
+        for (int rep = 0; rep < R1; ++rep) {
+            int o = lane + rep * WAVE, L = 0, R = 0, O = -1, B = 0;
+            if (o < NX * NX) {  // T1 = P' A
+                const int i = o / NX, j = o % NX;
+                L = qp_dpk(C::F_PP + i * NX, 0, 1); R = qp_dpk(C::P_A + j * NX, 1, 1); O = C::F_T1 + o;
+            } else if ((o -= NX * NX) < NX * NU) {  // T2 = P' Bt
+                const int i = o / NU, j = o % NU;
+                L = qp_dpk(C::F_PP + i * NX, 0, 1); R = qp_dpk(C::P_BT + j, 1, NU); O = C::F_T2 + o;
+            } else if ((o -= NX * NU) < NX * NX) {  // W1 = A' Pi'   (I at the last stage)
+                const int i = o / NX, j = o % NX;
+                L = qp_dpk(C::P_A + i * NX, 1, 1); R = qp_dpk(C::F_PIP + j, 0, NX); O = C::F_W1 + o;
+                B = (i == j) ? (V_ONE | (2 << 15)) : 0;
+            } else if ((o -= NX * NX) < NU * NX) {  // W2 = Bt' Pi'  (C_{K-2}' at the last stage)
+                const int i = o / NX, j = o % NX;
+                L = qp_dpk(C::P_BT + i, 1, NU); R = qp_dpk(C::F_PIP + j, 0, NX);
+                O = (C::F_W2 + o) | ((C::C_W2 + o + 1) << 15);
+                B = (C::P_C + i * NX + j) | (1 << 14) | (2 << 15);
+            } else if ((o -= NU * NX) < NX) {  // u = P' e  (global only)
+                L = qp_dpk(C::F_PP + o * NX, 0, 1); R = qp_dpk(C::P_E, 1, 1); O = sink | ((C::C_U + o + 1) << 15);
+            } else if ((o -= NX) < NX) {  // xe += Pi'' e
+                L = qp_dpk(C::F_PIP + o, 0, NX); R = qp_dpk(C::P_E, 1, 1); O = (V_XE + o) | (1 << 14);
+            }
+            d1[rep][0] = L; d1[rep][1] = R; d1[rep][2] = O; d1[rep][3] = B;
+        }
+#pragma unroll
+        for (int rep = 0; rep < R2; ++rep) {
+            int o = lane + rep * WAVE, L = 0, R = 0, O = -1, B = 0;
+            if (o < NX * NX) {  // Qh = Q + A' T1 (symmetric: (min, max) element for both halves)
+                const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
+                L = qp_dpk(C::P_A + p * NX, 1, 1); R = qp_dpk(C::F_T1 + q, 0, NX); O = C::F_QH + o;
+                B = (C::P_Q + p * NX + q) | (1 << 14) | (1 << 15);
+            } else if ((o -= NX * NX) < NU * NX) {  // Sh = S' + Bt' T1
+                const int i = o / NX, j = o % NX;
+                L = qp_dpk(C::P_BT + i, 1, NU); R = qp_dpk(C::F_T1 + j, 0, NX); O = C::F_SH + o;
+                B = (C::P_S + j * NU + i) | (1 << 14) | (1 << 15);
+            } else if ((o -= NU * NX) < NU * NU) {  // Rh = R + Bt' T2
+                const int i = o / NU, j = o % NU, p = i < j ? i : j, q = i < j ? j : i;
+                L = qp_dpk(C::P_BT + p, 1, NU); R = qp_dpk(C::F_T2 + q, 0, NU); O = C::F_RH + o;
+                B = (C::P_R + p * NU + q) | (1 << 14) | (1 << 15);
+            }
+            d2[rep][0] = L; d2[rep][1] = R; d2[rep][2] = O; d2[rep][3] = B;
+        }
+#pragma unroll
+        for (int rep = 0; rep < R4; ++rep) {
+            int o = lane + rep * WAVE, L = 0, R = 0, O = -1, B = 0;
+            if (o < NX * NX) {  // P = Qh + Sh' K (symmetric)
+                const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
+                L = qp_dpk(C::F_SH + p, 0, NX); R = qp_dpk(C::F_KK + q, 0, 2 * NX);
+                O = (C::F_PP + o) | ((C::C_P + o + 1) << 15); B = (C::F_QH + p * NX + q) | (1 << 15);
+            } else if ((o -= NX * NX) < NX * NX) {  // Pi = W1 + Sh' kappa
+                const int i = o / NX, j = o % NX;
+                L = qp_dpk(C::F_SH + i, 0, NX); R = qp_dpk(C::F_KK + NX + j, 0, 2 * NX);
+                O = (C::F_PIP + o) | ((C::C_PI + o + 1) << 15); B = (C::F_W1 + o) | (1 << 15);
+            } else if ((o -= NX * NX) < NX * NX) {  // M += W2' kappa (symmetric)
+                const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
+                L = qp_dpk(C::F_W2 + p, 0, NX); R = qp_dpk(C::F_KK + NX + q, 0, 2 * NX); O = (V_M + o) | (1 << 14);
+            } else if ((o -= NX * NX) < NX * NX) {  // Acl = A + Bt K
+                const int i = o / NX, j = o % NX;
+                L = qp_dpk(C::P_BT + i * NU, 1, 1); R = qp_dpk(C::F_KK + j, 0, 2 * NX);
+                O = sink | ((C::C_ACL + o + 1) << 15); B = (C::P_A + j * NX + i) | (1 << 14) | (1 << 15);
+            }
+            d4[rep][0] = L; d4[rep][1] = R; d4[rep][2] = O; d4[rep][3] = B;
+        }
+    }
+    auto run_desc = [&](const int* d, double val, int soff, bool last, int ts) __attribute__((always_inline)) {
+        const int O = qp_opaque(d[2]), B = qp_opaque(d[3]);
+        const int bk = B >> 15;
+        const double bv = lds[(B & 0x3FFF) + ((B >> 14) & 1) * soff];
+        const double v = val + ((bk == 1 || (bk == 2 && last)) ? bv : 0.0);
+        if (O >= 0) {
+            const int oo = O & 0x3FFF;
+            const double old = lds[oo];
+            lds[oo] = ((O >> 14) & 1) ? old + v : v;
+            const int g = (O >> 15) - 1;
+            if (g >= 0) wb.st(g * WAVE * 8, ts * 8, v);
+        }
+    };
+
+    // ------------------------------------------------------------------ factor sweep
+    // Stage inputs (Q, S, R, e of the node phase; A, Bt, C_{t-1}) are in packet t; outputs go to the
+    // stage-minor columns, M (and its LU) / Pi_0 / xe to persistent LDS.  false on a breakdown.
+    constexpr int PFN = (PKT + WAVE - 1) / WAVE;
+    auto factor = [&]() __attribute__((always_inline)) -> bool {
+        for (int e = lane; e < NX * NX; e += WAVE) { lds[C::F_PP + e] = 0.0; lds[C::F_PIP + e] = 0.0; lds[V_M + e] = 0.0; }
+        if (lane < NX) lds[V_XE + lane] = 0.0;
+        if (lane == 0) lds[V_FLAG] = 0.0;
+        __syncthreads();  // the node phase wrote the packets (global) from other lanes
+        double pf[PFN];
+        auto pf_load = [&](int ts) __attribute__((always_inline)) {
+#pragma unroll
+            for (int k = 0; k < PFN; ++k) {
+                const int e = lane + WAVE * k;
+                pf[k] = e < PKT ? wb.ld(e * 8, PKB + ts * PKT * 8) : 0.0;
+            }
+        };
+        auto pf_store = [&](int slot) __attribute__((always_inline)) {
+#pragma unroll
+            for (int k = 0; k < PFN; ++k) {
+                const int e = lane + WAVE * k;
+                if (e < PKT) lds[C::F_RING + slot * PKT + e] = pf[k];
+            }
+        };
+        pf_load(K - 1);
+        pf_store((K - 1) & 1);
+        wsync();
+        bool bad = false;
+        for (int ts = K - 1; ts >= 0; --ts) {
+            const int soff = (ts & 1) * PKT;
+            const bool last = ts == K - 1;
+            if (ts > 0) pf_load(ts - 1);
+            // ---- phase 1: T1 = P'A, T2 = P'Bt, W1 = A'Pi', W2 = Bt'Pi', u = P'e, xe += Pi''e
+#pragma unroll
+            for (int rep = 0; rep < R1; ++rep) run_desc(d1[rep], qp_dot<NX>(lds, d1[rep][0], d1[rep][1], soff), soff, last, ts);
+            wsync();
+            // ---- phase 2: Qh = Q + A'T1, Sh = S' + Bt'T1, Rh = R + Bt'T2
+#pragma unroll
+            for (int rep = 0; rep < R2; ++rep) run_desc(d2[rep], qp_dot<NX>(lds, d2[rep][0], d2[rep][1], soff), soff, last, ts);
+            wsync();
+            // ---- phase 3: Rh = L D L' in registers (every lane); [K | kappa] = -Rh^-1 [Sh | W2]
+            {
+                const bool fx = last && T.fix_last_input;
+                double Lm[NU * NU], dinv[NU];
+#pragma unroll
+                for (int e = 0; e < NU * NU; ++e) Lm[e] = lds[C::F_RH + e];
+                double dmax = 0.0;
+#pragma unroll
+                for (int j = 0; j < NU; ++j) dmax = fmax(dmax, fabs(Lm[j * NU + j]));
+                // pivots that rounding pushed below 1e-13 max|diag| are clamped (Rh is a Schur
+                // complement that loses definiteness at extreme barrier scalings); NaN is fatal
+                const double dmin = 1e-13 * dmax + 1e-300;
+                bool nan = dmax != dmax;
+#pragma unroll
+                for (int j = 0; j < NU; ++j) {
+                    double d = Lm[j * NU + j];
+#pragma unroll
+                    for (int k = 0; k < j; ++k) d -= Lm[j * NU + k] * Lm[j * NU + k] * Lm[k * NU + k];
+                    nan |= d != d;
+                    d = d > dmin ? d : dmin;
+                    Lm[j * NU + j] = d;
+                    dinv[j] = 1.0 / d;
+#pragma unroll
+                    for (int i = j + 1; i < NU; ++i) {
+                        double v = Lm[i * NU + j];
+#pragma unroll
+                        for (int k = 0; k < j; ++k) v -= Lm[i * NU + k] * Lm[j * NU + k] * Lm[k * NU + k];
+                        Lm[i * NU + j] = v * dinv[j];
+                    }
+                }
+                bad |= nan;
+                if (fx) {
+#pragma unroll
+                    for (int e = 0; e < NU * NU; ++e) Lm[e] = (e / NU == e % NU) ? 1.0 : 0.0;
+#pragma unroll
+                    for (int j = 0; j < NU; ++j) dinv[j] = 1.0;
+                }
+                if (lane < 2 * NX) {
+                    const int c = lane;
+                    const int off = c < NX ? C::F_SH + c : C::F_W2 + c - NX;
+                    double x[NU];
+#pragma unroll
+                    for (int i = 0; i < NU; ++i) {
+                        double v = lds[off + i * NX];
+#pragma unroll
+                        for (int k = 0; k < i; ++k) v -= Lm[i * NU + k] * x[k];
+                        x[i] = v;
+                    }
+#pragma unroll
+                    for (int i = 0; i < NU; ++i) x[i] *= dinv[i];
+#pragma unroll
+                    for (int i = NU - 1; i >= 0; --i) {
+                        double v = x[i];
+#pragma unroll
+                        for (int k = i + 1; k < NU; ++k) v -= Lm[k * NU + i] * x[k];
+                        x[i] = v;
+                    }
+                    const int g = c < NX ? C::C_K + c : C::C_KAP + c - NX;
+#pragma unroll
+                    for (int i = 0; i < NU; ++i) {
+                        const double v = fx ? 0.0 : -x[i];
+                        lds[C::F_KK + i * 2 * NX + c] = v;
+                        wb.st((g + i * NX) * WAVE * 8, ts * 8, v);
+                    }
+                }
+                if (lane < NU * NU) {
+                    double v = 0.0;
+#pragma unroll
+                    for (int e = 0; e < NU * NU; ++e) {
+                        const int ei = e / NU, ej = e % NU;
+                        v = fma(qp_mask(e, lane), (ei > ej) ? Lm[e] : (ei == ej ? dinv[ei] : 0.0), v);
+                    }
+                    wb.st((C::C_LD + lane) * WAVE * 8, ts * 8, v);
+                }
+            }
+            wsync();
+            // ---- phase 4: P = Qh + Sh'K, Pi = W1 + Sh'kappa, M += W2'kappa, Acl = A + Bt K
+#pragma unroll
+            for (int rep = 0; rep < R4; ++rep) run_desc(d4[rep], qp_dot<NU>(lds, d4[rep][0], d4[rep][1], soff), soff, last, ts);
+            if (ts > 0) pf_store((ts - 1) & 1);
+            wsync();
+        }
+        if (bad) lds[V_FLAG] = 1.0;  // any lane (all agree)
+        wsync();
+        // Pi_0 -> persistent; LU with partial pivoting of M (lane 0, registers)
+        for (int e = lane; e < NX * NX; e += WAVE) lds[V_PI0 + e] = lds[C::F_PIP + e];
+        if (fin && lane == 0) {
+            double Mr[NX * NX];
+#pragma unroll
+            for (int e = 0; e < NX * NX; ++e) Mr[e] = lds[V_M + e];
+#pragma unroll
+            for (int k = 0; k < NX; ++k) {
+                int p = k;
+                double best = fabs(Mr[k * NX + k]);
+#pragma unroll
+                for (int i = k + 1; i < NX; ++i) {
+                    const double v = fabs(Mr[i * NX + k]);
+                    if (v > best) { best = v; p = i; }
+                }
+                lds[V_PIV + k] = (double)p;
+#pragma unroll
+                for (int i = k + 1; i < NX; ++i) {
+                    const double m = qp_mask(i, p);
+#pragma unroll
+                    for (int j = 0; j < NX; ++j) {
+                        const double dlt = m * (Mr[i * NX + j] - Mr[k * NX + j]);
+                        Mr[k * NX + j] += dlt;
+                        Mr[i * NX + j] -= dlt;
+                    }
+                }
+                const double d = Mr[k * NX + k];
+                if (d == 0.0 || d != d) lds[V_FLAG] = 2.0;
+                const double inv = d != 0.0 ? 1.0 / d : 0.0;
+#pragma unroll
+                for (int i = k + 1; i < NX; ++i) {
+                    const double f = Mr[i * NX + k] * inv;
+                    Mr[i * NX + k] = f;
+#pragma unroll
+                    for (int j = k + 1; j < NX; ++j) Mr[i * NX + j] -= f * Mr[k * NX + j];
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < NX * NX; ++e) lds[V_M + e] = Mr[e];
+        }
+        wsync();
+        return lds[V_FLAG] == 0.0;
+    };
+
+    // ------------------------------------------------------------------ solve (one Newton rhs)
+    // In: q (NX), r (NU) of this node (registers), e (packet), V_XI0 / V_R2F (LDS).
+    // Out: dzo (NZ) = (dx_t, du_t), dyo (NX) = dy_t of this lane; V_DYI / V_DYF (LDS) the
+    // initial / terminal multiplier directions.
+    auto solve = [&](const double* q, const double* r, double* dzo, double* dyo) __attribute__((always_inline)) {
+        __syncthreads();  // factor columns were written by other lanes (global)
+        // ---- backward pre-pass: g = q + K'r + Acl'(P_{t+1} e)
+        if (act) {
+            double g[NX];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) g[i] = q[i];
+#pragma unroll
+            for (int i = 0; i < NU; ++i)
+#pragma unroll
+                for (int j = 0; j < NX; ++j) g[j] = fma(cld(C::C_K + i * NX + j), r[i], g[j]);
+            double* pk = lds + S_PK + t * PKS;
+            if (t < K - 1) {
+                double u[NX];
+#pragma unroll
+                for (int i = 0; i < NX; ++i) u[i] = cld(C::C_U + i);
+#pragma unroll
+                for (int i = 0; i < NX; ++i)
+#pragma unroll
+                    for (int j = 0; j < NX; ++j) {
+                        const double v = cld(C::C_ACL + i * NX + j);
+                        pk[i * NX + j] = v;
+                        g[j] = fma(v, u[i], g[j]);
+                    }
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) pk[NX * NX + i] = g[i];
+        }
+        wsync();
+        // ---- backward chain p_t = Acl_t' p_{t+1} + g_t (lane i: element i)
+        if (lane < NX) {
+            double p = lds[S_PK + (K - 1) * PKS + NX * NX + lane];
+            lds[V_CH + (K - 1) * NX + lane] = p;
+            for (int ts = K - 2; ts >= 0; --ts) {
+                const double* pk = lds + S_PK + ts * PKS;
+                double v = pk[NX * NX + lane];
+                wsync();
+#pragma unroll
+                for (int k = 0; k < NX; ++k) v = fma(pk[k * NX + lane], lds[V_CH + (ts + 1) * NX + k], v);
+                lds[V_CH + ts * NX + lane] = v;
+            }
+        }
+        wsync();
+        // ---- backward post-pass: k0 = -Rh^-1 (r + Bt'(P_{t+1} e + p_{t+1})), xacc = sum W2'k0
+        double k0[NU], pv[NX], xa[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) { xa[i] = 0.0; pv[i] = 0.0; }
+#pragma unroll
+        for (int j = 0; j < NU; ++j) k0[j] = 0.0;
+        if (act) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) pv[i] = lds[V_CH + t * NX + i];
+            double rh[NU];
+#pragma unroll
+            for (int j = 0; j < NU; ++j) rh[j] = r[j];
+            if (t < K - 1) {
+#pragma unroll
+                for (int i = 0; i < NX; ++i) {
+                    const double h = cld(C::C_U + i) + lds[V_CH + (t + 1) * NX + i];
+#pragma unroll
+                    for (int j = 0; j < NU; ++j) rh[j] = fma(cld(C::C_BT + i * NU + j), h, rh[j]);
+                }
+            }
+            double Ld[NU * NU];
+#pragma unroll
+            for (int e = 0; e < NU * NU; ++e) Ld[e] = cld(C::C_LD + e);
+#pragma unroll
+            for (int i = 0; i < NU; ++i) {
+                double v = rh[i];
+#pragma unroll
+                for (int k = 0; k < i; ++k) v -= Ld[i * NU + k] * k0[k];
+                k0[i] = v;
+            }
+#pragma unroll
+            for (int i = 0; i < NU; ++i) k0[i] *= Ld[i * NU + i];
+#pragma unroll
+            for (int i = NU - 1; i >= 0; --i) {
+                double v = k0[i];
+#pragma unroll
+                for (int k = i + 1; k < NU; ++k) v -= Ld[k * NU + i] * k0[k];
+                k0[i] = v;
+            }
+#pragma unroll
+            for (int i = 0; i < NU; ++i) k0[i] = fixed_u ? 0.0 : -k0[i];
+#pragma unroll
+            for (int i = 0; i < NU; ++i)
+#pragma unroll
+                for (int j = 0; j < NX; ++j) xa[j] = fma(cld(C::C_W2 + i * NX + j), k0[i], xa[j]);
+        }
+        // ---- terminal multiplier mu = M^-1 (r2f - xacc - xe - Pi_0' xi0)   (every lane)
+        double mu[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            double v = lds[V_R2F + i] - wave_sum(xa[i]) - lds[V_XE + i];
+#pragma unroll
+            for (int k = 0; k < NX; ++k) v -= lds[V_PI0 + k * NX + i] * lds[V_XI0 + k];
+            mu[i] = fin ? v : 0.0;
+        }
+        if (fin) {
+#pragma unroll
+            for (int k = 0; k < NX; ++k) {
+                const int p = (int)lds[V_PIV + k];
+#pragma unroll
+                for (int i = k + 1; i < NX; ++i) {
+                    const double dlt = qp_mask(i, p) * (mu[i] - mu[k]);
+                    mu[k] += dlt;
+                    mu[i] -= dlt;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < NX; ++k)
+#pragma unroll
+                for (int i = k + 1; i < NX; ++i) mu[i] -= lds[V_M + i * NX + k] * mu[k];
+#pragma unroll
+            for (int i = NX - 1; i >= 0; --i) {
+                double v = mu[i];
+#pragma unroll
+                for (int j = i + 1; j < NX; ++j) v -= lds[V_M + i * NX + j] * mu[j];
+                mu[i] = v / lds[V_M + i * NX + i];
+            }
+        }
+        // ---- forward pre-pass: v0 = k0 + kappa mu, f = Bt v0 + e, pi = Pi_t mu
+        double v0[NU], piv[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) piv[i] = 0.0;
+#pragma unroll
+        for (int j = 0; j < NU; ++j) v0[j] = k0[j];
+        wsync();  // the chain vectors above are read; the packets are rewritten below
+        if (act) {
+#pragma unroll
+            for (int i = 0; i < NU; ++i)
+#pragma unroll
+                for (int j = 0; j < NX; ++j) v0[i] = fma(cld(C::C_KAP + i * NX + j), mu[j], v0[i]);
+#pragma unroll
+            for (int i = 0; i < NX; ++i)
+#pragma unroll
+                for (int j = 0; j < NX; ++j) piv[i] = fma(cld(C::C_PI + i * NX + j), mu[j], piv[i]);
+            if (t < K - 1) {
+                double* pk = lds + S_PK + t * PKS;
+#pragma unroll
+                for (int i = 0; i < NX; ++i) {
+                    double f = wb.ld(vpk, PKB + (C::P_E + i) * 8);
+#pragma unroll
+                    for (int j = 0; j < NU; ++j) f = fma(cld(C::C_BT + i * NU + j), v0[j], f);
+                    pk[NX * NX + i] = f;
+                }
+#pragma unroll
+                for (int e = 0; e < NX * NX; ++e) pk[e] = cld(C::C_ACL + e);
+            }
+        }
+        wsync();
+        // ---- forward chain xi_{t+1} = Acl_t xi_t + f_t
+        if (lane < NX) {
+            double x = lds[V_XI0 + lane];
+            lds[V_CH + lane] = x;
+            for (int ts = 0; ts < K - 1; ++ts) {
+                const double* pk = lds + S_PK + ts * PKS;
+                double v = pk[NX * NX + lane];
+                wsync();
+#pragma unroll
+                for (int k = 0; k < NX; ++k) v = fma(pk[lane * NX + k], lds[V_CH + ts * NX + k], v);
+                lds[V_CH + (ts + 1) * NX + lane] = v;
+            }
+        }
+        wsync();
+        // ---- forward post-pass: du = K xi + v0, dx = xi + C_{t-1} du, y_{t-1} = -(P xi + p + pi)
+        double ym[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) ym[i] = 0.0;
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) dzo[i] = 0.0;
+        if (act) {
+            double xi[NX], Cp[NX * NU];
+            load_cp(Cp);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) xi[i] = lds[V_CH + t * NX + i];
+            double du[NU];
+#pragma unroll
+            for (int j = 0; j < NU; ++j) {
+                double v = v0[j];
+#pragma unroll
+                for (int k = 0; k < NX; ++k) v = fma(cld(C::C_K + j * NX + k), xi[k], v);
+                du[j] = fixed_u ? 0.0 : v;
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                double dx = xi[i];
+#pragma unroll
+                for (int j = 0; j < NU; ++j) dx = fma(Cp[j * NX + i], du[j], dx);
+                dzo[i] = dx;
+                double y = pv[i] + piv[i];
+#pragma unroll
+                for (int k = 0; k < NX; ++k) y = fma(cld(C::C_P + i * NX + k), xi[k], y);
+                ym[i] = -y;
+            }
+#pragma unroll
+            for (int j = 0; j < NU; ++j) dzo[NX + j] = du[j];
+        }
+        // lane t computed y_{t-1}: lane t owns y_t (from lane t+1); lane 0's is the initial multiplier
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            const double nxt = __shfl_down(ym[i], 1, WAVE);
+            dyo[i] = (t < K - 1) ? nxt : 0.0;
+            if (lane == 0) { lds[V_DYI + i] = ym[i]; lds[V_DYF + i] = mu[i]; }
+        }
+    };
+
+    // ------------------------------------------------------------------ state
+    double z[NZ], y[NX], s[NR], l[NR], sq[NQ], lq[NQ], av[NGA];
+#pragma unroll
+    for (int i = 0; i < NX; ++i) { z[i] = act ? a.Xref[(agent * K + t) * NX + i] : 0.0; y[i] = 0.0; }
+#pragma unroll
+    for (int j = 0; j < NU; ++j) z[NX + j] = ub[j];
+#pragma unroll
+    for (int g = 0; g < NGA; ++g) av[g] = 0.0;
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) { sq[j] = 0.0; lq[j] = 0.0; }
+    if (lane < NX) { lds[V_YI + lane] = 0.0; lds[V_YF + lane] = 0.0; }
+    __syncthreads();
+
+    // ------------------------------------------------------------------ node-phase helpers
+    // soft rows (registers, reloaded per node phase)
+    double sg[NSA][3], sb[NSA];
+    auto load_soft = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) sg[q][i] = cld(C::C_SOFT + q * 4 + i);
+            sb[q] = cld(C::C_SOFT + q * 4 + 3);
+        }
+    };
+    auto grp_on = [&](int g) __attribute__((always_inline)) -> bool { return ineq && (g < NO ? g < nobs : has_coll); };
+    auto row_on = [&](int r) __attribute__((always_inline)) -> bool {
+        if (r < C::R_BOX) return ineq;
+        if (r < C::R_OBS) return ineq && ((r - C::R_BOX) >> 1) < nbox;
+        if (r < C::R_COL) return ineq && (r - C::R_OBS) < nobs;
+        if (r < C::R_GRP) return (r - C::R_COL) < ccount;
+        return grp_on(r - C::R_GRP);
+    };
+    auto sel_x = [&](const double* zz, int idx) __attribute__((always_inline)) -> double {
+        double v = 0.0;
+#pragma unroll
+        for (int i = 0; i < NX; ++i) v = fma(qp_mask(i, idx), zz[i], v);
+        return v;
+    };
+    // G_r [z; a] and h_r of row r (static after unrolling)
+    auto row_eval = [&](int r, const double* zz, const double* aa, double& gz, double& h) __attribute__((always_inline)) {
+        if (r < C::R_BOX) {
+            gz = 0.0; h = trv;
+#pragma unroll
+            for (int j = 0; j < NU; ++j) {
+                const bool neg = (r >> j) & 1;
+                gz += neg ? -zz[NX + j] : zz[NX + j];
+                h += neg ? -ub[j] : ub[j];
+            }
+        } else if (r < C::R_OBS) {
+            const int b = (r - C::R_BOX) >> 1, lo = (r - C::R_BOX) & 1;
+            const double xi = sel_x(zz, T.box_idx[b]);
+            gz = lo ? -xi : xi; h = lo ? -T.box_lo[b] : T.box_hi[b];
+        } else if (r < C::R_GRP) {
+            const int q = r - C::R_OBS, g = q < NO ? q : NO;
+            gz = -(sg[q][0] * zz[0] + sg[q][1] * zz[1] + sg[q][2] * zz[2]) - aa[g];
+            h = -sb[q];
+        } else {
+            gz = -aa[r - C::R_GRP]; h = 0.0;
+        }
+    };
+    // gzv += c G_r'|_z, gav += c G_r'|_a
+    auto row_accT = [&](int r, double c, double* gzv, double* gav) __attribute__((always_inline)) {
+        if (r < C::R_BOX) {
+#pragma unroll
+            for (int j = 0; j < NU; ++j) gzv[NX + j] += ((r >> j) & 1) ? -c : c;
+        } else if (r < C::R_OBS) {
+            const int b = (r - C::R_BOX) >> 1, lo = (r - C::R_BOX) & 1, idx = T.box_idx[b];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) gzv[i] = fma(qp_mask(i, idx), lo ? -c : c, gzv[i]);
+        } else if (r < C::R_GRP) {
+            const int q = r - C::R_OBS, g = q < NO ? q : NO;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) gzv[i] -= c * sg[q][i];
+            gav[g] -= c;
+        } else {
+            gav[r - C::R_GRP] -= c;
+        }
+    };
+    // gav += c G_r'|_a (group part only)
+    auto row_accA = [&](int r, double c, double* gav) __attribute__((always_inline)) {
+        if (r >= C::R_OBS && r < C::R_GRP) {
+            const int q = r - C::R_OBS;
+            gav[q < NO ? q : NO] -= c;
+        } else if (r >= C::R_GRP) {
+            gav[r - C::R_GRP] -= c;
+        }
+    };
+    auto gweight = [&](int g) __attribute__((always_inline)) -> double { return g < NO ? T.w_obs : T.w_coll; };
+
+    // Node Hessian (row scaling D_r, SOC block Wi2uu) -> packet Q, S, R (xi/u coordinates); group
+    // elimination factors -> columns C_GRP.  Also writes e = -rp into the packet.
+    auto assemble = [&](bool unit, const double* Wi2uu, const double* rp) __attribute__((always_inline)) {
+        double dbox[NX], Hpp[3][3], Huu[NU * NU];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) dbox[i] = 0.0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) Hpp[i][0] = Hpp[i][1] = Hpp[i][2] = 0.0;
+#pragma unroll
+        for (int i = 0; i < NU; ++i)
+#pragma unroll
+            for (int j = 0; j < NU; ++j) Huu[i * NU + j] = (i == j ? 2.0 * wu : 0.0) + (soc ? Wi2uu[i * NU + j] : 0.0);
+        double Haa[NGA], Hpa[NGA][3];
+#pragma unroll
+        for (int g = 0; g < NGA; ++g) { Haa[g] = 0.0; Hpa[g][0] = Hpa[g][1] = Hpa[g][2] = 0.0; }
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const double Dr = row_on(r) ? (unit ? 1.0 : l[r] / s[r]) : 0.0;
+            if (r < C::R_BOX) {
+#pragma unroll
+                for (int i = 0; i < NU; ++i)
+#pragma unroll
+                    for (int j = 0; j < NU; ++j) Huu[i * NU + j] += (((r >> i) ^ (r >> j)) & 1) ? -Dr : Dr;
+            } else if (r < C::R_OBS) {
+                const int idx = T.box_idx[(r - C::R_BOX) >> 1];
+#pragma unroll
+                for (int i = 0; i < NX; ++i) dbox[i] = fma(qp_mask(i, idx), Dr, dbox[i]);
+            } else if (r < C::R_GRP) {
+                const int q = r - C::R_OBS, g = q < NO ? q : NO;
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) Hpp[i][j] += Dr * sg[q][i] * sg[q][j];
+                Haa[g] += Dr;
+#pragma unroll
+                for (int i = 0; i < 3; ++i) Hpa[g][i] += Dr * sg[q][i];
+            } else {
+                Haa[r - C::R_GRP] += Dr;
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const bool on = grp_on(g);
+            const double ih = on ? 1.0 / Haa[g] : 0.0;
+            double hp[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { hp[i] = Hpa[g][i] * ih; cst(C::C_GRP + g * 4 + i, hp[i]); }
+            cst(C::C_GRP + g * 4 + 3, ih);
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) Hpp[i][j] -= hp[i] * Hpa[g][j];
+        }
+        if (!act) return;
+        double Q[NX * NX], Cp[NX * NU];
+        load_cp(Cp);
+#pragma unroll
+        for (int i = 0; i < NX; ++i)
+#pragma unroll
+            for (int j = 0; j < NX; ++j) {
+                double v = (i == j) ? dbox[i] : 0.0;
+                if (i < 3 && j < 3) v += Hpp[i < 3 ? i : 0][j < 3 ? j : 0];
+                Q[i * NX + j] = v;
+                pst(C::P_Q + i * NX + j, v);
+            }
+        double Sx[NX * NU];
+#pragma unroll
+        for (int i = 0; i < NX; ++i)
+#pragma unroll
+            for (int j = 0; j < NU; ++j) {
+                double v = 0.0;
+#pragma unroll
+                for (int k = 0; k < NX; ++k) v = fma(Q[i * NX + k], Cp[j * NX + k], v);
+                Sx[i * NU + j] = v;
+                pst(C::P_S + i * NU + j, v);
+            }
+#pragma unroll
+        for (int i = 0; i < NU; ++i)
+#pragma unroll
+            for (int j = 0; j < NU; ++j) {
+                double v = Huu[i * NU + j];
+#pragma unroll
+                for (int k = 0; k < NX; ++k) v = fma(Cp[i * NX + k], Sx[k * NU + j], v);
+                pst(C::P_R + i * NU + j, v);
+            }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) pst(C::P_E + i, (t < K - 1) ? -rp[i] : 0.0);
+    };
+    // eliminate the group part of a Newton rhs: r1_p -= sum_g Hpa_g r1a_g / Haa_g ; returns the
+    // (xi, u) linear terms q, r of the node
+    auto reduce_rhs = [&](double* r1, const double* r1a, double* q, double* r) __attribute__((always_inline)) {
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            cst(C::C_R1A + g, r1a[g]);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) r1[i] -= cld(C::C_GRP + g * 4 + i) * r1a[g];
+        }
+        if (fixed_u) {
+#pragma unroll
+            for (int j = 0; j < NU; ++j) r1[NX + j] = 0.0;
+        }
+        double Cp[NX * NU];
+        load_cp(Cp);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) q[i] = -r1[i];
+#pragma unroll
+        for (int j = 0; j < NU; ++j) {
+            double v = r1[NX + j];
+#pragma unroll
+            for (int k = 0; k < NX; ++k) v = fma(Cp[j * NX + k], r1[k], v);
+            r[j] = fixed_u ? 0.0 : -v;
+        }
+    };
+    // group directions: da_g = (r1a_g - Hpa_g' dp) / Haa_g
+    auto recover_aux = [&](const double* dzl, double* da) __attribute__((always_inline)) {
+#pragma unroll
+        for (int g = 0; g < NGA; ++g) da[g] = 0.0;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            double v = cld(C::C_R1A + g) * cld(C::C_GRP + g * 4 + 3);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) v -= cld(C::C_GRP + g * 4 + i) * dzl[i];
+            da[g] = grp_on(g) ? v : 0.0;
+        }
+    };
+    auto set_boundary = [&](const double* zz) __attribute__((always_inline)) {
+        // lane 0 holds z_0, lane K-1 holds z_{K-1}
+        if (t == 0) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) lds[V_XI0 + i] = a.x_init[agent * NX + i] - zz[i];
+        }
+        if (t == K - 1) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) lds[V_R2F + i] = fin ? a.x_final[agent * NX + i] - zz[i] : 0.0;
+        }
+    };
+    // dynamics residual rp_t = x_{t+1} - A x_t - B u_t - C u_{t+1} - S sigma - z  (lane t < K-1)
+    auto dyn_residual = [&](const double* zz, double* rp) __attribute__((always_inline)) {
+        double zn[NZ];
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) zn[i] = __shfl_down(zz[i], 1, WAVE);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            double v = zn[i] - fma(cld(C::C_DT + NX * NX + 2 * NX * NU + i), sig, cld(C::C_DT + NX * NX + 2 * NX * NU + NX + i));
+#pragma unroll
+            for (int k = 0; k < NX; ++k) v -= cld(C::C_DT + k * NX + i) * zz[k];
+#pragma unroll
+            for (int j = 0; j < NU; ++j)
+                v -= cld(C::C_DT + NX * NX + j * NX + i) * zz[NX + j] + cld(C::C_DT + NX * NX + NX * NU + j * NX + i) * zn[NX + j];
+            rp[i] = (t < K - 1) ? v : 0.0;
+        }
+    };
+    auto soc_step = [&](const double* x, const double* dx) __attribute__((always_inline)) {
+        double qa = dx[0] * dx[0], qb = x[0] * dx[0], qc = x[0] * x[0];
+#pragma unroll
+        for (int j = 1; j < NQ; ++j) { qa -= dx[j] * dx[j]; qb -= x[j] * dx[j]; qc -= x[j] * x[j]; }
+        qb *= 2.0;
+        double best = 1e300;
+        if (fabs(qa) < 1e-300) {
+            if (qb < 0) best = fmin(best, -qc / qb);
+        } else {
+            const double disc_ = qb * qb - 4 * qa * qc;
+            if (disc_ >= 0) {
+                const double sqd = sqrt(disc_), q1 = (-qb - sqd) / (2 * qa), q2 = (-qb + sqd) / (2 * qa);
+                if (q1 > 0) best = fmin(best, q1);
+                if (q2 > 0) best = fmin(best, q2);
+            }
+        }
+        if (dx[0] < 0) best = fmin(best, -x[0] / dx[0]);
+        return best;
+    };
+    // NT scaling W = eta [[w0, w1'], [w1, I + w1 w1'/(1 + w0)]], W^-1 the same with -w1, 1/eta
+    auto w_apply = [&](const double* w, double eta, bool inv, const double* x, double* y) __attribute__((always_inline)) {
+        const double sgn = inv ? -1.0 : 1.0, sc = inv ? 1.0 / eta : eta;
+        double d = 0.0;
+#pragma unroll
+        for (int j = 1; j < NQ; ++j) d += w[j] * x[j];
+        d *= sgn;
+        y[0] = sc * (w[0] * x[0] + d);
+        const double f = x[0] + d / (1.0 + w[0]);
+#pragma unroll
+        for (int j = 1; j < NQ; ++j) y[j] = sc * (x[j] + sgn * w[j] * f);
+    };
+
+    int status = SCVX_STATUS_MAX_ITER;
+    int it = 0;
+    double fail_code = 0.0;
+    // ------------------------------------------------------------------ starting point
+    // minimiser of 1/2 z'Pz + q'z + 1/2 ||Gz - h||^2 s.t. Az = b from z_ref (aux = 0), unit scaling
+    // (CVXOPT coneqp initialisation; oracle/qp_dense.py does the same on the dense form)
+    {
+        load_soft();
+        double Wu[NU * NU], rp[NX];
+#pragma unroll
+        for (int e = 0; e < NU * NU; ++e) Wu[e] = (e / NU == e % NU) ? 1.0 : 0.0;
+        dyn_residual(z, rp);
+        assemble(true, Wu, rp);
+        double r1[NZ], r1a[NGA];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) r1[i] = 0.0;
+#pragma unroll
+        for (int j = 0; j < NU; ++j) r1[NX + j] = -2.0 * wu * z[NX + j] - (soc ? z[NX + j] : 0.0);
+#pragma unroll
+        for (int g = 0; g < NGA; ++g) r1a[g] = -gweight(g);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            double gz, h;
+            row_eval(r, z, av, gz, h);
+            if (row_on(r)) row_accT(r, -(gz - h), r1, r1a);
+        }
+        double q[NX], rr[NU];
+        reduce_rhs(r1, r1a, q, rr);
+        set_boundary(z);
+        if (!factor()) status = SCVX_STATUS_NUMERICAL;
+        double dz[NZ], dy[NX], da[NGA];
+        solve(q, rr, dz, dy);
+        recover_aux(dz, da);
+        load_soft();
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) z[i] += act ? dz[i] : 0.0;
+#pragma unroll
+        for (int g = 0; g < NGA; ++g) av[g] += da[g];
+        double smin = 1e300, lmin = 1e300;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            double gz, h;
+            row_eval(r, z, av, gz, h);
+            const bool on = row_on(r);
+            s[r] = on ? h - gz : 1.0;
+            l[r] = on ? gz - h : 0.0;
+            if (on) { smin = fmin(smin, h - gz); lmin = fmin(lmin, gz - h); }
+        }
+        if (soc) {
+            double nu2 = 0.0;
+            sq[0] = T.u_max; lq[0] = -T.u_max;
+#pragma unroll
+            for (int j = 0; j < NU; ++j) { sq[1 + j] = z[NX + j]; lq[1 + j] = -z[NX + j]; nu2 += z[NX + j] * z[NX + j]; }
+            smin = fmin(smin, T.u_max - sqrt(nu2));
+            lmin = fmin(lmin, -T.u_max - sqrt(nu2));
+        }
+        smin = wave_min(smin); lmin = wave_min(lmin);
+        const double shs = fmax(0.0, 1.0 - smin), shl = fmax(0.0, 1.0 - lmin);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            if (row_on(r)) { s[r] += shs; l[r] += shl; }
+        }
+        if (soc) { sq[0] += shs; lq[0] += shl; }
+    }
+    double degl = 0.0;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) degl += row_on(r) ? 1.0 : 0.0;
+    degl += soc ? 1.0 : 0.0;
+    const double deg = fmax(wave_sum(degl), 1.0);
+    const double tol = T.tol > 0 ? T.tol : 1e-9;
+    double qscl = 1.0;  // max objective weight
+    if (nobs > 0) qscl = fmax(qscl, T.w_obs);
+    if (has_coll) qscl = fmax(qscl, T.w_coll);
+
+    // ------------------------------------------------------------------ IPM iterations
+    long long cyc_factor = 0, cyc_solve = 0, cyc_all0 = __builtin_amdgcn_s_memtime();
+    for (it = 0; it < T.max_iter && status != SCVX_STATUS_NUMERICAL; ++it) {
+        load_soft();
+        double rp[NX];
+        dyn_residual(z, rp);
+        // dual residual rd = Pz + q + A'y + G'lam (z and group parts)
+        double rd[NZ], rda[NGA];
+        double pres = 0.0, dres = 0.0, gap = 0.0, hsc = 1.0, pobj = 0.0;
+#pragma unroll
+        for (int i = 0; i < NX; ++i) pres = fmax(pres, fabs(rp[i]));
+        if (t == 0) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) pres = fmax(pres, fabs(z[i] - a.x_init[agent * NX + i]));
+        }
+        if (act && t == K - 1 && fin) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) pres = fmax(pres, fabs(z[i] - a.x_final[agent * NX + i]));
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) rd[i] = 0.0;
+#pragma unroll
+        for (int j = 0; j < NU; ++j) rd[NX + j] = 2.0 * wu * z[NX + j];
+#pragma unroll
+        for (int g = 0; g < NGA; ++g) rda[g] = gweight(g);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            double gz, h;
+            row_eval(r, z, av, gz, h);
+            if (row_on(r)) {
+                const double rcr = gz + s[r] - h;
+                pres = fmax(pres, fabs(rcr));
+                hsc = fmax(hsc, fabs(h));
+                gap += s[r] * l[r];
+                row_accT(r, l[r], rd, rda);
+            }
+        }
+        double rcq[NQ];
+        if (soc) {
+            rcq[0] = sq[0] - T.u_max;
+#pragma unroll
+            for (int j = 0; j < NU; ++j) { rcq[1 + j] = sq[1 + j] - z[NX + j]; rd[NX + j] -= lq[1 + j]; }
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) { pres = fmax(pres, fabs(rcq[j])); gap += sq[j] * lq[j]; }
+            hsc = fmax(hsc, T.u_max);
+        } else {
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) rcq[j] = 0.0;
+        }
+        {
+            // dynamics multipliers: y_{t-1} from lane t-1
+            double ym[NX];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) ym[i] = __shfl_up(y[i], 1, WAVE);
+            if (act) {
+                if (t == 0) {
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) rd[i] += lds[V_YI + i];
+                }
+                if (t == K - 1 && fin) {
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) rd[i] += lds[V_YF + i];
+                }
+                if (t >= 1) {
+                    double Cp[NX * NU];
+                    load_cp(Cp);
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) rd[i] += ym[i];
+#pragma unroll
+                    for (int j = 0; j < NU; ++j)
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) rd[NX + j] -= Cp[j * NX + i] * ym[i];
+                }
+                if (t < K - 1) {
+#pragma unroll
+                    for (int k = 0; k < NX; ++k)
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) rd[k] -= cld(C::C_DT + k * NX + i) * y[i];
+#pragma unroll
+                    for (int j = 0; j < NU; ++j)
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) rd[NX + j] -= cld(C::C_DT + NX * NX + j * NX + i) * y[i];
+                }
+                if (fixed_u) {
+#pragma unroll
+                    for (int j = 0; j < NU; ++j) rd[NX + j] = 0.0;
+                }
+#pragma unroll
+                for (int i = 0; i < NZ; ++i) { dres = fmax(dres, fabs(rd[i])); cst(C::C_RD + i, rd[i]); }
+#pragma unroll
+                for (int g = 0; g < NG; ++g) {
+                    if (grp_on(g)) { dres = fmax(dres, fabs(rda[g])); pobj += gweight(g) * av[g]; }
+                }
+#pragma unroll
+                for (int j = 0; j < NU; ++j) pobj += wu * z[NX + j] * z[NX + j];
+            }
+        }
+        pres = wave_max(pres); dres = wave_max(dres); hsc = wave_max(hsc);
+        gap = wave_sum(gap); pobj = wave_sum(pobj);
+        const double mu = gap / deg;
+        if (!isfinite(pres + dres + mu)) { status = SCVX_STATUS_NUMERICAL; fail_code = 3.0; break; }
+        if (pres <= tol * hsc && dres <= tol * qscl && gap <= tol * fmax(1.0, fabs(pobj))) {
+            status = SCVX_STATUS_OPTIMAL;
+            break;
+        }
+        // ECOS-style reduced accuracy: what a numerical breakdown below leaves is still usable
+        const bool near = pres <= 1e-6 * hsc && dres <= 1e-6 * qscl && gap <= 1e-6 * fmax(1.0, fabs(pobj));
+        // SOC Nesterov-Todd scaling (hyperbolic-rotation form, W lam = W^-1 s)
+        double wv[NQ], eta = 1.0, ltq[NQ], Wi2uu[NU * NU];
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) { wv[j] = 0.0; ltq[j] = 0.0; }
+#pragma unroll
+        for (int e = 0; e < NU * NU; ++e) Wi2uu[e] = 0.0;
+        if (soc) {
+            double n1s = 0.0, n1z = 0.0;
+#pragma unroll
+            for (int j = 1; j < NQ; ++j) { n1s += sq[j] * sq[j]; n1z += lq[j] * lq[j]; }
+            n1s = sqrt(n1s); n1z = sqrt(n1z);
+            const double Js = fmax((sq[0] - n1s) * (sq[0] + n1s), 1e-300), Jz = fmax((lq[0] - n1z) * (lq[0] + n1z), 1e-300);
+            const double ns = sqrt(Js), nz = sqrt(Jz);
+            double sbv[NQ], zbv[NQ], dot = 0.0;
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) { sbv[j] = sq[j] / ns; zbv[j] = lq[j] / nz; dot += sbv[j] * zbv[j]; }
+            const double gam = sqrt((1.0 + dot) / 2.0);
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) wv[j] = (sbv[j] + (j == 0 ? zbv[j] : -zbv[j])) / (2.0 * gam);
+            eta = sqrt(sqrt(Js / Jz));
+            w_apply(wv, eta, false, lq, ltq);
+            // (W^-2)_uu = rows/cols 1.. of W^-1 W^-1
+            double Wi[NQ * NQ];
+#pragma unroll
+            for (int c = 0; c < NQ; ++c) {
+                double ec[NQ], col[NQ];
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) ec[j] = (j == c) ? 1.0 : 0.0;
+                w_apply(wv, eta, true, ec, col);
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) Wi[j * NQ + c] = col[j];
+            }
+#pragma unroll
+            for (int i = 0; i < NU; ++i)
+#pragma unroll
+                for (int j = 0; j < NU; ++j) {
+                    double v = 0.0;
+#pragma unroll
+                    for (int k = 0; k < NQ; ++k) v += Wi[(1 + i) * NQ + k] * Wi[k * NQ + 1 + j];
+                    Wi2uu[i * NU + j] = v;
+                }
+        }
+        assemble(false, Wi2uu, rp);
+        set_boundary(z);
+        long long st0 = __builtin_amdgcn_s_memtime();
+        if (!factor()) { status = near ? SCVX_STATUS_MAX_ITER : SCVX_STATUS_NUMERICAL; fail_code = lds[V_FLAG]; break; }
+        cyc_factor += __builtin_amdgcn_s_memtime() - st0;
+
+        // Newton direction for complementarity rhs rco (rows) / rcq2 (SOC); directions out
+        double dz[NZ], dy[NX], da[NGA], dsq[NQ], dlq[NQ], rho[NQ];
+        // complementarity rhs of row r: predictor -s l ; corrector -s l - ds_a dl_a + sigma mu
+        double sgmu = 0.0;
+        auto rco_of = [&](int r, bool corr) __attribute__((always_inline)) -> double {
+            const double v = -s[r] * l[r];
+            return corr ? v - lds[V_CP + r * WAVE + lane] + sgmu : v;
+        };
+        auto newton = [&](bool corr, const double* rcq2) __attribute__((always_inline)) {
+            load_soft();
+            double r1[NZ], r1a[NGA];
+#pragma unroll
+            for (int i = 0; i < NZ; ++i) r1[i] = act ? -cld(C::C_RD + i) : 0.0;
+#pragma unroll
+            for (int g = 0; g < NGA; ++g) r1a[g] = -gweight(g);
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                if (row_on(r)) {
+                    double gz, h;
+                    row_eval(r, z, av, gz, h);
+                    const double rcr = gz + s[r] - h;
+                    row_accA(r, -l[r], r1a);  // -rd, group part: -(w_g - sum lambda)
+                    row_accT(r, -(rco_of(r, corr) + l[r] * rcr) / s[r], r1, r1a);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) rho[j] = 0.0;
+            if (soc) {
+                // rho = ltq o^-1 rcq2 ; u part of G'(W^-1 rho + W^-2 rcq) = -(...)[1:]
+                double J = ltq[0] * ltq[0], r0 = ltq[0] * rcq2[0], w2[NQ], w3[NQ];
+#pragma unroll
+                for (int j = 1; j < NQ; ++j) { J -= ltq[j] * ltq[j]; r0 -= ltq[j] * rcq2[j]; }
+                r0 /= J;
+                rho[0] = r0;
+#pragma unroll
+                for (int j = 1; j < NQ; ++j) rho[j] = (rcq2[j] - r0 * ltq[j]) / ltq[0];
+                w_apply(wv, eta, true, rcq, w2);
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) w2[j] += rho[j];
+                w_apply(wv, eta, true, w2, w3);
+#pragma unroll
+                for (int i = 0; i < NU; ++i) r1[NX + i] += w3[1 + i];
+            }
+            double q[NX], rr[NU];
+            reduce_rhs(r1, r1a, q, rr);
+            long long st1 = __builtin_amdgcn_s_memtime();
+            solve(q, rr, dz, dy);
+            cyc_solve += __builtin_amdgcn_s_memtime() - st1;
+            recover_aux(dz, da);
+            load_soft();
+            if (soc) {
+                double v2[NQ], w2[NQ];
+                dsq[0] = -rcq[0];
+                v2[0] = rcq[0];
+#pragma unroll
+                for (int j = 1; j < NQ; ++j) { dsq[j] = -rcq[j] + dz[NX + j - 1]; v2[j] = rcq[j] - dz[NX + j - 1]; }
+                w_apply(wv, eta, true, v2, w2);
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) w2[j] += rho[j];
+                w_apply(wv, eta, true, w2, dlq);
+            } else {
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) { dsq[j] = 0.0; dlq[j] = 0.0; }
+            }
+        };
+        // row directions ds = -rc - G d, dl = (rco + l (rc + G d)) / s
+        auto row_dir = [&](int r, bool corr, double& dsr, double& dlr) __attribute__((always_inline)) {
+            double gz, h, gd, h2;
+            row_eval(r, z, av, gz, h);
+            row_eval(r, dz, da, gd, h2);
+            const double rcr = gz + s[r] - h;
+            dsr = -rcr - gd;
+            dlr = (rco_of(r, corr) + l[r] * (rcr + gd)) / s[r];
+        };
+        auto max_step = [&](bool corr) __attribute__((always_inline)) {
+            double am = 1e300;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                if (row_on(r)) {
+                    double dsr, dlr;
+                    row_dir(r, corr, dsr, dlr);
+                    if (dsr < 0) am = fmin(am, -s[r] / dsr);
+                    if (dlr < 0) am = fmin(am, -l[r] / dlr);
+                }
+            }
+            if (soc) { am = fmin(am, soc_step(sq, dsq)); am = fmin(am, soc_step(lq, dlq)); }
+            return wave_min(am);
+        };
+
+        // ---- predictor (affine scaling)
+        double rcq2[NQ];
+        if (soc) {
+            double d0 = 0.0;
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) d0 += ltq[j] * ltq[j];
+            rcq2[0] = -d0;
+#pragma unroll
+            for (int j = 1; j < NQ; ++j) rcq2[j] = -2.0 * ltq[0] * ltq[j];
+        } else {
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) rcq2[j] = 0.0;
+        }
+        newton(false, rcq2);
+        const double aa = fmin(1.0, max_step(false));
+        double gap_a = 0.0;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            if (row_on(r)) {
+                double dsr, dlr;
+                row_dir(r, false, dsr, dlr);
+                gap_a += (s[r] + aa * dsr) * (l[r] + aa * dlr);
+                lds[V_CP + r * WAVE + lane] = dsr * dlr;
+            }
+        }
+        if (soc) {
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) gap_a += (sq[j] + aa * dsq[j]) * (lq[j] + aa * dlq[j]);
+        }
+        gap_a = wave_sum(gap_a);
+        const double mu_a = gap_a / deg;
+        const double sgm = mu > 0 ? pow(fmax(mu_a, 0.0) / mu, 3.0) : 0.0;
+        // ---- corrector
+        sgmu = sgm * mu;
+        if (soc) {
+            double a1[NQ], b1[NQ];
+            w_apply(wv, eta, true, dsq, a1);
+            w_apply(wv, eta, false, dlq, b1);
+            double d0 = 0.0;
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) d0 += a1[j] * b1[j];
+            rcq2[0] -= d0;
+#pragma unroll
+            for (int j = 1; j < NQ; ++j) rcq2[j] -= a1[0] * b1[j] + b1[0] * a1[j];
+            rcq2[0] += sgmu;
+        }
+        newton(true, rcq2);
+        const double al = fmin(1.0, 0.99 * max_step(true));
+        {
+            double chk = al;
+#pragma unroll
+            for (int i = 0; i < NZ; ++i) chk += 0.0 * dz[i];
+            chk = wave_sum(chk);  // NaN anywhere in the direction poisons the sum
+            if (!(chk == chk) || !(al > 0.0)) {
+                status = near ? SCVX_STATUS_MAX_ITER : SCVX_STATUS_NUMERICAL;
+                fail_code = 4.0;
+                break;
+            }
+        }
+        if (a.trace && agent == a.trace_agent && lane == 0 && it < a.trace_cap) {
+            double* tr_ = a.trace + 8 * it;
+            tr_[0] = pres; tr_[1] = dres; tr_[2] = gap; tr_[3] = pobj; tr_[4] = aa; tr_[5] = al; tr_[6] = sgm; tr_[7] = mu;
+        }
+        // ---- update
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            if (row_on(r)) {
+                double dsr, dlr;
+                row_dir(r, true, dsr, dlr);
+                s[r] += al * dsr;
+                l[r] += al * dlr;
+            }
+        }
+        if (act) {
+#pragma unroll
+            for (int i = 0; i < NZ; ++i) z[i] += al * dz[i];
+#pragma unroll
+            for (int g = 0; g < NGA; ++g) av[g] += al * da[g];
+            if (soc) {
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) { sq[j] += al * dsq[j]; lq[j] += al * dlq[j]; }
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) y[i] += al * dy[i];
+        }
+        if (lane < NX) {
+            lds[V_YI + lane] += al * lds[V_DYI + lane];
+            lds[V_YF + lane] += al * lds[V_DYF + lane];
+        }
+    }
+
+    // ------------------------------------------------------------------ outputs
+    if (a.trace && agent == a.trace_agent && lane == 0) {
+        double* dd = a.trace + 8 * a.trace_cap;
+        dd[0] = (double)cyc_factor; dd[1] = (double)cyc_solve; dd[2] = (double)(__builtin_amdgcn_s_memtime() - cyc_all0);
+        dd[3] = fail_code;
+    }
+    double pobj = 0.0;
+    if (act) {
+#pragma unroll
+        for (int i = 0; i < NX; ++i) a.X[(agent * K + t) * NX + i] = z[i];
+#pragma unroll
+        for (int j = 0; j < NU; ++j) { a.U[(agent * K + t) * NU + j] = z[NX + j]; pobj += wu * z[NX + j] * z[NX + j]; }
+#pragma unroll
+        for (int g = 0; g < NG; ++g) pobj += grp_on(g) ? gweight(g) * av[g] : 0.0;
+        a.slack_coll[agent * K + t] = (has_coll && ineq) ? av[NG > 0 ? NG - 1 : 0] : 0.0;
+    }
+    pobj = wave_sum(pobj);
+    if (lane == 0) {
+        a.obj[agent] = pobj;
+        a.status[agent] = status;
+        a.iters[agent] = it;
+    }
+}
+
+// launch helpers (qp_capi.hip picks the instantiation)
+template <class C>
+int qp_launch(const QPArgs& a, hipStream_t st) {
+    const size_t lds = sizeof(double) * (size_t)qp_lds_doubles(C::NX, C::NU, a.T.K, C::NR);
+    if (lds > 65536) (void)hipFuncSetAttribute((const void*)qp_ipm_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(qp_ipm_kernel<C>, dim3(a.N), dim3(WAVE), lds, st, a);
+    return check_launch("qp_ipm_kernel");
+}
+
+}  // namespace scvx

@@ -1,9 +1,8 @@
 // Wave-level helpers for one-agent-per-wavefront kernels (gfx950, wave64, float64).
 //
-// A workgroup is exactly one 64-lane wavefront, so __syncthreads() is a cheap s_barrier that
-// also orders LDS and global traffic between the lanes of the wave.  Small dense matrices
-// (<= 16x16) live in LDS row-major; element-parallel ops give every lane one (or a few) output
-// elements.
+// A workgroup is exactly one 64-lane wavefront.  LDS instructions of one wave execute in issue
+// order, so lanes of the wave exchange data through LDS without a hardware barrier: a phase
+// boundary only needs the compiler not to move LDS accesses across it (wsync).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -11,61 +10,46 @@ namespace scvx {
 
 constexpr int WAVE = 64;
 
-// LDS-only barrier for a one-wavefront workgroup.  __syncthreads() emits s_waitcnt vmcnt(0)
-// (it fences global memory too), which would drain every prefetch load and every store in flight
-// at each phase of a sequential sweep.  Lanes of one wave exchange data through LDS in issue
-// order, so a phase boundary only needs the LDS counter drained plus a compiler barrier.
+// Phase boundary inside a one-wave workgroup: a compiler-level LDS fence.  With
+// SCVX_WSYNC_WAIT the LDS counter is drained as well (debug aid; not needed for correctness
+// because DS instructions of one wave are processed in order).
 __device__ __forceinline__ void wsync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only (vmcnt, expcnt left at max)
+#ifdef SCVX_WSYNC_WAIT
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only
+#endif
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
-    return v;
+// 64-bit DPP move (two 32-bit halves).  All 64 lanes must be active.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
 }
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, WAVE));
-    return v;
-}
-__device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, WAVE));
-    return v;
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
 }
 
-// out[i][j] (R x C) = (add ? add[i][j] : 0) + alpha * sum_k op(A)[i][k] op(B)[k][j]
-// op(A) is R x KK: TA ? A stored KK x R : A stored R x KK.  op(B) is KK x C similarly.
-template <int R, int C, int KK, bool TA, bool TB>
-__device__ __forceinline__ void mm(double* __restrict__ out, const double* __restrict__ A,
-                                   const double* __restrict__ B, const double* add, double alpha, int lane) {
-    for (int e = lane; e < R * C; e += WAVE) {
-        const int i = e / C, j = e % C;
-        double acc = 0.0;
-#pragma unroll
-        for (int k = 0; k < KK; ++k) {
-            const double a = TA ? A[k * R + i] : A[i * KK + k];
-            const double b = TB ? B[j * KK + k] : B[k * C + j];
-            acc = fma(a, b, acc);
-        }
-        out[e] = (add ? add[e] : 0.0) + alpha * acc;
+// Reductions over the 64 lanes (result uniform): DPP inside each 16-lane row (quad xor 1, quad
+// xor 2, half-row mirror, row mirror), then the four row results through readlane.
+#define SCVX_WAVE_REDUCE(NAME, OP)                                     \
+    __device__ __forceinline__ double NAME(double v) {                 \
+        v = OP(v, dpp_d<0xB1>(v));  /* quad_perm [1,0,3,2] */          \
+        v = OP(v, dpp_d<0x4E>(v));  /* quad_perm [2,3,0,1] */          \
+        v = OP(v, dpp_d<0x141>(v)); /* row_half_mirror */              \
+        v = OP(v, dpp_d<0x140>(v)); /* row_mirror */                   \
+        return OP(OP(readlane_d(v, 0), readlane_d(v, 16)),             \
+                  OP(readlane_d(v, 32), readlane_d(v, 48)));           \
     }
-}
-
-// y (R) = (add ? add : 0) + alpha * op(A) x,   op(A) R x C
-template <int R, int C, bool TA>
-__device__ __forceinline__ void mv(double* __restrict__ y, const double* __restrict__ A, const double* __restrict__ x,
-                                   const double* add, double alpha, int lane) {
-    if (lane < R) {
-        double acc = 0.0;
-#pragma unroll
-        for (int k = 0; k < C; ++k) acc = fma(TA ? A[k * R + lane] : A[lane * C + k], x[k], acc);
-        y[lane] = (add ? add[lane] : 0.0) + alpha * acc;
-    }
-}
+__device__ __forceinline__ double op_add(double a, double b) { return a + b; }
+SCVX_WAVE_REDUCE(wave_sum, op_add)
+SCVX_WAVE_REDUCE(wave_max, fmax)
+SCVX_WAVE_REDUCE(wave_min, fmin)
+#undef SCVX_WAVE_REDUCE
 
 }  // namespace scvx

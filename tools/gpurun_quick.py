@@ -23,10 +23,13 @@ for rep in range(3):
     print(f"N={N} foh {1e3*(t1-t0):.3f} ms  qp {1e3*(t2-t1):.3f} ms  status {np.bincount(st, minlength=3)}  iters mean {it.mean():.1f} max {it.max()}", flush=True)
 if os.environ.get("TRACE"):
     import ctypes
-    buf = torch.zeros(8 * 80, dtype=torch.float64, device=d)
+    buf = torch.zeros(8 * 80 + 16, dtype=torch.float64, device=d)
     scvx_hip.lib().scvx_qp_set_trace(ctypes.c_void_p(buf.data_ptr()), 0, 80)
     out = solver.solve(disc, sig, X, U, xi, xf, tr)
     torch.cuda.synchronize()
-    b = buf.view(80, 8).cpu().numpy()
+    b = buf[:640].view(80, 8).cpu().numpy()
+    cyc = buf[640:644].cpu().numpy()
+    n_it = int(out["iters"][0].item())
+    print(f"cycles: factor {cyc[0]:.3e} ({cyc[0]/max(n_it,1):.3e}/it)  solve {cyc[1]:.3e} ({cyc[1]/max(n_it,1)/2:.3e}/solve)  total {cyc[2]:.3e} ({cyc[2]/max(n_it,1):.3e}/it)  fail {cyc[3]}")
     for i in range(int(out["iters"][0].item())):
         print("it %2d pres %.2e dres %.2e gap %.2e pobj %.6e aa %.3f al %.3f sg %.2e mu %.2e" % ((i,) + tuple(b[i])))
