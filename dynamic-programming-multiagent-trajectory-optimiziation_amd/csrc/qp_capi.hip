@@ -66,9 +66,8 @@ int qp_check(const scvx_qp_template* T, int N, const ModelTable*& mt, int& cls) 
 
 size_t ws_bytes(const ModelTable& mt, int cls, int N) {
     const int nb = mt.caps[3 * cls], no = mt.caps[3 * cls + 1], nc = mt.caps[3 * cls + 2];
-    (void)nb;
     const int ns = no + nc, ng = no + (nc > 0 ? 1 : 0);
-    return sizeof(double) * (size_t)N * (size_t)qp_ws_doubles(mt.nx, mt.nu, ns, ng);
+    return sizeof(double) * (size_t)N * (size_t)qp_ws_doubles(mt.nx, mt.nu, nb, ns, ng);
 }
 }  // namespace
 

@@ -12,24 +12,30 @@
 // slacks (obstacle slacks, the shared collision slack S_t of dist_scvx_3d.py:93-107) are
 // eliminated per node.
 //
-// Mapping (one agent per 64-lane wavefront = one workgroup; lane t = node t):
-//   * node phases  -- lane-parallel over the nodes.  The inequality-row state (slacks s,
-//                     duals lambda) lives in registers: rows have compile-time capacities
-//                     (QPCfg: 2^m trust-region facets, NB boxes, NO obstacles, NC collision
-//                     rows, their slack groups), so every row loop is unrolled with the row
-//                     kind resolved at compile time;
+// Mapping: one agent per 64-lane wavefront (= workgroup), lane t = node t.  The design follows
+// the measured gfx950 latencies (tools/ubench/lat.hip: dependent LDS load ~60 cycles, FP64 FMA 6,
+// a readlane-broadcast 6x6 chain step ~180, a global load under full-chip load ~2,500):
+// nothing on a sequential chain touches global memory, and every lane-parallel phase issues its
+// global loads as one batch.
+//   * node phases  -- lane-parallel over the nodes.  The per-node state (z, y, slacks s and duals
+//                     lambda of every inequality row, SOC pair, slack groups) lives in the
+//                     agent workspace and is loaded as one batch at the start of each phase, so
+//                     nothing node-sized stays in registers across the sweeps.  Rows have
+//                     compile-time capacities (QPCfg: 2^m trust-region facets, NB boxes, NO
+//                     obstacles, NC collision rows, their slack groups): every row loop is
+//                     unrolled with the row kind resolved at compile time;
 //   * factor sweep -- sequential over stages, element-parallel over lanes: 4 straight-line
 //                     phases per stage, each lane's output element picked by a packed
-//                     descriptor computed once (no per-stage branching), stage inputs
-//                     streamed through a 2-slot LDS ring one stage ahead;
-//   * solves       -- closed-loop form.  With Acl_t = A_t + Bt_t K_t the backward pass is the
-//                     chain p_t = Acl_t' p_{t+1} + g_t and the forward pass the chain
-//                     xi_{t+1} = Acl_t xi_t + f_t: g_t, f_t and every output that does not sit on
-//                     the chain (feed-forward k0, inputs, multipliers) are computed
-//                     lane-parallel before/after the chain, so each chain step is one
-//                     n-term dot product per lane.
-// Factor outputs are kept in an agent-private workspace in stage-minor columns
-// (ws[col * 64 + t]): lane-parallel passes read them coalesced.
+//                     descriptor (no per-stage branching); stage packets are prefetched three
+//                     stages ahead into a 4-slot LDS ring;
+//   * solves       -- closed-loop form.  With Acl_t = A_t + Bt_t K_t (kept in LDS by the factor)
+//                     the backward pass is the chain p_t = Acl_t' p_{t+1} + g_t and the forward
+//                     pass the chain xi_{t+1} = Acl_t xi_t + f_t: g_t, f_t and every output off
+//                     the chain (feed-forward k0, inputs, multipliers) are computed lane-parallel
+//                     before/after the chain, and each chain step is one n-term dot product per
+//                     lane with the previous vector broadcast through readlane.
+// Factor outputs other than Acl go to stage-minor workspace columns (ws[col * 64 + t]) that the
+// lane-parallel passes read coalesced.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -65,21 +71,17 @@ struct QPArgs {
 
 // ---- sizes shared by host (workspace / LDS bytes) and device
 constexpr int qp_dstr(int nx, int nu) { return nx * (nx + 2 * nu + 2); }
-constexpr int qp_pkt(int nx, int nu) { return 2 * nx * nx + 3 * nx * nu + nu * nu + nx; }
-constexpr int qp_ncol(int nx, int nu, int ns, int ng) {
-    return qp_dstr(nx, nu) + 3 * nu * nx + nu * nu + 3 * nx * nx + nx + nx * nu + 4 * ns + 4 * ng + nx + nu + ng;
-}
-constexpr long long qp_ws_doubles(int nx, int nu, int ns, int ng) {
-    return (long long)qp_ncol(nx, nu, ns, ng) * 64 + 64LL * qp_pkt(nx, nu);
-}
+constexpr int qp_pkt(int nx, int nu) { return 2 * nx * nx + 4 * nx * nu + nu * nu + nx; }
 constexpr int qp_even(int x) { return (x + 1) & ~1; }
-constexpr int qp_lds_factor(int nx, int nu) {
-    return qp_even(2 * qp_pkt(nx, nu) + 5 * nx * nx + 2 * nx * nu + nu * nx + nu * nu + 2 * nu * nx + 8);
+// workspace columns (doubles x 64) of a capacity class
+constexpr int qp_ncol(int nx, int nu, int nb, int ns, int ng) {
+    // disc^T | K kappa LD W2 P Pi u | Bt | soft rows | groups | rd | r1a | cP | ub | node state | SOC
+    return qp_dstr(nx, nu) + 3 * nu * nx + nu * nu + 2 * nx * nx + nx + nx * nu + 4 * ns + 4 * ng + (nx + nu) + ng +
+           ((1 << nu) + 2 * nb + ns + ng) + nu +
+           (2 * ((1 << nu) + 2 * nb + ns + ng) + (nx + nu) + nx + 2 * (nu + 1) + ng) + (3 * (nu + 1) + 1 + (nu + 1));
 }
-constexpr int qp_lds_doubles(int nx, int nu, int K, int nr) {
-    // max(factor region, solve packets) + persistent vectors + predictor row products [nr][64]
-    return (qp_lds_factor(nx, nu) > K * (nx * nx + nx) ? qp_lds_factor(nx, nu) : qp_even(K * (nx * nx + nx))) +
-           2 * nx * nx + (K + 1) * nx + 10 * nx + 8 + 64 * nr;
+constexpr long long qp_ws_doubles(int nx, int nu, int nb, int ns, int ng) {
+    return (long long)qp_ncol(nx, nu, nb, ns, ng) * 64 + 64LL * qp_pkt(nx, nu);
 }
 
 template <int NX_, int NU_, int NB_, int NO_, int NC_>
@@ -91,90 +93,137 @@ struct QPCfg {
     static constexpr int R_BOX = NTR, R_OBS = NTR + 2 * NB, R_COL = R_OBS + NO, R_GRP = R_COL + NC;
     static constexpr int NR = R_GRP + NG;
     static constexpr int DSTR = qp_dstr(NX, NU);
-    // factor packet [t][PKT]: node Hessian Q|S|R, e, then the constant A | Bt | C_{t-1}
+    // factor packet [t][PKT]: node Hessian Q|S|R, e, then the constant A (column-major) | Bt
+    // column-major | Bt row-major | C_{t-1} (column-major).  Every dot product of the factor
+    // phases then reads two contiguous LDS vectors.
     static constexpr int P_Q = 0, P_S = P_Q + NX * NX, P_R = P_S + NX * NU, P_E = P_R + NU * NU,
-                         P_A = P_E + NX, P_BT = P_A + NX * NX, P_C = P_BT + NX * NU, PKT = P_C + NX * NU;
+                         P_A = P_E + NX, P_BT = P_A + NX * NX, P_BTR = P_BT + NX * NU, P_C = P_BTR + NX * NU,
+                         PKT = P_C + NX * NU;
     static_assert(PKT == qp_pkt(NX, NU), "packet size");
     // stage-minor workspace columns
-    static constexpr int C_DT = 0;                // disc, transposed: A (col-major) | B | C | S | z
-    static constexpr int C_K = C_DT + DSTR;       // K      NU x NX
-    static constexpr int C_KAP = C_K + NU * NX;   // kappa  NU x NX
-    static constexpr int C_LD = C_KAP + NU * NX;  // LDL' of Rhat: L[i][j] (i > j), 1/d_i on the diagonal
-    static constexpr int C_W2 = C_LD + NU * NU;   // W2 = Bt' Pi_{t+1}  NU x NX
-    static constexpr int C_P = C_W2 + NU * NX;    // P_t
-    static constexpr int C_PI = C_P + NX * NX;    // Pi_t
-    static constexpr int C_ACL = C_PI + NX * NX;  // Acl_t = A_t + Bt_t K_t (row-major)
-    static constexpr int C_U = C_ACL + NX * NX;   // P_{t+1} e_t
-    static constexpr int C_BT = C_U + NX;         // Bt_t (row-major)
-    static constexpr int C_SOFT = C_BT + NX * NU; // soft rows (g0, g1, g2, b)
-    static constexpr int C_GRP = C_SOFT + 4 * NS; // per group: Hpa/Haa (3), 1/Haa
-    static constexpr int C_RD = C_GRP + 4 * NG;   // dual residual (x, u part)
-    static constexpr int C_R1A = C_RD + NZ;       // group part of the current Newton rhs
-    static constexpr int NCOL = C_R1A + NG;
-    static_assert(NCOL == qp_ncol(NX, NU, NS, NG), "column count");
-    // LDS (doubles): factor region (aliased by the solve packets), then persistent vectors
-    static constexpr int F_RING = 0, F_PP = 2 * PKT, F_PIP = F_PP + NX * NX, F_T1 = F_PIP + NX * NX,
+    static constexpr int C_DT = 0;                 // disc, transposed: A (col-major) | B | C | S | z
+    static constexpr int C_K = C_DT + DSTR;        // K      NU x NX
+    static constexpr int C_KAP = C_K + NU * NX;    // kappa  NU x NX
+    static constexpr int C_LD = C_KAP + NU * NX;   // LDL' of Rhat: L[i][j] (i > j), 1/d_i on the diagonal
+    static constexpr int C_W2 = C_LD + NU * NU;    // W2 = Bt' Pi_{t+1}  NU x NX
+    static constexpr int C_P = C_W2 + NU * NX;     // P_t
+    static constexpr int C_PI = C_P + NX * NX;     // Pi_t
+    static constexpr int C_U = C_PI + NX * NX;     // P_{t+1} e_t
+    static constexpr int C_BT = C_U + NX;          // Bt_t (row-major)
+    static constexpr int C_SOFT = C_BT + NX * NU;  // soft rows (g0, g1, g2, b)
+    static constexpr int C_GRP = C_SOFT + 4 * NS;  // per group: Hpa/Haa (3), 1/Haa
+    static constexpr int C_RD = C_GRP + 4 * NG;    // dual residual (x, u part)
+    static constexpr int C_R1A = C_RD + NZ;        // group part of the current Newton rhs
+    static constexpr int C_CP = C_R1A + NG;        // predictor products ds_a dl_a per row
+    static constexpr int C_UB = C_CP + NR;         // reference input ubar_t
+    // node state
+    static constexpr int C_S = C_UB + NU, C_L = C_S + NR, C_Z = C_L + NR, C_Y = C_Z + NZ, C_SQ = C_Y + NX,
+                         C_LQ = C_SQ + NQ, C_AV = C_LQ + NQ;
+    // SOC scaling of the current iteration: w (NQ), eta, W lam (NQ), rc (NQ), rho (NQ)
+    static constexpr int C_WV = C_AV + NG, C_ETA = C_WV + NQ, C_LTQ = C_ETA + 1, C_RCQ = C_LTQ + NQ,
+                         C_RHO = C_RCQ + NQ;
+    static constexpr int NCOL = C_RHO + NQ;
+    static_assert(NCOL == qp_ncol(NX, NU, NB, NS, NG), "column count");
+    // LDS (doubles, compile-time offsets except the K-sized blocks at the end):
+    // factor: 4-slot packet ring, P', Pi' (col-major), T1, T2 (col-major), W1, W2 (col-major), Qh,
+    // Sh (col-major), Rh, [K | kappa] (col-major), sink
+    static constexpr int F_RING = 0, F_PP = 4 * PKT, F_PIP = F_PP + NX * NX, F_T1 = F_PIP + NX * NX,
                          F_T2 = F_T1 + NX * NX, F_W1 = F_T2 + NX * NU, F_W2 = F_W1 + NX * NX,
                          F_QH = F_W2 + NU * NX, F_SH = F_QH + NX * NX, F_RH = F_SH + NU * NX,
-                         F_KK = F_RH + NU * NU, F_SINK = F_KK + 2 * NU * NX, F_END = F_SINK + 8;
-    static_assert(qp_even(F_END) == qp_lds_factor(NX, NU), "factor LDS");
-    static constexpr int PKS = NX * NX + NX;  // solve packet per stage: Acl | g or f
+                         F_KK = F_RH + NU * NU, F_SINK = F_KK + 2 * NU * NX, F_END = qp_even(F_SINK + 8);
+    static constexpr int L_M = F_END, L_PI0 = L_M + NX * NX, L_XE = L_PI0 + NX * NX, L_XI0 = L_XE + NX,
+                         L_R2F = L_XI0 + NX, L_YI = L_R2F + NX, L_YF = L_YI + NX, L_DYI = L_YF + NX,
+                         L_DYF = L_DYI + NX, L_PIV = L_DYF + NX, L_ONE = L_PIV + NX, L_FLAG = L_ONE + 1,
+                         L_ST = qp_even(L_FLAG + 4), L_VAR = L_ST + 16;
+    // K-sized: Acl [K][NX*NX] (row-major), chain offsets g/f [K][NX], chain vectors [K+1][NX]
+    static constexpr int lds_doubles(int K) { return L_VAR + K * NX * NX + K * NX + (K + 1) * NX; }
 };
 
-// packed phase descriptors: operand = LDS offset (14 bits) | ring-slot relative << 14 | stride << 15
-__host__ __device__ constexpr int qp_dpk(int off, int slot, int stride) { return off | (slot << 14) | (stride << 15); }
-// output = LDS offset | accumulate << 14 | (global column + 1) << 15 ; base = offset | slot << 14 | kind << 15
-// (kind 0: none, 1: always, 2: last stage only)
+// packed phase descriptors (all operands are contiguous LDS vectors):
+//   operand = LDS offset (15 bits) | ring-slot relative << 15
+//   output  = LDS offset | accumulate << 15 | stage-relative (Acl block) << 16 | (global column + 1) << 17
+//   base    = LDS offset | ring-slot relative << 15 | kind << 16   (kind 0: none, 1: always, 2: last stage)
+__host__ __device__ constexpr int qp_dpk(int off, int slot) { return off | (slot << 15); }
 
 // Agent workspace accessor: raw buffer loads/stores with the lane part of the address in one
-// VGPR (voffset) and the column part as an SGPR/immediate (soffset), so no per-column 64-bit
-// address is ever materialised (or hoisted) in vector registers.
+// VGPR (voffset) and the column part as a (rematerialisable) SGPR constant (soffset), so no
+// per-column 64-bit address is ever materialised in vector registers.
 typedef unsigned int qp_u2 __attribute__((ext_vector_type(2)));
 struct QPBuf {
     __amdgpu_buffer_rsrc_t rs;
     __device__ __forceinline__ double ld(int voff, int soff) const {
         soff = __builtin_amdgcn_readfirstlane(soff);  // uniform by construction
-        asm volatile("" : "+s"(soff));
         return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
     }
     __device__ __forceinline__ void st(int voff, int soff, double v) const {
         soff = __builtin_amdgcn_readfirstlane(soff);
-        asm volatile("" : "+s"(soff));
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(qp_u2, v), rs, voff, soff, 0);
     }
 };
-// keep a value opaque to loop-invariant code motion (re-derive it at the point of use)
+// keep a value opaque to the optimiser (volatile: re-derived where it is used, never hoisted)
 __device__ __forceinline__ int qp_opaque(int v) {
     asm volatile("" : "+v"(v));
     return v;
 }
-
 // 1.0 if a == b else 0.0, opaque to the optimiser: selecting an array element by a runtime
 // index with this mask stays arithmetic (a compare/select chain is turned back into a
 // dynamically indexed private array, i.e. scratch memory)
 __device__ __forceinline__ double qp_mask(int a, int b) {
     int m = a == b ? 1 : 0;
-    asm volatile("" : "+v"(m));
+    asm("" : "+v"(m));
     return (double)m;
 }
 
 template <int KK>
 __device__ __forceinline__ double qp_dot(const double* lds, int L, int R, int soff) {
-    L = qp_opaque(L);
-    R = qp_opaque(R);
-    const int lo = (L & 0x3FFF) + ((L >> 14) & 1) * soff, ls = L >> 15;
-    const int ro = (R & 0x3FFF) + ((R >> 14) & 1) * soff, rs = R >> 15;
-    double acc = 0.0;
+    const double* lp = lds + (L & 0x7FFF) + ((L >> 15) & 1) * soff;
+    const double* rp = lds + (R & 0x7FFF) + ((R >> 15) & 1) * soff;
+    double acc0 = 0.0, acc1 = 0.0;
 #pragma unroll
-    for (int k = 0; k < KK; ++k) acc = fma(lds[lo + k * ls], lds[ro + k * rs], acc);
-    return acc;
+    for (int k = 0; k < KK; ++k) {
+        if (k & 1) acc1 = fma(lp[k], rp[k], acc1); else acc0 = fma(lp[k], rp[k], acc0);
+    }
+    return acc0 + acc1;
+}
+
+// One element-parallel phase of the factor sweep: every lane evaluates its NREP descriptors
+// (out = base + sum_k L[k] R[k]).  The descriptors are made opaque once, at the top of the phase
+// (one scheduling barrier), so their decoding is neither hoisted out of the sweep (register
+// pressure) nor serialised between the repetitions.
+template <int KK, int NREP>
+__device__ __forceinline__ void qp_phase(double* lds, const int (&d)[NREP][4], int soff, bool last, int acl_off,
+                                         const QPBuf& wb, int ts) {
+    int Ld[NREP], Rd[NREP], Od[NREP], Bd[NREP];
+#pragma unroll
+    for (int r = 0; r < NREP; ++r) {
+        Ld[r] = d[r][0]; Rd[r] = d[r][1]; Od[r] = d[r][2]; Bd[r] = d[r][3];
+        asm volatile("" : "+v"(Ld[r]), "+v"(Rd[r]), "+v"(Od[r]), "+v"(Bd[r]));
+    }
+    double val[NREP];
+#pragma unroll
+    for (int r = 0; r < NREP; ++r) {
+        const int bk = Bd[r] >> 16;
+        const double bv = lds[(Bd[r] & 0x7FFF) + ((Bd[r] >> 15) & 1) * soff];
+        val[r] = qp_dot<KK>(lds, Ld[r], Rd[r], soff) + ((bk == 1 || (bk == 2 && last)) ? bv : 0.0);
+    }
+#pragma unroll
+    for (int r = 0; r < NREP; ++r) {
+        const int O = Od[r];
+        if (O >= 0) {
+            const int oo = (O & 0x7FFF) + ((O >> 16) & 1) * acl_off;
+            const double old = lds[oo];
+            lds[oo] = ((O >> 15) & 1) ? old + val[r] : val[r];
+            const int g = (O >> 17) - 1;
+            if (g >= 0) wb.st(g * WAVE * 8, ts * 8, val[r]);
+        }
+    }
 }
 
 template <class C>
 __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
-    constexpr int NX = C::NX, NU = C::NU, NZ = C::NZ, NQ = C::NQ, NR = C::NR, NG = C::NG,
-                  NS = C::NS, NO = C::NO, NC = C::NC, PKT = C::PKT, PKS = C::PKS;
-    constexpr int NGA = NG > 0 ? NG : 1, NSA = NS > 0 ? NS : 1;
+    constexpr int NX = C::NX, NU = C::NU, NZ = C::NZ, NQ = C::NQ, NR = C::NR, NG = C::NG, NS = C::NS,
+                  NO = C::NO, NC = C::NC, NB = C::NB, PKT = C::PKT;
+    constexpr int NGA = NG > 0 ? NG : 1, NSA = NS > 0 ? NS : 1, NBA = NB > 0 ? NB : 1;
     extern __shared__ double lds[];
     const scvx_qp_template& T = a.T;
     const int K = T.K, lane = threadIdx.x, t = lane;
@@ -182,7 +231,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     const bool act = t < K;
     const bool ineq = act && ((t < K - 1) || T.ineq_last);
     const bool fin = T.has_final != 0;
+#ifdef QPX_NOSOC
+    const bool soc = false;
+#else
     const bool soc = ineq && T.has_soc;
+#endif
     const bool has_coll = NC > 0 && T.j_max > 0;
     const int nobs = T.n_obs, nbox = T.n_box;
     const int ccount = (ineq && has_coll) ? min((int)a.coll_count[agent * K + t], min(T.j_max, NC)) : 0;
@@ -197,30 +250,32 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     const int vt = t * 8;  // this lane's element of a stage-minor column
     constexpr int PKB = C::NCOL * WAVE * 8;  // byte offset of the packets [t][PKT]
     const int vpk = t * PKT * 8;
-    // column c at this lane's stage
-    auto cld = [&](int c) __attribute__((always_inline)) -> double { return wb.ld(vt, c * WAVE * 8); };
+    // Loads go through `vcur`, this lane's offset re-derived (opaquely) at the start of every
+    // phase: a load in one phase is then never merged with the same load of an earlier phase,
+    // which would keep the value live in registers across the sweeps in between.
+    int vcur = vt;
+    auto fresh = [&]() __attribute__((always_inline)) { vcur = qp_opaque(vt); };
+    auto cld = [&](int c) __attribute__((always_inline)) -> double { return wb.ld(vcur, c * WAVE * 8); };
     auto cst = [&](int c, double v) __attribute__((always_inline)) { wb.st(vt, c * WAVE * 8, v); };
     auto pst = [&](int e, double v) __attribute__((always_inline)) { wb.st(vpk, PKB + e * 8, v); };
 
-    // persistent LDS vectors
-    const int R0 = qp_lds_factor(NX, NU) > K * PKS ? qp_lds_factor(NX, NU) : qp_even(K * PKS);
-    const int V_M = R0, V_PI0 = V_M + NX * NX, V_CH = V_PI0 + NX * NX, V_XE = V_CH + (K + 1) * NX,
-              V_XI0 = V_XE + NX, V_R2F = V_XI0 + NX, V_YI = V_R2F + NX, V_YF = V_YI + NX, V_DYI = V_YF + NX, V_DYF = V_DYI + NX, V_PIV = V_DYF + NX,
-              V_ONE = V_PIV + NX, V_FLAG = V_ONE + 1, V_CP = qp_even(V_FLAG + 4);
-    constexpr int S_PK = 0;
-
-    // ------------------------------------------------------------------ setup (once per solve)
-    double ub[NU];  // reference input
-#pragma unroll
-    for (int j = 0; j < NU; ++j) ub[j] = act ? a.Uref[(agent * K + t) * NU + j] : 0.0;
-    // C_{t-1} (column-major as disc) of this node, from the transposed disc at stage t-1
-    auto load_cp = [&](double* Cp) __attribute__((always_inline)) {
-#pragma unroll
-        for (int e = 0; e < NX * NU; ++e) {
-            const double v = wb.ld(vt - 8, (C::C_DT + NX * NX + NX * NU + e) * WAVE * 8);
-            Cp[e] = (t > 0) ? v : 0.0;
+    constexpr int V_M = C::L_M, V_PI0 = C::L_PI0, V_XE = C::L_XE, V_XI0 = C::L_XI0, V_R2F = C::L_R2F,
+                  V_YI = C::L_YI, V_YF = C::L_YF, V_DYI = C::L_DYI, V_DYF = C::L_DYF, V_PIV = C::L_PIV,
+                  V_ONE = C::L_ONE, V_FLAG = C::L_FLAG, V_ST = C::L_ST, V_ACL = C::L_VAR;
+    const int V_G = V_ACL + K * NX * NX, V_CH = V_G + K * NX;
+    // region timers of the traced agent (diagnostics): cycles since the previous stamp -> V_ST[i]
+    const bool stamp_on = a.trace && agent == a.trace_agent;
+    long long tprev = 0;
+    auto stamp = [&](int i) __attribute__((always_inline)) {
+        if (stamp_on) {
+            __builtin_amdgcn_s_waitcnt(0);  // attribute outstanding memory traffic to its region
+            const long long now = __builtin_amdgcn_s_memtime();
+            if (lane == 0 && i >= 0) lds[V_ST + i] += (double)(now - tprev);
+            tprev = now;
         }
     };
+
+    // ------------------------------------------------------------------ setup (once per solve)
     {
         double Cp[NX * NU];
 #pragma unroll
@@ -229,10 +284,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         // transposed disc (zero for t >= K-1), Bt = B + A C_{t-1}, the constant part of the packets
         double Ad[NX * NX], Bd[NX * NU];
         const bool dyn = t < K - 1;
-        for (int e = 0; e < C::DSTR; ++e) {
-            const double v = dyn ? disc[(long long)t * C::DSTR + e] : 0.0;
-            cst(C::C_DT + e, v);
-        }
+        for (int e = 0; e < C::DSTR; ++e) cst(C::C_DT + e, dyn ? disc[(long long)t * C::DSTR + e] : 0.0);
 #pragma unroll
         for (int e = 0; e < NX * NX; ++e) Ad[e] = dyn ? disc[(long long)t * C::DSTR + e] : 0.0;
 #pragma unroll
@@ -246,7 +298,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                     for (int k = 0; k < NX; ++k) v = fma(Ad[k * NX + i], Cp[j * NX + k], v);
                     cst(C::C_BT + i * NU + j, v);
-                    pst(C::P_BT + i * NU + j, v);
+                    pst(C::P_BT + j * NX + i, v);
+                    pst(C::P_BTR + i * NU + j, v);
                 }
 #pragma unroll
             for (int e = 0; e < NX * NX; ++e) pst(C::P_A + e, Ad[e]);
@@ -290,134 +343,158 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) cst(C::C_SOFT + (NO + c) * 4 + i, g[i]);
         }
+        // initial node state: z = (xbar, ubar), y = 0, slack groups 0
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            cst(C::C_Z + i, act ? a.Xref[(agent * K + t) * NX + i] : 0.0);
+            cst(C::C_Y + i, 0.0);
+        }
+#pragma unroll
+        for (int j = 0; j < NU; ++j) {
+            const double u = act ? a.Uref[(agent * K + t) * NU + j] : 0.0;
+            cst(C::C_UB + j, u);
+            cst(C::C_Z + NX + j, u);
+        }
+#pragma unroll
+        for (int g = 0; g < NG; ++g) cst(C::C_AV + g, 0.0);
         if (lane == 0) lds[V_ONE] = 1.0;
+        if (lane < NX) { lds[V_YI + lane] = 0.0; lds[V_YF + lane] = 0.0; }
+        if (lane < 16) lds[V_ST + lane] = 0.0;
     }
-
-    // ------------------------------------------------------------------ phase descriptors
-    constexpr int E1 = 2 * NX * NX + 2 * NX * NU + 2 * NX, E2 = NX * NX + NU * NX + NU * NU, E4 = 4 * NX * NX;
-    constexpr int R1 = (E1 + WAVE - 1) / WAVE, R2 = (E2 + WAVE - 1) / WAVE, R4 = (E4 + WAVE - 1) / WAVE;
-    int d1[R1][4], d2[R2][4], d4[R4][4];
-    {
-        const int sink = C::F_SINK;
+    // C_{t-1} (column-major as disc) of this node, from the transposed disc at stage t-1
+    auto load_cp = [&](double* Cp) __attribute__((always_inline)) {
 #pragma unroll
-        for (int rep = 0; rep < R1; ++rep) {
-            int o = lane + rep * WAVE, L = 0, R = 0, O = -1, B = 0;
-            if (o < NX * NX) {  // T1 = P' A
-                const int i = o / NX, j = o % NX;
-                L = qp_dpk(C::F_PP + i * NX, 0, 1); R = qp_dpk(C::P_A + j * NX, 1, 1); O = C::F_T1 + o;
-            } else if ((o -= NX * NX) < NX * NU) {  // T2 = P' Bt
-                const int i = o / NU, j = o % NU;
-                L = qp_dpk(C::F_PP + i * NX, 0, 1); R = qp_dpk(C::P_BT + j, 1, NU); O = C::F_T2 + o;
-            } else if ((o -= NX * NU) < NX * NX) {  // W1 = A' Pi'   (I at the last stage)
-                const int i = o / NX, j = o % NX;
-                L = qp_dpk(C::P_A + i * NX, 1, 1); R = qp_dpk(C::F_PIP + j, 0, NX); O = C::F_W1 + o;
-                B = (i == j) ? (V_ONE | (2 << 15)) : 0;
-            } else if ((o -= NX * NX) < NU * NX) {  // W2 = Bt' Pi'  (C_{K-2}' at the last stage)
-                const int i = o / NX, j = o % NX;
-                L = qp_dpk(C::P_BT + i, 1, NU); R = qp_dpk(C::F_PIP + j, 0, NX);
-                O = (C::F_W2 + o) | ((C::C_W2 + o + 1) << 15);
-                B = (C::P_C + i * NX + j) | (1 << 14) | (2 << 15);
-            } else if ((o -= NU * NX) < NX) {  // u = P' e  (global only)
-                L = qp_dpk(C::F_PP + o * NX, 0, 1); R = qp_dpk(C::P_E, 1, 1); O = sink | ((C::C_U + o + 1) << 15);
-            } else if ((o -= NX) < NX) {  // xe += Pi'' e
-                L = qp_dpk(C::F_PIP + o, 0, NX); R = qp_dpk(C::P_E, 1, 1); O = (V_XE + o) | (1 << 14);
-            }
-            d1[rep][0] = L; d1[rep][1] = R; d1[rep][2] = O; d1[rep][3] = B;
-        }
-#pragma unroll
-        for (int rep = 0; rep < R2; ++rep) {
-            int o = lane + rep * WAVE, L = 0, R = 0, O = -1, B = 0;
-            if (o < NX * NX) {  // Qh = Q + A' T1 (symmetric: (min, max) element for both halves)
-                const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
-                L = qp_dpk(C::P_A + p * NX, 1, 1); R = qp_dpk(C::F_T1 + q, 0, NX); O = C::F_QH + o;
-                B = (C::P_Q + p * NX + q) | (1 << 14) | (1 << 15);
-            } else if ((o -= NX * NX) < NU * NX) {  // Sh = S' + Bt' T1
-                const int i = o / NX, j = o % NX;
-                L = qp_dpk(C::P_BT + i, 1, NU); R = qp_dpk(C::F_T1 + j, 0, NX); O = C::F_SH + o;
-                B = (C::P_S + j * NU + i) | (1 << 14) | (1 << 15);
-            } else if ((o -= NU * NX) < NU * NU) {  // Rh = R + Bt' T2
-                const int i = o / NU, j = o % NU, p = i < j ? i : j, q = i < j ? j : i;
-                L = qp_dpk(C::P_BT + p, 1, NU); R = qp_dpk(C::F_T2 + q, 0, NU); O = C::F_RH + o;
-                B = (C::P_R + p * NU + q) | (1 << 14) | (1 << 15);
-            }
-            d2[rep][0] = L; d2[rep][1] = R; d2[rep][2] = O; d2[rep][3] = B;
-        }
-#pragma unroll
-        for (int rep = 0; rep < R4; ++rep) {
-            int o = lane + rep * WAVE, L = 0, R = 0, O = -1, B = 0;
-            if (o < NX * NX) {  // P = Qh + Sh' K (symmetric)
-                const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
-                L = qp_dpk(C::F_SH + p, 0, NX); R = qp_dpk(C::F_KK + q, 0, 2 * NX);
-                O = (C::F_PP + o) | ((C::C_P + o + 1) << 15); B = (C::F_QH + p * NX + q) | (1 << 15);
-            } else if ((o -= NX * NX) < NX * NX) {  // Pi = W1 + Sh' kappa
-                const int i = o / NX, j = o % NX;
-                L = qp_dpk(C::F_SH + i, 0, NX); R = qp_dpk(C::F_KK + NX + j, 0, 2 * NX);
-                O = (C::F_PIP + o) | ((C::C_PI + o + 1) << 15); B = (C::F_W1 + o) | (1 << 15);
-            } else if ((o -= NX * NX) < NX * NX) {  // M += W2' kappa (symmetric)
-                const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
-                L = qp_dpk(C::F_W2 + p, 0, NX); R = qp_dpk(C::F_KK + NX + q, 0, 2 * NX); O = (V_M + o) | (1 << 14);
-            } else if ((o -= NX * NX) < NX * NX) {  // Acl = A + Bt K
-                const int i = o / NX, j = o % NX;
-                L = qp_dpk(C::P_BT + i * NU, 1, 1); R = qp_dpk(C::F_KK + j, 0, 2 * NX);
-                O = sink | ((C::C_ACL + o + 1) << 15); B = (C::P_A + j * NX + i) | (1 << 14) | (1 << 15);
-            }
-            d4[rep][0] = L; d4[rep][1] = R; d4[rep][2] = O; d4[rep][3] = B;
-        }
-    }
-    auto run_desc = [&](const int* d, double val, int soff, bool last, int ts) __attribute__((always_inline)) {
-        const int O = qp_opaque(d[2]), B = qp_opaque(d[3]);
-        const int bk = B >> 15;
-        const double bv = lds[(B & 0x3FFF) + ((B >> 14) & 1) * soff];
-        const double v = val + ((bk == 1 || (bk == 2 && last)) ? bv : 0.0);
-        if (O >= 0) {
-            const int oo = O & 0x3FFF;
-            const double old = lds[oo];
-            lds[oo] = ((O >> 14) & 1) ? old + v : v;
-            const int g = (O >> 15) - 1;
-            if (g >= 0) wb.st(g * WAVE * 8, ts * 8, v);
+        for (int e = 0; e < NX * NU; ++e) {
+            const double v = wb.ld(vcur - 8, (C::C_DT + NX * NX + NX * NU + e) * WAVE * 8);
+            Cp[e] = (t > 0) ? v : 0.0;
         }
     };
 
     // ------------------------------------------------------------------ factor sweep
-    // Stage inputs (Q, S, R, e of the node phase; A, Bt, C_{t-1}) are in packet t; outputs go to the
-    // stage-minor columns, M (and its LU) / Pi_0 / xe to persistent LDS.  false on a breakdown.
+    // Stage inputs (Q, S, R, e of the node phase; A, Bt, C_{t-1}) are in packet t; Acl goes to
+    // LDS, the other outputs to the stage-minor columns, M (and its LU) / Pi_0 / xe to persistent
+    // LDS.  false on a breakdown.
     constexpr int PFN = (PKT + WAVE - 1) / WAVE;
     auto factor = [&]() __attribute__((always_inline)) -> bool {
+#ifdef QPX_NOFACTOR
+        return true;
+#endif
+        // phase descriptors (rebuilt per call: nothing of them stays live outside the sweep)
+        constexpr int E1 = 2 * NX * NX + 2 * NX * NU + 2 * NX, E2 = NX * NX + NU * NX + NU * NU, E4 = 4 * NX * NX;
+        constexpr int R1 = (E1 + WAVE - 1) / WAVE, R2 = (E2 + WAVE - 1) / WAVE, R4 = (E4 + WAVE - 1) / WAVE;
+        int d1[R1][4], d2[R2][4], d4[R4][4];
+        {
+            const int sink = C::F_SINK;
+            const int ln = qp_opaque(lane);  // volatile: keeps the descriptors inside the IPM loop
+#pragma unroll
+            for (int rep = 0; rep < R1; ++rep) {
+                int o = ln + rep * WAVE, L = 0, R = 0, O = -1, B = 0;
+                if (o < NX * NX) {  // T1 = P' A  -> T1 column-major
+                    const int i = o / NX, j = o % NX;
+                    L = qp_dpk(C::F_PP + i * NX, 0); R = qp_dpk(C::P_A + j * NX, 1); O = C::F_T1 + j * NX + i;
+                } else if ((o -= NX * NX) < NX * NU) {  // T2 = P' Bt -> column-major
+                    const int i = o / NU, j = o % NU;
+                    L = qp_dpk(C::F_PP + i * NX, 0); R = qp_dpk(C::P_BT + j * NX, 1); O = C::F_T2 + j * NX + i;
+                } else if ((o -= NX * NU) < NX * NX) {  // W1 = A' Pi'   (I at the last stage)
+                    const int i = o / NX, j = o % NX;
+                    L = qp_dpk(C::P_A + i * NX, 1); R = qp_dpk(C::F_PIP + j * NX, 0); O = C::F_W1 + o;
+                    B = (i == j) ? (V_ONE | (2 << 16)) : 0;
+                } else if ((o -= NX * NX) < NU * NX) {  // W2 = Bt' Pi' -> column-major (C_{K-2}' at the last stage)
+                    const int i = o / NX, j = o % NX;
+                    L = qp_dpk(C::P_BT + i * NX, 1); R = qp_dpk(C::F_PIP + j * NX, 0);
+                    O = (C::F_W2 + j * NU + i) | ((C::C_W2 + o + 1) << 17);
+                    B = (C::P_C + i * NX + j) | (1 << 15) | (2 << 16);
+                } else if ((o -= NU * NX) < NX) {  // u = P' e  (global only)
+                    L = qp_dpk(C::F_PP + o * NX, 0); R = qp_dpk(C::P_E, 1); O = sink | ((C::C_U + o + 1) << 17);
+                } else if ((o -= NX) < NX) {  // xe += Pi'' e
+                    L = qp_dpk(C::F_PIP + o * NX, 0); R = qp_dpk(C::P_E, 1); O = (V_XE + o) | (1 << 15);
+                }
+                d1[rep][0] = L; d1[rep][1] = R; d1[rep][2] = O; d1[rep][3] = B;
+            }
+#pragma unroll
+            for (int rep = 0; rep < R2; ++rep) {
+                int o = ln + rep * WAVE, L = 0, R = 0, O = -1, B = 0;
+                if (o < NX * NX) {  // Qh = Q + A' T1 (symmetric: (min, max) element for both halves)
+                    const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
+                    L = qp_dpk(C::P_A + p * NX, 1); R = qp_dpk(C::F_T1 + q * NX, 0); O = C::F_QH + o;
+                    B = (C::P_Q + p * NX + q) | (1 << 15) | (1 << 16);
+                } else if ((o -= NX * NX) < NU * NX) {  // Sh = S' + Bt' T1 -> column-major
+                    const int i = o / NX, j = o % NX;
+                    L = qp_dpk(C::P_BT + i * NX, 1); R = qp_dpk(C::F_T1 + j * NX, 0); O = C::F_SH + j * NU + i;
+                    B = (C::P_S + j * NU + i) | (1 << 15) | (1 << 16);
+                } else if ((o -= NU * NX) < NU * NU) {  // Rh = R + Bt' T2
+                    const int i = o / NU, j = o % NU, p = i < j ? i : j, q = i < j ? j : i;
+                    L = qp_dpk(C::P_BT + p * NX, 1); R = qp_dpk(C::F_T2 + q * NX, 0); O = C::F_RH + o;
+                    B = (C::P_R + p * NU + q) | (1 << 15) | (1 << 16);
+                }
+                d2[rep][0] = L; d2[rep][1] = R; d2[rep][2] = O; d2[rep][3] = B;
+            }
+#pragma unroll
+            for (int rep = 0; rep < R4; ++rep) {
+                int o = ln + rep * WAVE, L = 0, R = 0, O = -1, B = 0;
+                if (o < NX * NX) {  // P = Qh + Sh' K (symmetric)
+                    const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
+                    L = qp_dpk(C::F_SH + p * NU, 0); R = qp_dpk(C::F_KK + q * NU, 0);
+                    O = (C::F_PP + o) | ((C::C_P + o + 1) << 17); B = (C::F_QH + p * NX + q) | (1 << 16);
+                } else if ((o -= NX * NX) < NX * NX) {  // Pi = W1 + Sh' kappa -> Pi' column-major
+                    const int i = o / NX, j = o % NX;
+                    L = qp_dpk(C::F_SH + i * NU, 0); R = qp_dpk(C::F_KK + (NX + j) * NU, 0);
+                    O = (C::F_PIP + j * NX + i) | ((C::C_PI + o + 1) << 17); B = (C::F_W1 + o) | (1 << 16);
+                } else if ((o -= NX * NX) < NX * NX) {  // M += W2' kappa (symmetric)
+                    const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
+                    L = qp_dpk(C::F_W2 + p * NU, 0); R = qp_dpk(C::F_KK + (NX + q) * NU, 0); O = (V_M + o) | (1 << 15);
+                } else if ((o -= NX * NX) < NX * NX) {  // Acl = A + Bt K  -> LDS Acl block of the stage
+                    const int i = o / NX, j = o % NX;
+                    L = qp_dpk(C::P_BTR + i * NU, 1); R = qp_dpk(C::F_KK + j * NU, 0);
+                    O = (V_ACL + o) | (1 << 16); B = (C::P_A + j * NX + i) | (1 << 15) | (1 << 16);
+                }
+                d4[rep][0] = L; d4[rep][1] = R; d4[rep][2] = O; d4[rep][3] = B;
+            }
+        }
         for (int e = lane; e < NX * NX; e += WAVE) { lds[C::F_PP + e] = 0.0; lds[C::F_PIP + e] = 0.0; lds[V_M + e] = 0.0; }
         if (lane < NX) lds[V_XE + lane] = 0.0;
         if (lane == 0) lds[V_FLAG] = 0.0;
         __syncthreads();  // the node phase wrote the packets (global) from other lanes
-        double pf[PFN];
-        auto pf_load = [&](int ts) __attribute__((always_inline)) {
+        // packets stream through a 4-slot ring, loads issued 3 stages ahead (register buffers
+        // pf[0..2], so the stage loop is unrolled by 3 to keep their indices static)
+        double pf[3][PFN];
+        auto pf_load = [&](int ts, double* b) __attribute__((always_inline)) {
 #pragma unroll
             for (int k = 0; k < PFN; ++k) {
                 const int e = lane + WAVE * k;
-                pf[k] = e < PKT ? wb.ld(e * 8, PKB + ts * PKT * 8) : 0.0;
+                b[k] = (e < PKT && ts >= 0) ? wb.ld(e * 8, PKB + (ts > 0 ? ts : 0) * PKT * 8) : 0.0;
             }
         };
-        auto pf_store = [&](int slot) __attribute__((always_inline)) {
+        auto pf_store = [&](int ts, const double* b) __attribute__((always_inline)) {
 #pragma unroll
             for (int k = 0; k < PFN; ++k) {
                 const int e = lane + WAVE * k;
-                if (e < PKT) lds[C::F_RING + slot * PKT + e] = pf[k];
+                if (e < PKT) lds[C::F_RING + (ts & 3) * PKT + e] = b[k];
             }
         };
-        pf_load(K - 1);
-        pf_store((K - 1) & 1);
+        pf_load(K - 1, pf[0]);
+        pf_load(K - 2, pf[1]);
+        pf_load(K - 3, pf[2]);
+        pf_store(K - 1, pf[0]);
+        pf_load(K - 4, pf[0]);
         wsync();
         bool bad = false;
-        for (int ts = K - 1; ts >= 0; --ts) {
-            const int soff = (ts & 1) * PKT;
+        // one stage; buffer `nb` receives stage ts-3 (issued now), buffer `cb` holds stage ts-1
+        auto stage = [&](int ts, double* nb, const double* cb) __attribute__((always_inline)) {
+            const int soff = (ts & 3) * PKT;
             const bool last = ts == K - 1;
-            if (ts > 0) pf_load(ts - 1);
+            const int acl_off = ts * NX * NX;
+            if (ts - 3 >= 0 && ts < K - 1) pf_load(ts - 3, nb);  // (stage K-1 issued K-4 before the loop)
+            const bool fst = ts >= 20 && ts < 30;
+            if (fst) stamp(-1);
             // ---- phase 1: T1 = P'A, T2 = P'Bt, W1 = A'Pi', W2 = Bt'Pi', u = P'e, xe += Pi''e
-#pragma unroll
-            for (int rep = 0; rep < R1; ++rep) run_desc(d1[rep], qp_dot<NX>(lds, d1[rep][0], d1[rep][1], soff), soff, last, ts);
+            qp_phase<NX, R1>(lds, d1, soff, last, acl_off, wb, ts);
             wsync();
+            if (fst) stamp(11);
             // ---- phase 2: Qh = Q + A'T1, Sh = S' + Bt'T1, Rh = R + Bt'T2
-#pragma unroll
-            for (int rep = 0; rep < R2; ++rep) run_desc(d2[rep], qp_dot<NX>(lds, d2[rep][0], d2[rep][1], soff), soff, last, ts);
+            qp_phase<NX, R2>(lds, d2, soff, last, acl_off, wb, ts);
             wsync();
+            if (fst) stamp(12);
             // ---- phase 3: Rh = L D L' in registers (every lane); [K | kappa] = -Rh^-1 [Sh | W2]
             {
                 const bool fx = last && T.fix_last_input;
@@ -457,11 +534,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 }
                 if (lane < 2 * NX) {
                     const int c = lane;
-                    const int off = c < NX ? C::F_SH + c : C::F_W2 + c - NX;
+                    const int off = c < NX ? C::F_SH + c * NU : C::F_W2 + (c - NX) * NU;
                     double x[NU];
 #pragma unroll
                     for (int i = 0; i < NU; ++i) {
-                        double v = lds[off + i * NX];
+                        double v = lds[off + i];
 #pragma unroll
                         for (int k = 0; k < i; ++k) v -= Lm[i * NU + k] * x[k];
                         x[i] = v;
@@ -479,7 +556,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                     for (int i = 0; i < NU; ++i) {
                         const double v = fx ? 0.0 : -x[i];
-                        lds[C::F_KK + i * 2 * NX + c] = v;
+                        lds[C::F_KK + c * NU + i] = v;
                         wb.st((g + i * NX) * WAVE * 8, ts * 8, v);
                     }
                 }
@@ -494,16 +571,29 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 }
             }
             wsync();
+            if (fst) stamp(13);
             // ---- phase 4: P = Qh + Sh'K, Pi = W1 + Sh'kappa, M += W2'kappa, Acl = A + Bt K
-#pragma unroll
-            for (int rep = 0; rep < R4; ++rep) run_desc(d4[rep], qp_dot<NU>(lds, d4[rep][0], d4[rep][1], soff), soff, last, ts);
-            if (ts > 0) pf_store((ts - 1) & 1);
+            qp_phase<NU, R4>(lds, d4, soff, last, acl_off, wb, ts);
+            if (ts > 0) pf_store(ts - 1, cb);
             wsync();
+            if (fst) stamp(14);
+        };
+        // stage K-1 uses slot (K-1)&3 (stored), K-2 in pf[1], K-3 in pf[2], K-4 in pf[0]
+        int ts = K - 1;
+        stage(ts, pf[0], pf[1]);  // (its load of K-4 went out before the loop)
+        --ts;
+        while (ts >= 0) {
+            stage(ts, pf[1], pf[2]);
+            if (--ts < 0) break;
+            stage(ts, pf[2], pf[0]);
+            if (--ts < 0) break;
+            stage(ts, pf[0], pf[1]);
+            --ts;
         }
         if (bad) lds[V_FLAG] = 1.0;  // any lane (all agree)
         wsync();
         // Pi_0 -> persistent; LU with partial pivoting of M (lane 0, registers)
-        for (int e = lane; e < NX * NX; e += WAVE) lds[V_PI0 + e] = lds[C::F_PIP + e];
+        for (int e = lane; e < NX * NX; e += WAVE) lds[V_PI0 + e] = lds[C::F_PIP + (e % NX) * NX + e / NX];
         if (fin && lane == 0) {
             double Mr[NX * NX];
 #pragma unroll
@@ -549,10 +639,15 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     // ------------------------------------------------------------------ solve (one Newton rhs)
     // In: q (NX), r (NU) of this node (registers), e (packet), V_XI0 / V_R2F (LDS).
     // Out: dzo (NZ) = (dx_t, du_t), dyo (NX) = dy_t of this lane; V_DYI / V_DYF (LDS) the
-    // initial / terminal multiplier directions.
+    // initial / terminal multiplier directions.  Assumes a __syncthreads() since the factor.
     auto solve = [&](const double* q, const double* r, double* dzo, double* dyo) __attribute__((always_inline)) {
-        __syncthreads();  // factor columns were written by other lanes (global)
+#ifdef QPX_NOSOLVE
+        for (int i = 0; i < NZ; ++i) dzo[i] = q[i % NX] * r[0];
+        for (int i = 0; i < NX; ++i) dyo[i] = q[i];
+        return;
+#endif
         // ---- backward pre-pass: g = q + K'r + Acl'(P_{t+1} e)
+        fresh();
         if (act) {
             double g[NX];
 #pragma unroll
@@ -561,7 +656,6 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             for (int i = 0; i < NU; ++i)
 #pragma unroll
                 for (int j = 0; j < NX; ++j) g[j] = fma(cld(C::C_K + i * NX + j), r[i], g[j]);
-            double* pk = lds + S_PK + t * PKS;
             if (t < K - 1) {
                 double u[NX];
 #pragma unroll
@@ -569,31 +663,48 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                 for (int i = 0; i < NX; ++i)
 #pragma unroll
-                    for (int j = 0; j < NX; ++j) {
-                        const double v = cld(C::C_ACL + i * NX + j);
-                        pk[i * NX + j] = v;
-                        g[j] = fma(v, u[i], g[j]);
-                    }
+                    for (int j = 0; j < NX; ++j) g[j] = fma(lds[V_ACL + t * NX * NX + i * NX + j], u[i], g[j]);
             }
 #pragma unroll
-            for (int i = 0; i < NX; ++i) pk[NX * NX + i] = g[i];
+            for (int i = 0; i < NX; ++i) lds[V_G + t * NX + i] = g[i];
         }
         wsync();
-        // ---- backward chain p_t = Acl_t' p_{t+1} + g_t (lane i: element i)
+        stamp(4);
+        // ---- backward chain p_t = Acl_t' p_{t+1} + g_t (lane i: element i); p_{t+1} broadcast
+        // from lanes 0..NX-1 through readlane, the Acl column / g of the next stage read ahead
         if (lane < NX) {
-            double p = lds[S_PK + (K - 1) * PKS + NX * NX + lane];
+            double p = lds[V_G + (K - 1) * NX + lane];
             lds[V_CH + (K - 1) * NX + lane] = p;
-            for (int ts = K - 2; ts >= 0; --ts) {
-                const double* pk = lds + S_PK + ts * PKS;
-                double v = pk[NX * NX + lane];
-                wsync();
+            double an[NX], gn = 0.0;
 #pragma unroll
-                for (int k = 0; k < NX; ++k) v = fma(pk[k * NX + lane], lds[V_CH + (ts + 1) * NX + k], v);
-                lds[V_CH + ts * NX + lane] = v;
+            for (int k = 0; k < NX; ++k) an[k] = 0.0;
+            if (K >= 2) {
+#pragma unroll
+                for (int k = 0; k < NX; ++k) an[k] = lds[V_ACL + (K - 2) * NX * NX + k * NX + lane];
+                gn = lds[V_G + (K - 2) * NX + lane];
+            }
+            for (int ts = K - 2; ts >= 0; --ts) {
+                double ac[NX];
+#pragma unroll
+                for (int k = 0; k < NX; ++k) ac[k] = an[k];
+                double v0 = gn, v1 = 0.0;
+                const int tn = ts > 0 ? ts - 1 : 0;  // read ahead (clamped: no branch in the chain)
+#pragma unroll
+                for (int k = 0; k < NX; ++k) an[k] = lds[V_ACL + tn * NX * NX + k * NX + lane];
+                gn = lds[V_G + tn * NX + lane];
+#pragma unroll
+                for (int k = 0; k < NX; ++k) {
+                    const double pkv = readlane_d(p, k);
+                    if (k & 1) v1 = fma(ac[k], pkv, v1); else v0 = fma(ac[k], pkv, v0);
+                }
+                p = v0 + v1;
+                lds[V_CH + ts * NX + lane] = p;
             }
         }
         wsync();
+        stamp(5);
         // ---- backward post-pass: k0 = -Rh^-1 (r + Bt'(P_{t+1} e + p_{t+1})), xacc = sum W2'k0
+        fresh();
         double k0[NU], pv[NX], xa[NX];
 #pragma unroll
         for (int i = 0; i < NX; ++i) { xa[i] = 0.0; pv[i] = 0.0; }
@@ -671,13 +782,14 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 mu[i] = v / lds[V_M + i * NX + i];
             }
         }
+        stamp(6);
         // ---- forward pre-pass: v0 = k0 + kappa mu, f = Bt v0 + e, pi = Pi_t mu
+        fresh();
         double v0[NU], piv[NX];
 #pragma unroll
         for (int i = 0; i < NX; ++i) piv[i] = 0.0;
 #pragma unroll
         for (int j = 0; j < NU; ++j) v0[j] = k0[j];
-        wsync();  // the chain vectors above are read; the packets are rewritten below
         if (act) {
 #pragma unroll
             for (int i = 0; i < NU; ++i)
@@ -688,34 +800,51 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                 for (int j = 0; j < NX; ++j) piv[i] = fma(cld(C::C_PI + i * NX + j), mu[j], piv[i]);
             if (t < K - 1) {
-                double* pk = lds + S_PK + t * PKS;
 #pragma unroll
                 for (int i = 0; i < NX; ++i) {
                     double f = wb.ld(vpk, PKB + (C::P_E + i) * 8);
 #pragma unroll
                     for (int j = 0; j < NU; ++j) f = fma(cld(C::C_BT + i * NU + j), v0[j], f);
-                    pk[NX * NX + i] = f;
+                    lds[V_G + t * NX + i] = f;
                 }
-#pragma unroll
-                for (int e = 0; e < NX * NX; ++e) pk[e] = cld(C::C_ACL + e);
             }
         }
         wsync();
+        stamp(7);
         // ---- forward chain xi_{t+1} = Acl_t xi_t + f_t
         if (lane < NX) {
             double x = lds[V_XI0 + lane];
             lds[V_CH + lane] = x;
-            for (int ts = 0; ts < K - 1; ++ts) {
-                const double* pk = lds + S_PK + ts * PKS;
-                double v = pk[NX * NX + lane];
-                wsync();
+            double an[NX], fn = 0.0;
 #pragma unroll
-                for (int k = 0; k < NX; ++k) v = fma(pk[lane * NX + k], lds[V_CH + ts * NX + k], v);
-                lds[V_CH + (ts + 1) * NX + lane] = v;
+            for (int k = 0; k < NX; ++k) an[k] = 0.0;
+            if (K >= 2) {
+#pragma unroll
+                for (int k = 0; k < NX; ++k) an[k] = lds[V_ACL + lane * NX + k];
+                fn = lds[V_G + lane];
+            }
+            for (int ts = 0; ts < K - 1; ++ts) {
+                double ac[NX];
+#pragma unroll
+                for (int k = 0; k < NX; ++k) ac[k] = an[k];
+                double w0 = fn, w1 = 0.0;
+                const int tn = ts + 1 < K - 1 ? ts + 1 : ts;
+#pragma unroll
+                for (int k = 0; k < NX; ++k) an[k] = lds[V_ACL + tn * NX * NX + lane * NX + k];
+                fn = lds[V_G + tn * NX + lane];
+#pragma unroll
+                for (int k = 0; k < NX; ++k) {
+                    const double xk = readlane_d(x, k);
+                    if (k & 1) w1 = fma(ac[k], xk, w1); else w0 = fma(ac[k], xk, w0);
+                }
+                x = w0 + w1;
+                lds[V_CH + (ts + 1) * NX + lane] = x;
             }
         }
         wsync();
+        stamp(8);
         // ---- forward post-pass: du = K xi + v0, dx = xi + C_{t-1} du, y_{t-1} = -(P xi + p + pi)
+        fresh();
         double ym[NX];
 #pragma unroll
         for (int i = 0; i < NX; ++i) ym[i] = 0.0;
@@ -755,31 +884,48 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             dyo[i] = (t < K - 1) ? nxt : 0.0;
             if (lane == 0) { lds[V_DYI + i] = ym[i]; lds[V_DYF + i] = mu[i]; }
         }
+        stamp(9);
     };
 
-    // ------------------------------------------------------------------ state
-    double z[NZ], y[NX], s[NR], l[NR], sq[NQ], lq[NQ], av[NGA];
+    // ------------------------------------------------------------------ node state (workspace)
+    // Phase-local register copies: every node phase loads what it uses as one batch and stores
+    // what it changes, so no node-sized state is live across the sweeps.
+    double z[NZ], y[NX], s[NR], l[NR], sq[NQ], lq[NQ], av[NGA], ub[NU], sg[NSA][3], sb[NSA];
+    int bidx[NBA];
+    auto load_state = [&]() __attribute__((always_inline)) {
+        fresh();
 #pragma unroll
-    for (int i = 0; i < NX; ++i) { z[i] = act ? a.Xref[(agent * K + t) * NX + i] : 0.0; y[i] = 0.0; }
+        for (int i = 0; i < NZ; ++i) z[i] = cld(C::C_Z + i);
 #pragma unroll
-    for (int j = 0; j < NU; ++j) z[NX + j] = ub[j];
+        for (int i = 0; i < NX; ++i) y[i] = cld(C::C_Y + i);
 #pragma unroll
-    for (int g = 0; g < NGA; ++g) av[g] = 0.0;
+        for (int r = 0; r < NR; ++r) { s[r] = cld(C::C_S + r); l[r] = cld(C::C_L + r); }
 #pragma unroll
-    for (int j = 0; j < NQ; ++j) { sq[j] = 0.0; lq[j] = 0.0; }
-    if (lane < NX) { lds[V_YI + lane] = 0.0; lds[V_YF + lane] = 0.0; }
-    __syncthreads();
-
-    // ------------------------------------------------------------------ node-phase helpers
-    // soft rows (registers, reloaded per node phase)
-    double sg[NSA][3], sb[NSA];
-    auto load_soft = [&]() __attribute__((always_inline)) {
+        for (int j = 0; j < NQ; ++j) { sq[j] = cld(C::C_SQ + j); lq[j] = cld(C::C_LQ + j); }
+#pragma unroll
+        for (int g = 0; g < NGA; ++g) av[g] = g < NG ? cld(C::C_AV + g) : 0.0;
+#pragma unroll
+        for (int j = 0; j < NU; ++j) ub[j] = cld(C::C_UB + j);
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
 #pragma unroll
             for (int i = 0; i < 3; ++i) sg[q][i] = cld(C::C_SOFT + q * 4 + i);
             sb[q] = cld(C::C_SOFT + q * 4 + 3);
         }
+#pragma unroll
+        for (int b = 0; b < NB; ++b) bidx[b] = qp_opaque(T.box_idx[b]);
+    };
+    auto store_state = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) cst(C::C_Z + i, z[i]);
+#pragma unroll
+        for (int i = 0; i < NX; ++i) cst(C::C_Y + i, y[i]);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) { cst(C::C_S + r, s[r]); cst(C::C_L + r, l[r]); }
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) { cst(C::C_SQ + j, sq[j]); cst(C::C_LQ + j, lq[j]); }
+#pragma unroll
+        for (int g = 0; g < NG; ++g) cst(C::C_AV + g, av[g]);
     };
     auto grp_on = [&](int g) __attribute__((always_inline)) -> bool { return ineq && (g < NO ? g < nobs : has_coll); };
     auto row_on = [&](int r) __attribute__((always_inline)) -> bool {
@@ -807,7 +953,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             }
         } else if (r < C::R_OBS) {
             const int b = (r - C::R_BOX) >> 1, lo = (r - C::R_BOX) & 1;
-            const double xi = sel_x(zz, T.box_idx[b]);
+            const double xi = sel_x(zz, bidx[b]);
             gz = lo ? -xi : xi; h = lo ? -T.box_lo[b] : T.box_hi[b];
         } else if (r < C::R_GRP) {
             const int q = r - C::R_OBS, g = q < NO ? q : NO;
@@ -823,7 +969,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
             for (int j = 0; j < NU; ++j) gzv[NX + j] += ((r >> j) & 1) ? -c : c;
         } else if (r < C::R_OBS) {
-            const int b = (r - C::R_BOX) >> 1, lo = (r - C::R_BOX) & 1, idx = T.box_idx[b];
+            const int b = (r - C::R_BOX) >> 1, lo = (r - C::R_BOX) & 1, idx = bidx[b];
 #pragma unroll
             for (int i = 0; i < NX; ++i) gzv[i] = fma(qp_mask(i, idx), lo ? -c : c, gzv[i]);
         } else if (r < C::R_GRP) {
@@ -846,8 +992,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     };
     auto gweight = [&](int g) __attribute__((always_inline)) -> double { return g < NO ? T.w_obs : T.w_coll; };
 
-    // Node Hessian (row scaling D_r, SOC block Wi2uu) -> packet Q, S, R (xi/u coordinates); group
-    // elimination factors -> columns C_GRP.  Also writes e = -rp into the packet.
+    // Node Hessian (row scaling D_r = l/s or 1, SOC block Wi2uu) -> packet Q, S, R (xi/u
+    // coordinates); group elimination factors -> columns C_GRP.  Also writes e = -rp.
     auto assemble = [&](bool unit, const double* Wi2uu, const double* rp) __attribute__((always_inline)) {
         double dbox[NX], Hpp[3][3], Huu[NU * NU];
 #pragma unroll
@@ -870,7 +1016,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                     for (int j = 0; j < NU; ++j) Huu[i * NU + j] += (((r >> i) ^ (r >> j)) & 1) ? -Dr : Dr;
             } else if (r < C::R_OBS) {
-                const int idx = T.box_idx[(r - C::R_BOX) >> 1];
+                const int idx = bidx[(r - C::R_BOX) >> 1];
 #pragma unroll
                 for (int i = 0; i < NX; ++i) dbox[i] = fma(qp_mask(i, idx), Dr, dbox[i]);
             } else if (r < C::R_GRP) {
@@ -934,8 +1080,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
         for (int i = 0; i < NX; ++i) pst(C::P_E + i, (t < K - 1) ? -rp[i] : 0.0);
     };
-    // eliminate the group part of a Newton rhs: r1_p -= sum_g Hpa_g r1a_g / Haa_g ; returns the
-    // (xi, u) linear terms q, r of the node
+    // eliminate the group part of a Newton rhs (stores it for recover_aux): r1_p -= Hpa/Haa r1a;
+    // returns the (xi, u) linear terms q, r of the node
     auto reduce_rhs = [&](double* r1, const double* r1a, double* q, double* r) __attribute__((always_inline)) {
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
@@ -1018,16 +1164,24 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         return best;
     };
     // NT scaling W = eta [[w0, w1'], [w1, I + w1 w1'/(1 + w0)]], W^-1 the same with -w1, 1/eta
-    auto w_apply = [&](const double* w, double eta, bool inv, const double* x, double* y) __attribute__((always_inline)) {
+    auto w_apply = [&](const double* w, double eta, bool inv, const double* x, double* yv) __attribute__((always_inline)) {
         const double sgn = inv ? -1.0 : 1.0, sc = inv ? 1.0 / eta : eta;
         double d = 0.0;
 #pragma unroll
         for (int j = 1; j < NQ; ++j) d += w[j] * x[j];
         d *= sgn;
-        y[0] = sc * (w[0] * x[0] + d);
+        yv[0] = sc * (w[0] * x[0] + d);
         const double f = x[0] + d / (1.0 + w[0]);
 #pragma unroll
-        for (int j = 1; j < NQ; ++j) y[j] = sc * (x[j] + sgn * w[j] * f);
+        for (int j = 1; j < NQ; ++j) yv[j] = sc * (x[j] + sgn * w[j] * f);
+    };
+    // SOC scaling of the iteration (columns C_WV..C_RHO)
+    double wv[NQ], eta = 1.0, ltq[NQ], rcq[NQ];
+    auto load_soc = [&]() __attribute__((always_inline)) {
+        fresh();
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) { wv[j] = cld(C::C_WV + j); ltq[j] = cld(C::C_LTQ + j); rcq[j] = cld(C::C_RCQ + j); }
+        eta = cld(C::C_ETA);
     };
 
     int status = SCVX_STATUS_MAX_ITER;
@@ -1037,7 +1191,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     // minimiser of 1/2 z'Pz + q'z + 1/2 ||Gz - h||^2 s.t. Az = b from z_ref (aux = 0), unit scaling
     // (CVXOPT coneqp initialisation; oracle/qp_dense.py does the same on the dense form)
     {
-        load_soft();
+        load_state();
+#pragma unroll
+        for (int r = 0; r < NR; ++r) { s[r] = 1.0; l[r] = 0.0; }
         double Wu[NU * NU], rp[NX];
 #pragma unroll
         for (int e = 0; e < NU * NU; ++e) Wu[e] = (e / NU == e % NU) ? 1.0 : 0.0;
@@ -1060,10 +1216,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         reduce_rhs(r1, r1a, q, rr);
         set_boundary(z);
         if (!factor()) status = SCVX_STATUS_NUMERICAL;
+        __syncthreads();  // factor columns (global) -> lane-parallel solve passes
         double dz[NZ], dy[NX], da[NGA];
         solve(q, rr, dz, dy);
         recover_aux(dz, da);
-        load_soft();
+        load_state();
 #pragma unroll
         for (int i = 0; i < NZ; ++i) z[i] += act ? dz[i] : 0.0;
 #pragma unroll
@@ -1078,6 +1235,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             l[r] = on ? gz - h : 0.0;
             if (on) { smin = fmin(smin, h - gz); lmin = fmin(lmin, gz - h); }
         }
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) { sq[j] = 0.0; lq[j] = 0.0; }
         if (soc) {
             double nu2 = 0.0;
             sq[0] = T.u_max; lq[0] = -T.u_max;
@@ -1093,6 +1252,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             if (row_on(r)) { s[r] += shs; l[r] += shl; }
         }
         if (soc) { sq[0] += shs; lq[0] += shl; }
+        store_state();
     }
     double degl = 0.0;
 #pragma unroll
@@ -1105,9 +1265,10 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     if (has_coll) qscl = fmax(qscl, T.w_coll);
 
     // ------------------------------------------------------------------ IPM iterations
-    long long cyc_factor = 0, cyc_solve = 0, cyc_all0 = __builtin_amdgcn_s_memtime();
+    const long long cyc_all0 = __builtin_amdgcn_s_memtime();
+    stamp(-1);
     for (it = 0; it < T.max_iter && status != SCVX_STATUS_NUMERICAL; ++it) {
-        load_soft();
+        load_state();
         double rp[NX];
         dyn_residual(z, rp);
         // dual residual rd = Pz + q + A'y + G'lam (z and group parts)
@@ -1141,7 +1302,6 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 row_accT(r, l[r], rd, rda);
             }
         }
-        double rcq[NQ];
         if (soc) {
             rcq[0] = sq[0] - T.u_max;
 #pragma unroll
@@ -1212,9 +1372,10 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         // ECOS-style reduced accuracy: what a numerical breakdown below leaves is still usable
         const bool near = pres <= 1e-6 * hsc && dres <= 1e-6 * qscl && gap <= 1e-6 * fmax(1.0, fabs(pobj));
         // SOC Nesterov-Todd scaling (hyperbolic-rotation form, W lam = W^-1 s)
-        double wv[NQ], eta = 1.0, ltq[NQ], Wi2uu[NU * NU];
+        double Wi2uu[NU * NU];
 #pragma unroll
         for (int j = 0; j < NQ; ++j) { wv[j] = 0.0; ltq[j] = 0.0; }
+        eta = 1.0;
 #pragma unroll
         for (int e = 0; e < NU * NU; ++e) Wi2uu[e] = 0.0;
         if (soc) {
@@ -1253,25 +1414,31 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                     Wi2uu[i * NU + j] = v;
                 }
         }
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) { cst(C::C_WV + j, wv[j]); cst(C::C_LTQ + j, ltq[j]); cst(C::C_RCQ + j, rcq[j]); }
+        cst(C::C_ETA, eta);
         assemble(false, Wi2uu, rp);
         set_boundary(z);
-        long long st0 = __builtin_amdgcn_s_memtime();
+        stamp(0);
         if (!factor()) { status = near ? SCVX_STATUS_MAX_ITER : SCVX_STATUS_NUMERICAL; fail_code = lds[V_FLAG]; break; }
-        cyc_factor += __builtin_amdgcn_s_memtime() - st0;
+        stamp(1);
 
-        // Newton direction for complementarity rhs rco (rows) / rcq2 (SOC); directions out
-        double dz[NZ], dy[NX], da[NGA], dsq[NQ], dlq[NQ], rho[NQ];
         // complementarity rhs of row r: predictor -s l ; corrector -s l - ds_a dl_a + sigma mu
         double sgmu = 0.0;
+        double dz[NZ], dy[NX], da[NGA], dsq[NQ], dlq[NQ], cpv[NR];
         auto rco_of = [&](int r, bool corr) __attribute__((always_inline)) -> double {
             const double v = -s[r] * l[r];
-            return corr ? v - lds[V_CP + r * WAVE + lane] + sgmu : v;
+            return corr ? v - cpv[r] + sgmu : v;
         };
+        // Newton direction for the complementarity rhs (rows: rco_of, SOC: rcq2); directions out
         auto newton = [&](bool corr, const double* rcq2) __attribute__((always_inline)) {
-            load_soft();
-            double r1[NZ], r1a[NGA];
+            load_state();
+            load_soc();
+            double r1[NZ], r1a[NGA], rho[NQ];
 #pragma unroll
             for (int i = 0; i < NZ; ++i) r1[i] = act ? -cld(C::C_RD + i) : 0.0;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) cpv[r] = corr ? cld(C::C_CP + r) : 0.0;
 #pragma unroll
             for (int g = 0; g < NGA; ++g) r1a[g] = -gweight(g);
 #pragma unroll
@@ -1302,13 +1469,16 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                 for (int i = 0; i < NU; ++i) r1[NX + i] += w3[1 + i];
             }
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) cst(C::C_RHO + j, rho[j]);
             double q[NX], rr[NU];
             reduce_rhs(r1, r1a, q, rr);
-            long long st1 = __builtin_amdgcn_s_memtime();
+            stamp(2);
             solve(q, rr, dz, dy);
-            cyc_solve += __builtin_amdgcn_s_memtime() - st1;
+            // post-solve: group and SOC directions (state reloaded: nothing crossed the sweeps)
+            load_state();
+            load_soc();
             recover_aux(dz, da);
-            load_soft();
             if (soc) {
                 double v2[NQ], w2[NQ];
                 dsq[0] = -rcq[0];
@@ -1317,12 +1487,14 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 for (int j = 1; j < NQ; ++j) { dsq[j] = -rcq[j] + dz[NX + j - 1]; v2[j] = rcq[j] - dz[NX + j - 1]; }
                 w_apply(wv, eta, true, v2, w2);
 #pragma unroll
-                for (int j = 0; j < NQ; ++j) w2[j] += rho[j];
+                for (int j = 0; j < NQ; ++j) w2[j] += cld(C::C_RHO + j);
                 w_apply(wv, eta, true, w2, dlq);
             } else {
 #pragma unroll
                 for (int j = 0; j < NQ; ++j) { dsq[j] = 0.0; dlq[j] = 0.0; }
             }
+#pragma unroll
+            for (int r = 0; r < NR; ++r) cpv[r] = corr ? cld(C::C_CP + r) : 0.0;
         };
         // row directions ds = -rc - G d, dl = (rco + l (rc + G d)) / s
         auto row_dir = [&](int r, bool corr, double& dsr, double& dlr) __attribute__((always_inline)) {
@@ -1350,16 +1522,22 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 
         // ---- predictor (affine scaling)
         double rcq2[NQ];
-        if (soc) {
-            double d0 = 0.0;
+        load_soc();
+        {
+            double ltq0[NQ];
 #pragma unroll
-            for (int j = 0; j < NQ; ++j) d0 += ltq[j] * ltq[j];
-            rcq2[0] = -d0;
+            for (int j = 0; j < NQ; ++j) ltq0[j] = ltq[j];
+            if (soc) {
+                double d0 = 0.0;
 #pragma unroll
-            for (int j = 1; j < NQ; ++j) rcq2[j] = -2.0 * ltq[0] * ltq[j];
-        } else {
+                for (int j = 0; j < NQ; ++j) d0 += ltq0[j] * ltq0[j];
+                rcq2[0] = -d0;
 #pragma unroll
-            for (int j = 0; j < NQ; ++j) rcq2[j] = 0.0;
+                for (int j = 1; j < NQ; ++j) rcq2[j] = -2.0 * ltq0[0] * ltq0[j];
+            } else {
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) rcq2[j] = 0.0;
+            }
         }
         newton(false, rcq2);
         const double aa = fmin(1.0, max_step(false));
@@ -1370,7 +1548,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 double dsr, dlr;
                 row_dir(r, false, dsr, dlr);
                 gap_a += (s[r] + aa * dsr) * (l[r] + aa * dlr);
-                lds[V_CP + r * WAVE + lane] = dsr * dlr;
+                cst(C::C_CP + r, dsr * dlr);
             }
         }
         if (soc) {
@@ -1394,8 +1572,10 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             for (int j = 1; j < NQ; ++j) rcq2[j] -= a1[0] * b1[j] + b1[0] * a1[j];
             rcq2[0] += sgmu;
         }
+        stamp(3);
         newton(true, rcq2);
         const double al = fmin(1.0, 0.99 * max_step(true));
+        stamp(3);
         {
             double chk = al;
 #pragma unroll
@@ -1433,17 +1613,21 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
             for (int i = 0; i < NX; ++i) y[i] += al * dy[i];
         }
+        store_state();
         if (lane < NX) {
             lds[V_YI + lane] += al * lds[V_DYI + lane];
             lds[V_YF + lane] += al * lds[V_DYF + lane];
         }
+        stamp(10);
     }
 
     // ------------------------------------------------------------------ outputs
+    load_state();
     if (a.trace && agent == a.trace_agent && lane == 0) {
         double* dd = a.trace + 8 * a.trace_cap;
-        dd[0] = (double)cyc_factor; dd[1] = (double)cyc_solve; dd[2] = (double)(__builtin_amdgcn_s_memtime() - cyc_all0);
+        dd[0] = 0.0; dd[1] = 0.0; dd[2] = (double)(__builtin_amdgcn_s_memtime() - cyc_all0);
         dd[3] = fail_code;
+        for (int k = 0; k < 15; ++k) dd[4 + k] = lds[V_ST + k];
     }
     double pobj = 0.0;
     if (act) {
@@ -1466,7 +1650,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 // launch helpers (qp_capi.hip picks the instantiation)
 template <class C>
 int qp_launch(const QPArgs& a, hipStream_t st) {
-    const size_t lds = sizeof(double) * (size_t)qp_lds_doubles(C::NX, C::NU, a.T.K, C::NR);
+    const size_t lds = sizeof(double) * (size_t)C::lds_doubles(a.T.K);
     if (lds > 65536) (void)hipFuncSetAttribute((const void*)qp_ipm_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(qp_ipm_kernel<C>, dim3(a.N), dim3(WAVE), lds, st, a);
     return check_launch("qp_ipm_kernel");

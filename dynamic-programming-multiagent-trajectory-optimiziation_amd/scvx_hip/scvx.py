@@ -84,8 +84,10 @@ class JacobiSCvx:
             self.torch.distributed.all_gather_into_tensor(self.X_all, X.contiguous(), group=self.group)
         return self.X_all
 
-    def step(self, X, U):
-        """One SCvx iteration; returns the new (X, U) (device tensors owned by the solver)."""
+    def step(self, X, U, qp_events=None):
+        """One SCvx iteration; returns the new (X, U) (device tensors owned by the solver).
+        qp_events: optional list; a (start, end) pair of timing events recorded on the launch
+        stream around the QP kernel is appended to it."""
         torch = self.torch
         spec = self.spec
         self.disc = self.backend.foh(spec.model, X, U, self.sigma, self.nsub, self.disc)
@@ -94,7 +96,13 @@ class JacobiSCvx:
             X_all = self.gather_states(X)
             rows, count = self.backend.collision_rows(X_all, self.i0, self.N, self.coupling.R, spec.j_max,
                                                       spec.pos_dim, self.coupling.cull_radius, self.rows, self.count)
+        if qp_events is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(torch.cuda.current_stream())
         out = self.solver.solve(self.disc, self.sigma, X, U, self.x_init, self.x_final, self.tr, rows, count)
+        if qp_events is not None:
+            e1.record(torch.cuda.current_stream())
+            qp_events.append((e0, e1))
         Xn, Un = out["X"], out["U"]
         # cost_fcn (dist_scvx_3d.py:131-138) and the trust-region halving rule (:250-252)
         cost = (Un[:, :-1, :] * Un[:, :-1, :]).sum(dim=(1, 2))

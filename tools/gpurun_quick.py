@@ -6,12 +6,13 @@ import scvx_hip
 from oracle import problems as pb
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 K = 50
-sc = pb.synthetic_di(N, K=K, seed=1, obstacles=8)
+NOBS = int(os.environ.get("OBS", "8"))
+sc = pb.synthetic_di(N, K=K, seed=1, obstacles=NOBS)
 d = torch.device("cuda")
 X, U, sig = [torch.tensor(sc[k], device=d) for k in ("X", "U", "sigma")]
 xi, xf = torch.tensor(sc["x_init"], device=d), torch.tensor(sc["x_final"], device=d)
 tr = torch.full((N,), 0.25, dtype=torch.float64, device=d)
-spec = scvx_hip.QPSpec(model="di", K=K, box=[(0,-12,12),(1,-12,12)], obs=sc["obs"], u_max=1.0, max_iter=60)
+spec = scvx_hip.QPSpec(model="di", K=K, box=[(0,-12,12),(1,-12,12)], obs=sc["obs"] if NOBS else (), u_max=1.0 if os.environ.get("SOC", "1") == "1" else None, max_iter=60)
 solver = scvx_hip.QPSolver(spec, N)
 for rep in range(3):
     torch.cuda.synchronize(); t0 = time.time()
@@ -23,13 +24,17 @@ for rep in range(3):
     print(f"N={N} foh {1e3*(t1-t0):.3f} ms  qp {1e3*(t2-t1):.3f} ms  status {np.bincount(st, minlength=3)}  iters mean {it.mean():.1f} max {it.max()}", flush=True)
 if os.environ.get("TRACE"):
     import ctypes
-    buf = torch.zeros(8 * 80 + 16, dtype=torch.float64, device=d)
+    buf = torch.zeros(8 * 80 + 20, dtype=torch.float64, device=d)
     scvx_hip.lib().scvx_qp_set_trace(ctypes.c_void_p(buf.data_ptr()), 0, 80)
     out = solver.solve(disc, sig, X, U, xi, xf, tr)
     torch.cuda.synchronize()
     b = buf[:640].view(80, 8).cpu().numpy()
-    cyc = buf[640:644].cpu().numpy()
-    n_it = int(out["iters"][0].item())
-    print(f"cycles: factor {cyc[0]:.3e} ({cyc[0]/max(n_it,1):.3e}/it)  solve {cyc[1]:.3e} ({cyc[1]/max(n_it,1)/2:.3e}/solve)  total {cyc[2]:.3e} ({cyc[2]/max(n_it,1):.3e}/it)  fail {cyc[3]}")
+    cyc = buf[640:660].cpu().numpy()
+    n_it = max(int(out["iters"][0].item()), 1)
+    names = ["node+assemble", "factor", "newton rhs", "post-solve/step", "bwd pre", "bwd chain", "bwd post+mu",
+             "fwd pre", "fwd chain", "fwd post", "update", "f-ph1 x10st", "f-ph2 x10st", "f-ph3 x10st", "f-ph4 x10st"]
+    print(f"total {cyc[2]:.3e} cycles, {cyc[2]/n_it:.3e}/it, fail {cyc[3]}")
+    for k, nm in enumerate(names):
+        print(f"  {nm:16s} {cyc[4+k]/n_it:10.0f} cycles/it  ({100*cyc[4+k]/cyc[2]:.1f}%)")
     for i in range(int(out["iters"][0].item())):
         print("it %2d pres %.2e dres %.2e gap %.2e pobj %.6e aa %.3f al %.3f sg %.2e mu %.2e" % ((i,) + tuple(b[i])))
