@@ -27,7 +27,7 @@
 //   * factor sweep -- sequential over stages, element-parallel over lanes: 4 straight-line
 //                     phases per stage, each lane's output element picked by a packed
 //                     descriptor (no per-stage branching); stage packets are prefetched three
-//                     stages ahead into a 4-slot LDS ring;
+//                     stages ahead (register buffers) into a 2-slot LDS ring;
 //   * solves       -- closed-loop form.  With Acl_t = A_t + Bt_t K_t (kept in LDS by the factor)
 //                     the backward pass is the chain p_t = Acl_t' p_{t+1} + g_t and the forward
 //                     pass the chain xi_{t+1} = Acl_t xi_t + f_t: g_t, f_t and every output off
@@ -78,7 +78,7 @@ constexpr int qp_ncol(int nx, int nu, int nb, int ns, int ng) {
     // disc^T | K kappa LD W2 P Pi u | Bt | soft rows | groups | rd | r1a | cP | ub | node state | SOC
     return qp_dstr(nx, nu) + 3 * nu * nx + nu * nu + 2 * nx * nx + nx + nx * nu + 4 * ns + 4 * ng + (nx + nu) + ng +
            ((1 << nu) + 2 * nb + ns + ng) + nu +
-           (2 * ((1 << nu) + 2 * nb + ns + ng) + (nx + nu) + nx + 2 * (nu + 1) + ng) + (3 * (nu + 1) + 1 + (nu + 1));
+           ((nx + nu) + nx + 2 * (nu + 1) + ng) + (3 * (nu + 1) + 1 + (nu + 1)) + nx * nx;
 }
 constexpr long long qp_ws_doubles(int nx, int nu, int nb, int ns, int ng) {
     return (long long)qp_ncol(nx, nu, nb, ns, ng) * 64 + 64LL * qp_pkt(nx, nu);
@@ -117,26 +117,27 @@ struct QPCfg {
     static constexpr int C_CP = C_R1A + NG;        // predictor products ds_a dl_a per row
     static constexpr int C_UB = C_CP + NR;         // reference input ubar_t
     // node state
-    static constexpr int C_S = C_UB + NU, C_L = C_S + NR, C_Z = C_L + NR, C_Y = C_Z + NZ, C_SQ = C_Y + NX,
+    static constexpr int C_Z = C_UB + NU, C_Y = C_Z + NZ, C_SQ = C_Y + NX,
                          C_LQ = C_SQ + NQ, C_AV = C_LQ + NQ;
     // SOC scaling of the current iteration: w (NQ), eta, W lam (NQ), rc (NQ), rho (NQ)
     static constexpr int C_WV = C_AV + NG, C_ETA = C_WV + NQ, C_LTQ = C_ETA + 1, C_RCQ = C_LTQ + NQ,
                          C_RHO = C_RCQ + NQ;
-    static constexpr int NCOL = C_RHO + NQ;
+    static constexpr int C_ACL = C_RHO + NQ;       // Acl_t = A_t + Bt_t K_t (row-major)
+    static constexpr int NCOL = C_ACL + NX * NX;
     static_assert(NCOL == qp_ncol(NX, NU, NB, NS, NG), "column count");
     // LDS (doubles, compile-time offsets except the K-sized blocks at the end):
-    // factor: 4-slot packet ring, P', Pi' (col-major), T1, T2 (col-major), W1, W2 (col-major), Qh,
+    // factor: 2-slot packet ring, P', Pi' (col-major), T1, T2 (col-major), W1, W2 (col-major), Qh,
     // Sh (col-major), Rh, [K | kappa] (col-major), sink
-    static constexpr int F_RING = 0, F_PP = 4 * PKT, F_PIP = F_PP + NX * NX, F_T1 = F_PIP + NX * NX,
+    static constexpr int F_RING = 0, F_PP = 2 * PKT, F_PIP = F_PP + NX * NX, F_T1 = F_PIP + NX * NX,
                          F_T2 = F_T1 + NX * NX, F_W1 = F_T2 + NX * NU, F_W2 = F_W1 + NX * NX,
                          F_QH = F_W2 + NU * NX, F_SH = F_QH + NX * NX, F_RH = F_SH + NU * NX,
                          F_KK = F_RH + NU * NU, F_SINK = F_KK + 2 * NU * NX, F_END = qp_even(F_SINK + 8);
     static constexpr int L_M = F_END, L_PI0 = L_M + NX * NX, L_XE = L_PI0 + NX * NX, L_XI0 = L_XE + NX,
                          L_R2F = L_XI0 + NX, L_YI = L_R2F + NX, L_YF = L_YI + NX, L_DYI = L_YF + NX,
                          L_DYF = L_DYI + NX, L_PIV = L_DYF + NX, L_ONE = L_PIV + NX, L_FLAG = L_ONE + 1,
-                         L_ST = qp_even(L_FLAG + 4), L_VAR = L_ST + 16;
-    // K-sized: Acl [K][NX*NX] (row-major), chain offsets g/f [K][NX], chain vectors [K+1][NX]
-    static constexpr int lds_doubles(int K) { return L_VAR + K * NX * NX + K * NX + (K + 1) * NX; }
+                         L_ST = qp_even(L_FLAG + 4), L_S = L_ST + 16, L_L = L_S + NR * 64, L_VAR = L_L + NR * 64;
+    // row slacks s / duals lambda [r][lane]; then K-sized: chain offsets g/f [K][NX], chain vectors [K+1][NX]
+    static constexpr int lds_doubles(int K) { return L_VAR + K * NX + (K + 1) * NX; }
 };
 
 // packed phase descriptors (all operands are contiguous LDS vectors):
@@ -214,7 +215,9 @@ __device__ __forceinline__ void qp_phase(double* lds, const int (&d)[NREP][4], i
             const double old = lds[oo];
             lds[oo] = ((O >> 15) & 1) ? old + val[r] : val[r];
             const int g = (O >> 17) - 1;
+#ifndef QPX_NOGST
             if (g >= 0) wb.st(g * WAVE * 8, ts * 8, val[r]);
+#endif
         }
     }
 }
@@ -257,12 +260,23 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     auto fresh = [&]() __attribute__((always_inline)) { vcur = qp_opaque(vt); };
     auto cld = [&](int c) __attribute__((always_inline)) -> double { return wb.ld(vcur, c * WAVE * 8); };
     auto cst = [&](int c, double v) __attribute__((always_inline)) { wb.st(vt, c * WAVE * 8, v); };
+    // Batched loads: ldn issues the loads of n consecutive columns, hold pins values in registers.
+    // Issue every load of a phase first and hold them before the first use, so the phase pays one
+    // memory round trip (the scheduler otherwise serialises load -> wait -> use under pressure).
+    auto ldn = [&](double* dst, int c0, int n) __attribute__((always_inline)) {
+#pragma unroll
+        for (int e = 0; e < n; ++e) dst[e] = cld(c0 + e);
+    };
+    auto hold = [&](double* v, int n) __attribute__((always_inline)) {
+#pragma unroll
+        for (int e = 0; e < n; ++e) asm volatile("" : "+v"(v[e]));
+    };
     auto pst = [&](int e, double v) __attribute__((always_inline)) { wb.st(vpk, PKB + e * 8, v); };
 
     constexpr int V_M = C::L_M, V_PI0 = C::L_PI0, V_XE = C::L_XE, V_XI0 = C::L_XI0, V_R2F = C::L_R2F,
                   V_YI = C::L_YI, V_YF = C::L_YF, V_DYI = C::L_DYI, V_DYF = C::L_DYF, V_PIV = C::L_PIV,
-                  V_ONE = C::L_ONE, V_FLAG = C::L_FLAG, V_ST = C::L_ST, V_ACL = C::L_VAR;
-    const int V_G = V_ACL + K * NX * NX, V_CH = V_G + K * NX;
+                  V_ONE = C::L_ONE, V_FLAG = C::L_FLAG, V_ST = C::L_ST, V_S = C::L_S, V_L = C::L_L;
+    const int V_G = C::L_VAR, V_CH = V_G + K * NX;
     // region timers of the traced agent (diagnostics): cycles since the previous stamp -> V_ST[i]
     const bool stamp_on = a.trace && agent == a.trace_agent;
     long long tprev = 0;
@@ -364,10 +378,10 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     // C_{t-1} (column-major as disc) of this node, from the transposed disc at stage t-1
     auto load_cp = [&](double* Cp) __attribute__((always_inline)) {
 #pragma unroll
-        for (int e = 0; e < NX * NU; ++e) {
-            const double v = wb.ld(vcur - 8, (C::C_DT + NX * NX + NX * NU + e) * WAVE * 8);
-            Cp[e] = (t > 0) ? v : 0.0;
-        }
+        for (int e = 0; e < NX * NU; ++e) Cp[e] = wb.ld(vcur - 8, (C::C_DT + NX * NX + NX * NU + e) * WAVE * 8);
+        hold(Cp, NX * NU);
+#pragma unroll
+        for (int e = 0; e < NX * NU; ++e) Cp[e] = (t > 0) ? Cp[e] : 0.0;
     };
 
     // ------------------------------------------------------------------ factor sweep
@@ -446,7 +460,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 } else if ((o -= NX * NX) < NX * NX) {  // Acl = A + Bt K  -> LDS Acl block of the stage
                     const int i = o / NX, j = o % NX;
                     L = qp_dpk(C::P_BTR + i * NU, 1); R = qp_dpk(C::F_KK + j * NU, 0);
-                    O = (V_ACL + o) | (1 << 16); B = (C::P_A + j * NX + i) | (1 << 15) | (1 << 16);
+                    O = sink | ((C::C_ACL + o + 1) << 17); B = (C::P_A + j * NX + i) | (1 << 15) | (1 << 16);
                 }
                 d4[rep][0] = L; d4[rep][1] = R; d4[rep][2] = O; d4[rep][3] = B;
             }
@@ -455,7 +469,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         if (lane < NX) lds[V_XE + lane] = 0.0;
         if (lane == 0) lds[V_FLAG] = 0.0;
         __syncthreads();  // the node phase wrote the packets (global) from other lanes
-        // packets stream through a 4-slot ring, loads issued 3 stages ahead (register buffers
+        // packets stream through a 2-slot LDS ring, loads issued 3 stages ahead (register buffers
         // pf[0..2], so the stage loop is unrolled by 3 to keep their indices static)
         double pf[3][PFN];
         auto pf_load = [&](int ts, double* b) __attribute__((always_inline)) {
@@ -469,7 +483,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
             for (int k = 0; k < PFN; ++k) {
                 const int e = lane + WAVE * k;
-                if (e < PKT) lds[C::F_RING + (ts & 3) * PKT + e] = b[k];
+                if (e < PKT) lds[C::F_RING + (ts & 1) * PKT + e] = b[k];
             }
         };
         pf_load(K - 1, pf[0]);
@@ -481,7 +495,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         bool bad = false;
         // one stage; buffer `nb` receives stage ts-3 (issued now), buffer `cb` holds stage ts-1
         auto stage = [&](int ts, double* nb, const double* cb) __attribute__((always_inline)) {
-            const int soff = (ts & 3) * PKT;
+            const int soff = (ts & 1) * PKT;
             const bool last = ts == K - 1;
             const int acl_off = ts * NX * NX;
             if (ts - 3 >= 0 && ts < K - 1) pf_load(ts - 3, nb);  // (stage K-1 issued K-4 before the loop)
@@ -557,7 +571,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                     for (int i = 0; i < NU; ++i) {
                         const double v = fx ? 0.0 : -x[i];
                         lds[C::F_KK + c * NU + i] = v;
+#ifndef QPX_NOGST
                         wb.st((g + i * NX) * WAVE * 8, ts * 8, v);
+#endif
                     }
                 }
                 if (lane < NU * NU) {
@@ -567,7 +583,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                         const int ei = e / NU, ej = e % NU;
                         v = fma(qp_mask(e, lane), (ei > ej) ? Lm[e] : (ei == ej ? dinv[ei] : 0.0), v);
                     }
+#ifndef QPX_NOGST
                     wb.st((C::C_LD + lane) * WAVE * 8, ts * 8, v);
+#endif
                 }
             }
             wsync();
@@ -578,7 +596,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             wsync();
             if (fst) stamp(14);
         };
-        // stage K-1 uses slot (K-1)&3 (stored), K-2 in pf[1], K-3 in pf[2], K-4 in pf[0]
+        // stage K-1 uses slot (K-1)&1 (stored), K-2 in pf[1], K-3 in pf[2], K-4 in pf[0]
         int ts = K - 1;
         stage(ts, pf[0], pf[1]);  // (its load of K-4 went out before the loop)
         --ts;
@@ -649,21 +667,24 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         // ---- backward pre-pass: g = q + K'r + Acl'(P_{t+1} e)
         fresh();
         if (act) {
-            double g[NX];
+            double g[NX], Kt[NU * NX], u[NX], Ac[NX * NX];
+            ldn(Kt, C::C_K, NU * NX);
+            ldn(u, C::C_U, NX);
+            ldn(Ac, C::C_ACL, NX * NX);
+            hold(Kt, NU * NX);
+            hold(u, NX);
+            hold(Ac, NX * NX);
 #pragma unroll
             for (int i = 0; i < NX; ++i) g[i] = q[i];
 #pragma unroll
             for (int i = 0; i < NU; ++i)
 #pragma unroll
-                for (int j = 0; j < NX; ++j) g[j] = fma(cld(C::C_K + i * NX + j), r[i], g[j]);
+                for (int j = 0; j < NX; ++j) g[j] = fma(Kt[i * NX + j], r[i], g[j]);
             if (t < K - 1) {
-                double u[NX];
-#pragma unroll
-                for (int i = 0; i < NX; ++i) u[i] = cld(C::C_U + i);
 #pragma unroll
                 for (int i = 0; i < NX; ++i)
 #pragma unroll
-                    for (int j = 0; j < NX; ++j) g[j] = fma(lds[V_ACL + t * NX * NX + i * NX + j], u[i], g[j]);
+                    for (int j = 0; j < NX; ++j) g[j] = fma(Ac[i * NX + j], u[i], g[j]);
             }
 #pragma unroll
             for (int i = 0; i < NX; ++i) lds[V_G + t * NX + i] = g[i];
@@ -673,32 +694,39 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         // ---- backward chain p_t = Acl_t' p_{t+1} + g_t (lane i: element i); p_{t+1} broadcast
         // from lanes 0..NX-1 through readlane, the Acl column / g of the next stage read ahead
         if (lane < NX) {
-            double p = lds[V_G + (K - 1) * NX + lane];
-            lds[V_CH + (K - 1) * NX + lane] = p;
-            double an[NX], gn = 0.0;
+            // lane i needs column i of Acl_t: ws columns C_ACL + k*NX + i at stage index ts
+            // (L1-resident after the first touch of each line), loaded two stages ahead
+            const int va = (C::C_ACL + lane) * WAVE * 8;
+            auto ldA = [&](int ts, double* an, double& gn) __attribute__((always_inline)) {
+                const int tc = ts > 0 ? ts : 0;
 #pragma unroll
-            for (int k = 0; k < NX; ++k) an[k] = 0.0;
-            if (K >= 2) {
-#pragma unroll
-                for (int k = 0; k < NX; ++k) an[k] = lds[V_ACL + (K - 2) * NX * NX + k * NX + lane];
-                gn = lds[V_G + (K - 2) * NX + lane];
-            }
-            for (int ts = K - 2; ts >= 0; --ts) {
-                double ac[NX];
-#pragma unroll
-                for (int k = 0; k < NX; ++k) ac[k] = an[k];
-                double v0 = gn, v1 = 0.0;
-                const int tn = ts > 0 ? ts - 1 : 0;  // read ahead (clamped: no branch in the chain)
-#pragma unroll
-                for (int k = 0; k < NX; ++k) an[k] = lds[V_ACL + tn * NX * NX + k * NX + lane];
-                gn = lds[V_G + tn * NX + lane];
+                for (int k = 0; k < NX; ++k) an[k] = wb.ld(va + k * NX * WAVE * 8, tc * 8);
+                gn = lds[V_G + tc * NX + lane];
+            };
+            auto chain = [&](double p, const double* ac, double g) __attribute__((always_inline)) -> double {
+                double v0 = g, v1 = 0.0;
 #pragma unroll
                 for (int k = 0; k < NX; ++k) {
                     const double pkv = readlane_d(p, k);
                     if (k & 1) v1 = fma(ac[k], pkv, v1); else v0 = fma(ac[k], pkv, v0);
                 }
-                p = v0 + v1;
+                return v0 + v1;
+            };
+            double p = lds[V_G + (K - 1) * NX + lane];
+            lds[V_CH + (K - 1) * NX + lane] = p;
+            double a0[NX], a1[NX], g0, g1;
+            ldA(K - 2, a0, g0);
+            ldA(K - 3, a1, g1);
+            int ts = K - 2;
+            while (ts >= 0) {
+                p = chain(p, a0, g0);
                 lds[V_CH + ts * NX + lane] = p;
+                ldA(ts - 2, a0, g0);
+                if (--ts < 0) break;
+                p = chain(p, a1, g1);
+                lds[V_CH + ts * NX + lane] = p;
+                ldA(ts - 2, a1, g1);
+                --ts;
             }
         }
         wsync();
@@ -711,6 +739,12 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
         for (int j = 0; j < NU; ++j) k0[j] = 0.0;
         if (act) {
+            double uu[NX], Bt[NX * NU], Ld[NU * NU], W2[NU * NX];
+            ldn(uu, C::C_U, NX);
+            ldn(Bt, C::C_BT, NX * NU);
+            ldn(Ld, C::C_LD, NU * NU);
+            ldn(W2, C::C_W2, NU * NX);
+            hold(uu, NX); hold(Bt, NX * NU); hold(Ld, NU * NU); hold(W2, NU * NX);
 #pragma unroll
             for (int i = 0; i < NX; ++i) pv[i] = lds[V_CH + t * NX + i];
             double rh[NU];
@@ -719,14 +753,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             if (t < K - 1) {
 #pragma unroll
                 for (int i = 0; i < NX; ++i) {
-                    const double h = cld(C::C_U + i) + lds[V_CH + (t + 1) * NX + i];
+                    const double h = uu[i] + lds[V_CH + (t + 1) * NX + i];
 #pragma unroll
-                    for (int j = 0; j < NU; ++j) rh[j] = fma(cld(C::C_BT + i * NU + j), h, rh[j]);
+                    for (int j = 0; j < NU; ++j) rh[j] = fma(Bt[i * NU + j], h, rh[j]);
                 }
             }
-            double Ld[NU * NU];
-#pragma unroll
-            for (int e = 0; e < NU * NU; ++e) Ld[e] = cld(C::C_LD + e);
 #pragma unroll
             for (int i = 0; i < NU; ++i) {
                 double v = rh[i];
@@ -748,7 +779,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
             for (int i = 0; i < NU; ++i)
 #pragma unroll
-                for (int j = 0; j < NX; ++j) xa[j] = fma(cld(C::C_W2 + i * NX + j), k0[i], xa[j]);
+                for (int j = 0; j < NX; ++j) xa[j] = fma(W2[i * NX + j], k0[i], xa[j]);
         }
         // ---- terminal multiplier mu = M^-1 (r2f - xacc - xe - Pi_0' xi0)   (every lane)
         double mu[NX];
@@ -791,20 +822,27 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
         for (int j = 0; j < NU; ++j) v0[j] = k0[j];
         if (act) {
+            double kap[NU * NX], Pi[NX * NX], Bt[NX * NU], ev[NX];
+            ldn(kap, C::C_KAP, NU * NX);
+            ldn(Pi, C::C_PI, NX * NX);
+            ldn(Bt, C::C_BT, NX * NU);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) ev[i] = wb.ld(vpk, PKB + (C::P_E + i) * 8);
+            hold(kap, NU * NX); hold(Pi, NX * NX); hold(Bt, NX * NU); hold(ev, NX);
 #pragma unroll
             for (int i = 0; i < NU; ++i)
 #pragma unroll
-                for (int j = 0; j < NX; ++j) v0[i] = fma(cld(C::C_KAP + i * NX + j), mu[j], v0[i]);
+                for (int j = 0; j < NX; ++j) v0[i] = fma(kap[i * NX + j], mu[j], v0[i]);
 #pragma unroll
             for (int i = 0; i < NX; ++i)
 #pragma unroll
-                for (int j = 0; j < NX; ++j) piv[i] = fma(cld(C::C_PI + i * NX + j), mu[j], piv[i]);
+                for (int j = 0; j < NX; ++j) piv[i] = fma(Pi[i * NX + j], mu[j], piv[i]);
             if (t < K - 1) {
 #pragma unroll
                 for (int i = 0; i < NX; ++i) {
-                    double f = wb.ld(vpk, PKB + (C::P_E + i) * 8);
+                    double f = ev[i];
 #pragma unroll
-                    for (int j = 0; j < NU; ++j) f = fma(cld(C::C_BT + i * NU + j), v0[j], f);
+                    for (int j = 0; j < NU; ++j) f = fma(Bt[i * NU + j], v0[j], f);
                     lds[V_G + t * NX + i] = f;
                 }
             }
@@ -813,32 +851,38 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         stamp(7);
         // ---- forward chain xi_{t+1} = Acl_t xi_t + f_t
         if (lane < NX) {
-            double x = lds[V_XI0 + lane];
-            lds[V_CH + lane] = x;
-            double an[NX], fn = 0.0;
+            // lane i needs row i of Acl_t: ws columns C_ACL + i*NX + k
+            const int va = (C::C_ACL + lane * NX) * WAVE * 8;
+            auto ldA = [&](int ts, double* an, double& fn) __attribute__((always_inline)) {
+                const int tc = ts < K - 1 ? ts : K - 2;
 #pragma unroll
-            for (int k = 0; k < NX; ++k) an[k] = 0.0;
-            if (K >= 2) {
-#pragma unroll
-                for (int k = 0; k < NX; ++k) an[k] = lds[V_ACL + lane * NX + k];
-                fn = lds[V_G + lane];
-            }
-            for (int ts = 0; ts < K - 1; ++ts) {
-                double ac[NX];
-#pragma unroll
-                for (int k = 0; k < NX; ++k) ac[k] = an[k];
-                double w0 = fn, w1 = 0.0;
-                const int tn = ts + 1 < K - 1 ? ts + 1 : ts;
-#pragma unroll
-                for (int k = 0; k < NX; ++k) an[k] = lds[V_ACL + tn * NX * NX + lane * NX + k];
-                fn = lds[V_G + tn * NX + lane];
+                for (int k = 0; k < NX; ++k) an[k] = wb.ld(va + k * WAVE * 8, tc * 8);
+                fn = lds[V_G + tc * NX + lane];
+            };
+            auto chain = [&](double x, const double* ac, double f) __attribute__((always_inline)) -> double {
+                double w0 = f, w1 = 0.0;
 #pragma unroll
                 for (int k = 0; k < NX; ++k) {
                     const double xk = readlane_d(x, k);
                     if (k & 1) w1 = fma(ac[k], xk, w1); else w0 = fma(ac[k], xk, w0);
                 }
-                x = w0 + w1;
+                return w0 + w1;
+            };
+            double x = lds[V_XI0 + lane];
+            lds[V_CH + lane] = x;
+            double a0[NX], a1[NX], f0, f1;
+            ldA(0, a0, f0);
+            ldA(1, a1, f1);
+            int ts = 0;
+            while (ts < K - 1) {
+                x = chain(x, a0, f0);
                 lds[V_CH + (ts + 1) * NX + lane] = x;
+                ldA(ts + 2, a0, f0);
+                if (++ts >= K - 1) break;
+                x = chain(x, a1, f1);
+                lds[V_CH + (ts + 1) * NX + lane] = x;
+                ldA(ts + 2, a1, f1);
+                ++ts;
             }
         }
         wsync();
@@ -851,8 +895,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
         for (int i = 0; i < NZ; ++i) dzo[i] = 0.0;
         if (act) {
-            double xi[NX], Cp[NX * NU];
+            double xi[NX], Cp[NX * NU], Kt[NU * NX], P[NX * NX];
+            ldn(Kt, C::C_K, NU * NX);
+            ldn(P, C::C_P, NX * NX);
             load_cp(Cp);
+            hold(Kt, NU * NX); hold(P, NX * NX);
 #pragma unroll
             for (int i = 0; i < NX; ++i) xi[i] = lds[V_CH + t * NX + i];
             double du[NU];
@@ -860,7 +907,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             for (int j = 0; j < NU; ++j) {
                 double v = v0[j];
 #pragma unroll
-                for (int k = 0; k < NX; ++k) v = fma(cld(C::C_K + j * NX + k), xi[k], v);
+                for (int k = 0; k < NX; ++k) v = fma(Kt[j * NX + k], xi[k], v);
                 du[j] = fixed_u ? 0.0 : v;
             }
 #pragma unroll
@@ -871,7 +918,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 dzo[i] = dx;
                 double y = pv[i] + piv[i];
 #pragma unroll
-                for (int k = 0; k < NX; ++k) y = fma(cld(C::C_P + i * NX + k), xi[k], y);
+                for (int k = 0; k < NX; ++k) y = fma(P[i * NX + k], xi[k], y);
                 ym[i] = -y;
             }
 #pragma unroll
@@ -890,16 +937,16 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     // ------------------------------------------------------------------ node state (workspace)
     // Phase-local register copies: every node phase loads what it uses as one batch and stores
     // what it changes, so no node-sized state is live across the sweeps.
-    double z[NZ], y[NX], s[NR], l[NR], sq[NQ], lq[NQ], av[NGA], ub[NU], sg[NSA][3], sb[NSA];
+    double z[NZ], y[NX], sq[NQ], lq[NQ], av[NGA], ub[NU], sg[NSA][3], sb[NSA];
+    // row slacks s_r and duals lambda_r of this node: LDS [r][lane]
+    auto s_ = [&](int r) __attribute__((always_inline)) -> double& { return lds[V_S + r * WAVE + lane]; };
+    auto l_ = [&](int r) __attribute__((always_inline)) -> double& { return lds[V_L + r * WAVE + lane]; };
     int bidx[NBA];
-    auto load_state = [&]() __attribute__((always_inline)) {
-        fresh();
+    auto issue_state = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < NZ; ++i) z[i] = cld(C::C_Z + i);
 #pragma unroll
         for (int i = 0; i < NX; ++i) y[i] = cld(C::C_Y + i);
-#pragma unroll
-        for (int r = 0; r < NR; ++r) { s[r] = cld(C::C_S + r); l[r] = cld(C::C_L + r); }
 #pragma unroll
         for (int j = 0; j < NQ; ++j) { sq[j] = cld(C::C_SQ + j); lq[j] = cld(C::C_LQ + j); }
 #pragma unroll
@@ -912,16 +959,24 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             for (int i = 0; i < 3; ++i) sg[q][i] = cld(C::C_SOFT + q * 4 + i);
             sb[q] = cld(C::C_SOFT + q * 4 + 3);
         }
+    };
+    auto hold_state = [&]() __attribute__((always_inline)) {
+        hold(z, NZ); hold(y, NX); hold(sq, NQ); hold(lq, NQ); hold(av, NGA); hold(ub, NU);
+#pragma unroll
+        for (int q = 0; q < NS; ++q) { hold(sg[q], 3); hold(&sb[q], 1); }
 #pragma unroll
         for (int b = 0; b < NB; ++b) bidx[b] = qp_opaque(T.box_idx[b]);
+    };
+    auto load_state = [&]() __attribute__((always_inline)) {
+        fresh();
+        issue_state();
+        hold_state();
     };
     auto store_state = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < NZ; ++i) cst(C::C_Z + i, z[i]);
 #pragma unroll
         for (int i = 0; i < NX; ++i) cst(C::C_Y + i, y[i]);
-#pragma unroll
-        for (int r = 0; r < NR; ++r) { cst(C::C_S + r, s[r]); cst(C::C_L + r, l[r]); }
 #pragma unroll
         for (int j = 0; j < NQ; ++j) { cst(C::C_SQ + j, sq[j]); cst(C::C_LQ + j, lq[j]); }
 #pragma unroll
@@ -1009,7 +1064,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         for (int g = 0; g < NGA; ++g) { Haa[g] = 0.0; Hpa[g][0] = Hpa[g][1] = Hpa[g][2] = 0.0; }
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
-            const double Dr = row_on(r) ? (unit ? 1.0 : l[r] / s[r]) : 0.0;
+            const double Dr = row_on(r) ? (unit ? 1.0 : l_(r) / s_(r)) : 0.0;
             if (r < C::R_BOX) {
 #pragma unroll
                 for (int i = 0; i < NU; ++i)
@@ -1083,18 +1138,20 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     // eliminate the group part of a Newton rhs (stores it for recover_aux): r1_p -= Hpa/Haa r1a;
     // returns the (xi, u) linear terms q, r of the node
     auto reduce_rhs = [&](double* r1, const double* r1a, double* q, double* r) __attribute__((always_inline)) {
+        double grp[NGA * 4], Cp[NX * NU];
+        ldn(grp, C::C_GRP, NG * 4);
+        load_cp(Cp);
+        hold(grp, NG * 4);
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
             cst(C::C_R1A + g, r1a[g]);
 #pragma unroll
-            for (int i = 0; i < 3; ++i) r1[i] -= cld(C::C_GRP + g * 4 + i) * r1a[g];
+            for (int i = 0; i < 3; ++i) r1[i] -= grp[g * 4 + i] * r1a[g];
         }
         if (fixed_u) {
 #pragma unroll
             for (int j = 0; j < NU; ++j) r1[NX + j] = 0.0;
         }
-        double Cp[NX * NU];
-        load_cp(Cp);
 #pragma unroll
         for (int i = 0; i < NX; ++i) q[i] = -r1[i];
 #pragma unroll
@@ -1107,13 +1164,18 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     };
     // group directions: da_g = (r1a_g - Hpa_g' dp) / Haa_g
     auto recover_aux = [&](const double* dzl, double* da) __attribute__((always_inline)) {
+        double grp[NGA * 4], r1a[NGA];
+        ldn(grp, C::C_GRP, NG * 4);
+        ldn(r1a, C::C_R1A, NG);
+        hold(grp, NG * 4);
+        hold(r1a, NG);
 #pragma unroll
         for (int g = 0; g < NGA; ++g) da[g] = 0.0;
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
-            double v = cld(C::C_R1A + g) * cld(C::C_GRP + g * 4 + 3);
+            double v = r1a[g] * grp[g * 4 + 3];
 #pragma unroll
-            for (int i = 0; i < 3; ++i) v -= cld(C::C_GRP + g * 4 + i) * dzl[i];
+            for (int i = 0; i < 3; ++i) v -= grp[g * 4 + i] * dzl[i];
             da[g] = grp_on(g) ? v : 0.0;
         }
     };
@@ -1129,18 +1191,19 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
     };
     // dynamics residual rp_t = x_{t+1} - A x_t - B u_t - C u_{t+1} - S sigma - z  (lane t < K-1)
-    auto dyn_residual = [&](const double* zz, double* rp) __attribute__((always_inline)) {
+    // (dt: this node's transposed disc row, batch-loaded by the caller)
+    auto dyn_residual = [&](const double* zz, const double* dt, double* rp) __attribute__((always_inline)) {
         double zn[NZ];
 #pragma unroll
         for (int i = 0; i < NZ; ++i) zn[i] = __shfl_down(zz[i], 1, WAVE);
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
-            double v = zn[i] - fma(cld(C::C_DT + NX * NX + 2 * NX * NU + i), sig, cld(C::C_DT + NX * NX + 2 * NX * NU + NX + i));
+            double v = zn[i] - fma(dt[NX * NX + 2 * NX * NU + i], sig, dt[NX * NX + 2 * NX * NU + NX + i]);
 #pragma unroll
-            for (int k = 0; k < NX; ++k) v -= cld(C::C_DT + k * NX + i) * zz[k];
+            for (int k = 0; k < NX; ++k) v -= dt[k * NX + i] * zz[k];
 #pragma unroll
             for (int j = 0; j < NU; ++j)
-                v -= cld(C::C_DT + NX * NX + j * NX + i) * zz[NX + j] + cld(C::C_DT + NX * NX + NX * NU + j * NX + i) * zn[NX + j];
+                v -= dt[NX * NX + j * NX + i] * zz[NX + j] + dt[NX * NX + NX * NU + j * NX + i] * zn[NX + j];
             rp[i] = (t < K - 1) ? v : 0.0;
         }
     };
@@ -1177,11 +1240,16 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     };
     // SOC scaling of the iteration (columns C_WV..C_RHO)
     double wv[NQ], eta = 1.0, ltq[NQ], rcq[NQ];
-    auto load_soc = [&]() __attribute__((always_inline)) {
-        fresh();
+    auto issue_soc = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < NQ; ++j) { wv[j] = cld(C::C_WV + j); ltq[j] = cld(C::C_LTQ + j); rcq[j] = cld(C::C_RCQ + j); }
         eta = cld(C::C_ETA);
+    };
+    auto hold_soc = [&]() __attribute__((always_inline)) { hold(wv, NQ); hold(ltq, NQ); hold(rcq, NQ); hold(&eta, 1); };
+    auto load_soc = [&]() __attribute__((always_inline)) {
+        fresh();
+        issue_soc();
+        hold_soc();
     };
 
     int status = SCVX_STATUS_MAX_ITER;
@@ -1191,13 +1259,18 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     // minimiser of 1/2 z'Pz + q'z + 1/2 ||Gz - h||^2 s.t. Az = b from z_ref (aux = 0), unit scaling
     // (CVXOPT coneqp initialisation; oracle/qp_dense.py does the same on the dense form)
     {
-        load_state();
+        fresh();
+        double dt[C::DSTR];
+        issue_state();
+        ldn(dt, C::C_DT, C::DSTR);
+        hold_state();
+        hold(dt, C::DSTR);
 #pragma unroll
-        for (int r = 0; r < NR; ++r) { s[r] = 1.0; l[r] = 0.0; }
+        for (int r = 0; r < NR; ++r) { s_(r) = 1.0; l_(r) = 0.0; }
         double Wu[NU * NU], rp[NX];
 #pragma unroll
         for (int e = 0; e < NU * NU; ++e) Wu[e] = (e / NU == e % NU) ? 1.0 : 0.0;
-        dyn_residual(z, rp);
+        dyn_residual(z, dt, rp);
         assemble(true, Wu, rp);
         double r1[NZ], r1a[NGA];
 #pragma unroll
@@ -1231,8 +1304,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             double gz, h;
             row_eval(r, z, av, gz, h);
             const bool on = row_on(r);
-            s[r] = on ? h - gz : 1.0;
-            l[r] = on ? gz - h : 0.0;
+            s_(r) = on ? h - gz : 1.0;
+            l_(r) = on ? gz - h : 0.0;
             if (on) { smin = fmin(smin, h - gz); lmin = fmin(lmin, gz - h); }
         }
 #pragma unroll
@@ -1249,7 +1322,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         const double shs = fmax(0.0, 1.0 - smin), shl = fmax(0.0, 1.0 - lmin);
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
-            if (row_on(r)) { s[r] += shs; l[r] += shl; }
+            if (row_on(r)) { s_(r) += shs; l_(r) += shl; }
         }
         if (soc) { sq[0] += shs; lq[0] += shl; }
         store_state();
@@ -1268,9 +1341,15 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     const long long cyc_all0 = __builtin_amdgcn_s_memtime();
     stamp(-1);
     for (it = 0; it < T.max_iter && status != SCVX_STATUS_NUMERICAL; ++it) {
-        load_state();
+        fresh();
+        double dt[C::DSTR], Cpr[NX * NU];
+        issue_state();
+        ldn(dt, C::C_DT, C::DSTR);
+        load_cp(Cpr);
+        hold_state();
+        hold(dt, C::DSTR);
         double rp[NX];
-        dyn_residual(z, rp);
+        dyn_residual(z, dt, rp);
         // dual residual rd = Pz + q + A'y + G'lam (z and group parts)
         double rd[NZ], rda[NGA];
         double pres = 0.0, dres = 0.0, gap = 0.0, hsc = 1.0, pobj = 0.0;
@@ -1295,11 +1374,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             double gz, h;
             row_eval(r, z, av, gz, h);
             if (row_on(r)) {
-                const double rcr = gz + s[r] - h;
+                const double rcr = gz + s_(r) - h;
                 pres = fmax(pres, fabs(rcr));
                 hsc = fmax(hsc, fabs(h));
-                gap += s[r] * l[r];
-                row_accT(r, l[r], rd, rda);
+                gap += s_(r) * l_(r);
+                row_accT(r, l_(r), rd, rda);
             }
         }
         if (soc) {
@@ -1328,24 +1407,22 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                     for (int i = 0; i < NX; ++i) rd[i] += lds[V_YF + i];
                 }
                 if (t >= 1) {
-                    double Cp[NX * NU];
-                    load_cp(Cp);
 #pragma unroll
                     for (int i = 0; i < NX; ++i) rd[i] += ym[i];
 #pragma unroll
                     for (int j = 0; j < NU; ++j)
 #pragma unroll
-                        for (int i = 0; i < NX; ++i) rd[NX + j] -= Cp[j * NX + i] * ym[i];
+                        for (int i = 0; i < NX; ++i) rd[NX + j] -= Cpr[j * NX + i] * ym[i];
                 }
                 if (t < K - 1) {
 #pragma unroll
                     for (int k = 0; k < NX; ++k)
 #pragma unroll
-                        for (int i = 0; i < NX; ++i) rd[k] -= cld(C::C_DT + k * NX + i) * y[i];
+                        for (int i = 0; i < NX; ++i) rd[k] -= dt[k * NX + i] * y[i];
 #pragma unroll
                     for (int j = 0; j < NU; ++j)
 #pragma unroll
-                        for (int i = 0; i < NX; ++i) rd[NX + j] -= cld(C::C_DT + NX * NX + j * NX + i) * y[i];
+                        for (int i = 0; i < NX; ++i) rd[NX + j] -= dt[NX * NX + j * NX + i] * y[i];
                 }
                 if (fixed_u) {
 #pragma unroll
@@ -1427,18 +1504,25 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         double sgmu = 0.0;
         double dz[NZ], dy[NX], da[NGA], dsq[NQ], dlq[NQ], cpv[NR];
         auto rco_of = [&](int r, bool corr) __attribute__((always_inline)) -> double {
-            const double v = -s[r] * l[r];
+            const double v = -s_(r) * l_(r);
             return corr ? v - cpv[r] + sgmu : v;
         };
         // Newton direction for the complementarity rhs (rows: rco_of, SOC: rcq2); directions out
         auto newton = [&](bool corr, const double* rcq2) __attribute__((always_inline)) {
-            load_state();
-            load_soc();
             double r1[NZ], r1a[NGA], rho[NQ];
+            fresh();
+            issue_state();
+            issue_soc();
+            ldn(r1, C::C_RD, NZ);
+            if (corr) ldn(cpv, C::C_CP, NR);
+            hold_state();
+            hold_soc();
+            hold(r1, NZ);
+            if (corr) hold(cpv, NR);
 #pragma unroll
-            for (int i = 0; i < NZ; ++i) r1[i] = act ? -cld(C::C_RD + i) : 0.0;
+            for (int i = 0; i < NZ; ++i) r1[i] = act ? -r1[i] : 0.0;
 #pragma unroll
-            for (int r = 0; r < NR; ++r) cpv[r] = corr ? cld(C::C_CP + r) : 0.0;
+            for (int r = 0; r < NR; ++r) cpv[r] = corr ? cpv[r] : 0.0;
 #pragma unroll
             for (int g = 0; g < NGA; ++g) r1a[g] = -gweight(g);
 #pragma unroll
@@ -1446,9 +1530,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 if (row_on(r)) {
                     double gz, h;
                     row_eval(r, z, av, gz, h);
-                    const double rcr = gz + s[r] - h;
-                    row_accA(r, -l[r], r1a);  // -rd, group part: -(w_g - sum lambda)
-                    row_accT(r, -(rco_of(r, corr) + l[r] * rcr) / s[r], r1, r1a);
+                    const double rcr = gz + s_(r) - h;
+                    row_accA(r, -l_(r), r1a);  // -rd, group part: -(w_g - sum lambda)
+                    row_accT(r, -(rco_of(r, corr) + l_(r) * rcr) / s_(r), r1, r1a);
                 }
             }
 #pragma unroll
@@ -1476,8 +1560,15 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             stamp(2);
             solve(q, rr, dz, dy);
             // post-solve: group and SOC directions (state reloaded: nothing crossed the sweeps)
-            load_state();
-            load_soc();
+            fresh();
+            issue_state();
+            issue_soc();
+            if (corr) ldn(cpv, C::C_CP, NR);
+            ldn(rho, C::C_RHO, NQ);
+            hold_state();
+            hold_soc();
+            if (corr) hold(cpv, NR);
+            hold(rho, NQ);
             recover_aux(dz, da);
             if (soc) {
                 double v2[NQ], w2[NQ];
@@ -1487,23 +1578,23 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 for (int j = 1; j < NQ; ++j) { dsq[j] = -rcq[j] + dz[NX + j - 1]; v2[j] = rcq[j] - dz[NX + j - 1]; }
                 w_apply(wv, eta, true, v2, w2);
 #pragma unroll
-                for (int j = 0; j < NQ; ++j) w2[j] += cld(C::C_RHO + j);
+                for (int j = 0; j < NQ; ++j) w2[j] += rho[j];
                 w_apply(wv, eta, true, w2, dlq);
             } else {
 #pragma unroll
                 for (int j = 0; j < NQ; ++j) { dsq[j] = 0.0; dlq[j] = 0.0; }
             }
 #pragma unroll
-            for (int r = 0; r < NR; ++r) cpv[r] = corr ? cld(C::C_CP + r) : 0.0;
+            for (int r = 0; r < NR; ++r) cpv[r] = corr ? cpv[r] : 0.0;
         };
         // row directions ds = -rc - G d, dl = (rco + l (rc + G d)) / s
         auto row_dir = [&](int r, bool corr, double& dsr, double& dlr) __attribute__((always_inline)) {
             double gz, h, gd, h2;
             row_eval(r, z, av, gz, h);
             row_eval(r, dz, da, gd, h2);
-            const double rcr = gz + s[r] - h;
+            const double rcr = gz + s_(r) - h;
             dsr = -rcr - gd;
-            dlr = (rco_of(r, corr) + l[r] * (rcr + gd)) / s[r];
+            dlr = (rco_of(r, corr) + l_(r) * (rcr + gd)) / s_(r);
         };
         auto max_step = [&](bool corr) __attribute__((always_inline)) {
             double am = 1e300;
@@ -1512,8 +1603,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 if (row_on(r)) {
                     double dsr, dlr;
                     row_dir(r, corr, dsr, dlr);
-                    if (dsr < 0) am = fmin(am, -s[r] / dsr);
-                    if (dlr < 0) am = fmin(am, -l[r] / dlr);
+                    if (dsr < 0) am = fmin(am, -s_(r) / dsr);
+                    if (dlr < 0) am = fmin(am, -l_(r) / dlr);
                 }
             }
             if (soc) { am = fmin(am, soc_step(sq, dsq)); am = fmin(am, soc_step(lq, dlq)); }
@@ -1547,7 +1638,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             if (row_on(r)) {
                 double dsr, dlr;
                 row_dir(r, false, dsr, dlr);
-                gap_a += (s[r] + aa * dsr) * (l[r] + aa * dlr);
+                gap_a += (s_(r) + aa * dsr) * (l_(r) + aa * dlr);
                 cst(C::C_CP + r, dsr * dlr);
             }
         }
@@ -1597,8 +1688,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             if (row_on(r)) {
                 double dsr, dlr;
                 row_dir(r, true, dsr, dlr);
-                s[r] += al * dsr;
-                l[r] += al * dlr;
+                s_(r) += al * dsr;
+                l_(r) += al * dlr;
             }
         }
         if (act) {

@@ -7,7 +7,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libscvx_hip.so")
+LIB_PATH = os.environ.get("SCVX_HIP_LIB") or os.path.join(HERE, "libscvx_hip.so")  # override: diagnostics builds
 
 SCVX_MAX_BOX, SCVX_MAX_OBS = 4, 16
 MODEL_IDS = {"di": 0, "unicycle": 1, "si": 2, "quad": 3}
