@@ -714,19 +714,25 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             };
             double p = lds[V_G + (K - 1) * NX + lane];
             lds[V_CH + (K - 1) * NX + lane] = p;
-            double a0[NX], a1[NX], g0, g1;
-            ldA(K - 2, a0, g0);
-            ldA(K - 3, a1, g1);
+            // four register buffers: operands loaded four stages ahead
+            double ab[4][NX], gb[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) ldA(K - 2 - b, ab[b], gb[b]);
             int ts = K - 2;
-            while (ts >= 0) {
-                p = chain(p, a0, g0);
+            auto step = [&](double* a, double& g) __attribute__((always_inline)) {
+                p = chain(p, a, g);
                 lds[V_CH + ts * NX + lane] = p;
-                ldA(ts - 2, a0, g0);
-                if (--ts < 0) break;
-                p = chain(p, a1, g1);
-                lds[V_CH + ts * NX + lane] = p;
-                ldA(ts - 2, a1, g1);
+                ldA(ts - 4, a, g);
                 --ts;
+            };
+            while (ts >= 0) {
+                step(ab[0], gb[0]);
+                if (ts < 0) break;
+                step(ab[1], gb[1]);
+                if (ts < 0) break;
+                step(ab[2], gb[2]);
+                if (ts < 0) break;
+                step(ab[3], gb[3]);
             }
         }
         wsync();
@@ -870,19 +876,24 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             };
             double x = lds[V_XI0 + lane];
             lds[V_CH + lane] = x;
-            double a0[NX], a1[NX], f0, f1;
-            ldA(0, a0, f0);
-            ldA(1, a1, f1);
+            double ab[4][NX], fb[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) ldA(b, ab[b], fb[b]);
             int ts = 0;
-            while (ts < K - 1) {
-                x = chain(x, a0, f0);
+            auto step = [&](double* a, double& f) __attribute__((always_inline)) {
+                x = chain(x, a, f);
                 lds[V_CH + (ts + 1) * NX + lane] = x;
-                ldA(ts + 2, a0, f0);
-                if (++ts >= K - 1) break;
-                x = chain(x, a1, f1);
-                lds[V_CH + (ts + 1) * NX + lane] = x;
-                ldA(ts + 2, a1, f1);
+                ldA(ts + 4, a, f);
                 ++ts;
+            };
+            while (ts < K - 1) {
+                step(ab[0], fb[0]);
+                if (ts >= K - 1) break;
+                step(ab[1], fb[1]);
+                if (ts >= K - 1) break;
+                step(ab[2], fb[2]);
+                if (ts >= K - 1) break;
+                step(ab[3], fb[3]);
             }
         }
         wsync();
