@@ -75,13 +75,14 @@ constexpr int qp_pkt(int nx, int nu) { return 2 * nx * nx + 4 * nx * nu + nu * n
 constexpr int qp_even(int x) { return (x + 1) & ~1; }
 // workspace columns (doubles x 64) of a capacity class
 constexpr int qp_ncol(int nx, int nu, int nb, int ns, int ng) {
-    // disc^T | K kappa LD W2 P Pi u | Bt | soft rows | groups | rd | r1a | cP | ub | node state | SOC
-    return qp_dstr(nx, nu) + 3 * nu * nx + nu * nu + 2 * nx * nx + nx + nx * nu + 4 * ns + 4 * ng + (nx + nu) + ng +
-           ((1 << nu) + 2 * nb + ns + ng) + nu +
-           ((nx + nu) + nx + 2 * (nu + 1) + ng) + (3 * (nu + 1) + 1 + (nu + 1)) + nx * nx;
+    // disc^T | Bt | soft rows | groups | rd | r1a | cP | ub | node state | SOC
+    return qp_dstr(nx, nu) + nx * nu + 4 * ns + 4 * ng + (nx + nu) + ng + ((1 << nu) + 2 * nb + ns + ng) + nu +
+           ((nx + nu) + nx + 2 * (nu + 1) + ng) + (3 * (nu + 1) + 1 + (nu + 1));
 }
+// factor outputs per stage (stage-major block): K, kappa, LD, W2, P, Pi, u, Acl
+constexpr int qp_fbs(int nx, int nu) { return 3 * nu * nx + nu * nu + 3 * nx * nx + nx; }
 constexpr long long qp_ws_doubles(int nx, int nu, int nb, int ns, int ng) {
-    return (long long)qp_ncol(nx, nu, nb, ns, ng) * 64 + 64LL * qp_pkt(nx, nu);
+    return (long long)qp_ncol(nx, nu, nb, ns, ng) * 64 + 64LL * qp_pkt(nx, nu) + 64LL * qp_fbs(nx, nu);
 }
 
 template <int NX_, int NU_, int NB_, int NO_, int NC_>
@@ -100,16 +101,21 @@ struct QPCfg {
                          P_A = P_E + NX, P_BT = P_A + NX * NX, P_BTR = P_BT + NX * NU, P_C = P_BTR + NX * NU,
                          PKT = P_C + NX * NU;
     static_assert(PKT == qp_pkt(NX, NU), "packet size");
+    // factor outputs: stage-major blocks [t][FBS] (coalesced stores from the element-parallel
+    // factor; each lane-parallel pass reads its own stage's block)
+    static constexpr int B_K = 0;                  // K      NU x NX
+    static constexpr int B_KAP = B_K + NU * NX;    // kappa  NU x NX
+    static constexpr int B_LD = B_KAP + NU * NX;   // LDL' of Rhat: L[i][j] (i > j), 1/d_i on the diagonal
+    static constexpr int B_W2 = B_LD + NU * NU;    // W2 = Bt' Pi_{t+1}  NU x NX
+    static constexpr int B_P = B_W2 + NU * NX;     // P_t
+    static constexpr int B_PI = B_P + NX * NX;     // Pi_t
+    static constexpr int B_U = B_PI + NX * NX;     // P_{t+1} e_t
+    static constexpr int B_ACL = B_U + NX;         // Acl_t = A_t + Bt_t K_t (row-major)
+    static constexpr int FBS = B_ACL + NX * NX;
+    static_assert(FBS == qp_fbs(NX, NU), "factor block");
     // stage-minor workspace columns
     static constexpr int C_DT = 0;                 // disc, transposed: A (col-major) | B | C | S | z
-    static constexpr int C_K = C_DT + DSTR;        // K      NU x NX
-    static constexpr int C_KAP = C_K + NU * NX;    // kappa  NU x NX
-    static constexpr int C_LD = C_KAP + NU * NX;   // LDL' of Rhat: L[i][j] (i > j), 1/d_i on the diagonal
-    static constexpr int C_W2 = C_LD + NU * NU;    // W2 = Bt' Pi_{t+1}  NU x NX
-    static constexpr int C_P = C_W2 + NU * NX;     // P_t
-    static constexpr int C_PI = C_P + NX * NX;     // Pi_t
-    static constexpr int C_U = C_PI + NX * NX;     // P_{t+1} e_t
-    static constexpr int C_BT = C_U + NX;          // Bt_t (row-major)
+    static constexpr int C_BT = C_DT + DSTR;       // Bt_t (row-major)
     static constexpr int C_SOFT = C_BT + NX * NU;  // soft rows (g0, g1, g2, b)
     static constexpr int C_GRP = C_SOFT + 4 * NS;  // per group: Hpa/Haa (3), 1/Haa
     static constexpr int C_RD = C_GRP + 4 * NG;    // dual residual (x, u part)
@@ -122,8 +128,7 @@ struct QPCfg {
     // SOC scaling of the current iteration: w (NQ), eta, W lam (NQ), rc (NQ), rho (NQ)
     static constexpr int C_WV = C_AV + NG, C_ETA = C_WV + NQ, C_LTQ = C_ETA + 1, C_RCQ = C_LTQ + NQ,
                          C_RHO = C_RCQ + NQ;
-    static constexpr int C_ACL = C_RHO + NQ;       // Acl_t = A_t + Bt_t K_t (row-major)
-    static constexpr int NCOL = C_ACL + NX * NX;
+    static constexpr int NCOL = C_RHO + NQ;
     static_assert(NCOL == qp_ncol(NX, NU, NB, NS, NG), "column count");
     // LDS (doubles, compile-time offsets except the K-sized blocks at the end):
     // factor: 2-slot packet ring, P', Pi' (col-major), T1, T2 (col-major), W1, W2 (col-major), Qh,
@@ -193,7 +198,7 @@ __device__ __forceinline__ double qp_dot(const double* lds, int L, int R, int so
 // pressure) nor serialised between the repetitions.
 template <int KK, int NREP>
 __device__ __forceinline__ void qp_phase(double* lds, const int (&d)[NREP][4], int soff, bool last, int acl_off,
-                                         const QPBuf& wb, int ts) {
+                                         const QPBuf& wb, int fbo) {
     int Ld[NREP], Rd[NREP], Od[NREP], Bd[NREP];
 #pragma unroll
     for (int r = 0; r < NREP; ++r) {
@@ -216,7 +221,7 @@ __device__ __forceinline__ void qp_phase(double* lds, const int (&d)[NREP][4], i
             lds[oo] = ((O >> 15) & 1) ? old + val[r] : val[r];
             const int g = (O >> 17) - 1;
 #ifndef QPX_NOGST
-            if (g >= 0) wb.st(g * WAVE * 8, ts * 8, val[r]);
+            if (g >= 0) wb.st(g * 8, fbo, val[r]);
 #endif
         }
     }
@@ -252,7 +257,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     wb.rs = __builtin_amdgcn_make_buffer_rsrc(ws, (short)0, 0x7fffffff, 0x00020000);
     const int vt = t * 8;  // this lane's element of a stage-minor column
     constexpr int PKB = C::NCOL * WAVE * 8;  // byte offset of the packets [t][PKT]
+    constexpr int FBB = PKB + WAVE * PKT * 8;  // byte offset of the factor output blocks [t][FBS]
     const int vpk = t * PKT * 8;
+    const int vfb = t * C::FBS * 8;
     // Loads go through `vcur`, this lane's offset re-derived (opaquely) at the start of every
     // phase: a load in one phase is then never merged with the same load of an earlier phase,
     // which would keep the value live in registers across the sweeps in between.
@@ -266,6 +273,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     auto ldn = [&](double* dst, int c0, int n) __attribute__((always_inline)) {
 #pragma unroll
         for (int e = 0; e < n; ++e) dst[e] = cld(c0 + e);
+    };
+    // n consecutive elements of this lane's factor output block, from block offset b0
+    auto ldb = [&](double* dst, int b0, int n) __attribute__((always_inline)) {
+#pragma unroll
+        for (int e = 0; e < n; ++e) dst[e] = wb.ld(vfb, FBB + (b0 + e) * 8);
     };
     auto hold = [&](double* v, int n) __attribute__((always_inline)) {
 #pragma unroll
@@ -416,10 +428,10 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 } else if ((o -= NX * NX) < NU * NX) {  // W2 = Bt' Pi' -> column-major (C_{K-2}' at the last stage)
                     const int i = o / NX, j = o % NX;
                     L = qp_dpk(C::P_BT + i * NX, 1); R = qp_dpk(C::F_PIP + j * NX, 0);
-                    O = (C::F_W2 + j * NU + i) | ((C::C_W2 + o + 1) << 17);
+                    O = (C::F_W2 + j * NU + i) | ((C::B_W2 + o + 1) << 17);
                     B = (C::P_C + i * NX + j) | (1 << 15) | (2 << 16);
                 } else if ((o -= NU * NX) < NX) {  // u = P' e  (global only)
-                    L = qp_dpk(C::F_PP + o * NX, 0); R = qp_dpk(C::P_E, 1); O = sink | ((C::C_U + o + 1) << 17);
+                    L = qp_dpk(C::F_PP + o * NX, 0); R = qp_dpk(C::P_E, 1); O = sink | ((C::B_U + o + 1) << 17);
                 } else if ((o -= NX) < NX) {  // xe += Pi'' e
                     L = qp_dpk(C::F_PIP + o * NX, 0); R = qp_dpk(C::P_E, 1); O = (V_XE + o) | (1 << 15);
                 }
@@ -449,18 +461,18 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 if (o < NX * NX) {  // P = Qh + Sh' K (symmetric)
                     const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
                     L = qp_dpk(C::F_SH + p * NU, 0); R = qp_dpk(C::F_KK + q * NU, 0);
-                    O = (C::F_PP + o) | ((C::C_P + o + 1) << 17); B = (C::F_QH + p * NX + q) | (1 << 16);
+                    O = (C::F_PP + o) | ((C::B_P + o + 1) << 17); B = (C::F_QH + p * NX + q) | (1 << 16);
                 } else if ((o -= NX * NX) < NX * NX) {  // Pi = W1 + Sh' kappa -> Pi' column-major
                     const int i = o / NX, j = o % NX;
                     L = qp_dpk(C::F_SH + i * NU, 0); R = qp_dpk(C::F_KK + (NX + j) * NU, 0);
-                    O = (C::F_PIP + j * NX + i) | ((C::C_PI + o + 1) << 17); B = (C::F_W1 + o) | (1 << 16);
+                    O = (C::F_PIP + j * NX + i) | ((C::B_PI + o + 1) << 17); B = (C::F_W1 + o) | (1 << 16);
                 } else if ((o -= NX * NX) < NX * NX) {  // M += W2' kappa (symmetric)
                     const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
                     L = qp_dpk(C::F_W2 + p * NU, 0); R = qp_dpk(C::F_KK + (NX + q) * NU, 0); O = (V_M + o) | (1 << 15);
                 } else if ((o -= NX * NX) < NX * NX) {  // Acl = A + Bt K  -> LDS Acl block of the stage
                     const int i = o / NX, j = o % NX;
                     L = qp_dpk(C::P_BTR + i * NU, 1); R = qp_dpk(C::F_KK + j * NU, 0);
-                    O = sink | ((C::C_ACL + o + 1) << 17); B = (C::P_A + j * NX + i) | (1 << 15) | (1 << 16);
+                    O = sink | ((C::B_ACL + o + 1) << 17); B = (C::P_A + j * NX + i) | (1 << 15) | (1 << 16);
                 }
                 d4[rep][0] = L; d4[rep][1] = R; d4[rep][2] = O; d4[rep][3] = B;
             }
@@ -498,15 +510,16 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             const int soff = (ts & 1) * PKT;
             const bool last = ts == K - 1;
             const int acl_off = ts * NX * NX;
+            const int fbo = FBB + ts * C::FBS * 8;  // byte offset of this stage's output block
             if (ts - 3 >= 0 && ts < K - 1) pf_load(ts - 3, nb);  // (stage K-1 issued K-4 before the loop)
             const bool fst = ts >= 20 && ts < 30;
             if (fst) stamp(-1);
             // ---- phase 1: T1 = P'A, T2 = P'Bt, W1 = A'Pi', W2 = Bt'Pi', u = P'e, xe += Pi''e
-            qp_phase<NX, R1>(lds, d1, soff, last, acl_off, wb, ts);
+            qp_phase<NX, R1>(lds, d1, soff, last, acl_off, wb, fbo);
             wsync();
             if (fst) stamp(11);
             // ---- phase 2: Qh = Q + A'T1, Sh = S' + Bt'T1, Rh = R + Bt'T2
-            qp_phase<NX, R2>(lds, d2, soff, last, acl_off, wb, ts);
+            qp_phase<NX, R2>(lds, d2, soff, last, acl_off, wb, fbo);
             wsync();
             if (fst) stamp(12);
             // ---- phase 3: Rh = L D L' in registers (every lane); [K | kappa] = -Rh^-1 [Sh | W2]
@@ -566,13 +579,13 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                         for (int k = i + 1; k < NU; ++k) v -= Lm[k * NU + i] * x[k];
                         x[i] = v;
                     }
-                    const int g = c < NX ? C::C_K + c : C::C_KAP + c - NX;
+                    const int g = c < NX ? C::B_K + c : C::B_KAP + c - NX;
 #pragma unroll
                     for (int i = 0; i < NU; ++i) {
                         const double v = fx ? 0.0 : -x[i];
                         lds[C::F_KK + c * NU + i] = v;
 #ifndef QPX_NOGST
-                        wb.st((g + i * NX) * WAVE * 8, ts * 8, v);
+                        wb.st((g + i * NX) * 8, fbo, v);
 #endif
                     }
                 }
@@ -584,14 +597,14 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                         v = fma(qp_mask(e, lane), (ei > ej) ? Lm[e] : (ei == ej ? dinv[ei] : 0.0), v);
                     }
 #ifndef QPX_NOGST
-                    wb.st((C::C_LD + lane) * WAVE * 8, ts * 8, v);
+                    wb.st((C::B_LD + lane) * 8, fbo, v);
 #endif
                 }
             }
             wsync();
             if (fst) stamp(13);
             // ---- phase 4: P = Qh + Sh'K, Pi = W1 + Sh'kappa, M += W2'kappa, Acl = A + Bt K
-            qp_phase<NU, R4>(lds, d4, soff, last, acl_off, wb, ts);
+            qp_phase<NU, R4>(lds, d4, soff, last, acl_off, wb, fbo);
             if (ts > 0) pf_store(ts - 1, cb);
             wsync();
             if (fst) stamp(14);
@@ -668,9 +681,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         fresh();
         if (act) {
             double g[NX], Kt[NU * NX], u[NX], Ac[NX * NX];
-            ldn(Kt, C::C_K, NU * NX);
-            ldn(u, C::C_U, NX);
-            ldn(Ac, C::C_ACL, NX * NX);
+            ldb(Kt, C::B_K, NU * NX);
+            ldb(u, C::B_U, NX);
+            ldb(Ac, C::B_ACL, NX * NX);
             hold(Kt, NU * NX);
             hold(u, NX);
             hold(Ac, NX * NX);
@@ -694,13 +707,12 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         // ---- backward chain p_t = Acl_t' p_{t+1} + g_t (lane i: element i); p_{t+1} broadcast
         // from lanes 0..NX-1 through readlane, the Acl column / g of the next stage read ahead
         if (lane < NX) {
-            // lane i needs column i of Acl_t: ws columns C_ACL + k*NX + i at stage index ts
-            // (L1-resident after the first touch of each line), loaded two stages ahead
-            const int va = (C::C_ACL + lane) * WAVE * 8;
+            // lane i needs column i of Acl_t (stage block, B_ACL + k*NX + i)
+            const int va = (C::B_ACL + lane) * 8;
             auto ldA = [&](int ts, double* an, double& gn) __attribute__((always_inline)) {
                 const int tc = ts > 0 ? ts : 0;
 #pragma unroll
-                for (int k = 0; k < NX; ++k) an[k] = wb.ld(va + k * NX * WAVE * 8, tc * 8);
+                for (int k = 0; k < NX; ++k) an[k] = wb.ld(va + k * NX * 8, FBB + tc * C::FBS * 8);
                 gn = lds[V_G + tc * NX + lane];
             };
             auto chain = [&](double p, const double* ac, double g) __attribute__((always_inline)) -> double {
@@ -746,10 +758,10 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         for (int j = 0; j < NU; ++j) k0[j] = 0.0;
         if (act) {
             double uu[NX], Bt[NX * NU], Ld[NU * NU], W2[NU * NX];
-            ldn(uu, C::C_U, NX);
+            ldb(uu, C::B_U, NX);
             ldn(Bt, C::C_BT, NX * NU);
-            ldn(Ld, C::C_LD, NU * NU);
-            ldn(W2, C::C_W2, NU * NX);
+            ldb(Ld, C::B_LD, NU * NU);
+            ldb(W2, C::B_W2, NU * NX);
             hold(uu, NX); hold(Bt, NX * NU); hold(Ld, NU * NU); hold(W2, NU * NX);
 #pragma unroll
             for (int i = 0; i < NX; ++i) pv[i] = lds[V_CH + t * NX + i];
@@ -829,8 +841,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         for (int j = 0; j < NU; ++j) v0[j] = k0[j];
         if (act) {
             double kap[NU * NX], Pi[NX * NX], Bt[NX * NU], ev[NX];
-            ldn(kap, C::C_KAP, NU * NX);
-            ldn(Pi, C::C_PI, NX * NX);
+            ldb(kap, C::B_KAP, NU * NX);
+            ldb(Pi, C::B_PI, NX * NX);
             ldn(Bt, C::C_BT, NX * NU);
 #pragma unroll
             for (int i = 0; i < NX; ++i) ev[i] = wb.ld(vpk, PKB + (C::P_E + i) * 8);
@@ -857,12 +869,12 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         stamp(7);
         // ---- forward chain xi_{t+1} = Acl_t xi_t + f_t
         if (lane < NX) {
-            // lane i needs row i of Acl_t: ws columns C_ACL + i*NX + k
-            const int va = (C::C_ACL + lane * NX) * WAVE * 8;
+            // lane i needs row i of Acl_t (stage block, B_ACL + i*NX + k)
+            const int va = (C::B_ACL + lane * NX) * 8;
             auto ldA = [&](int ts, double* an, double& fn) __attribute__((always_inline)) {
                 const int tc = ts < K - 1 ? ts : K - 2;
 #pragma unroll
-                for (int k = 0; k < NX; ++k) an[k] = wb.ld(va + k * WAVE * 8, tc * 8);
+                for (int k = 0; k < NX; ++k) an[k] = wb.ld(va + k * 8, FBB + tc * C::FBS * 8);
                 fn = lds[V_G + tc * NX + lane];
             };
             auto chain = [&](double x, const double* ac, double f) __attribute__((always_inline)) -> double {
@@ -907,8 +919,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         for (int i = 0; i < NZ; ++i) dzo[i] = 0.0;
         if (act) {
             double xi[NX], Cp[NX * NU], Kt[NU * NX], P[NX * NX];
-            ldn(Kt, C::C_K, NU * NX);
-            ldn(P, C::C_P, NX * NX);
+            ldb(Kt, C::B_K, NU * NX);
+            ldb(P, C::B_P, NX * NX);
             load_cp(Cp);
             hold(Kt, NU * NX); hold(P, NX * NX);
 #pragma unroll
