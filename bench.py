@@ -46,6 +46,20 @@ def qp_flops_per_ipm_iter(n, m, K, rows):
     return K * (factor + 2 * solve + node)
 
 
+def committed_traffic(kernel_prefix="scvx::qp_ipm_kernel<scvx::QPCfg<6, 3, 2, 8, 0>"):
+    """HBM-side bytes per launch of the dominant kernel from the newest committed rocprofv3 --pmc
+    summary (profiles/*_pmc_traffic.json, made by tools/pmc_summary.py from separate FETCH_SIZE /
+    WRITE_SIZE passes of this same bench, gfx950 FETCH_SIZE x2 correction applied); None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")))  # round-tagged names
+    for f in reversed(files):
+        d = json.load(open(f))
+        for k, v in d.items():
+            if k.startswith(kernel_prefix):
+                return v["traffic_bytes"], os.path.relpath(f, REPO)
+    return None, None
+
+
 def make_workload(N, seed, device):
     import torch
     from oracle import problems as pb
@@ -143,6 +157,7 @@ def main():
     rows = (1 << 3) + 2 * len(BOX) + 2 * N_OBS
     flops = qp_flops_per_ipm_iter(6, 3, K, rows) * ipm_iters / args.steps
     achieved = flops / (qp_avg_ms * 1e-3) / 1e12
+    traffic, traffic_src = committed_traffic()
     if rank == 0:
         cpu = None
         if not args.no_cpu:
@@ -165,7 +180,8 @@ def main():
                                    "tr=0.25, 8 obstacles (soft), SOC ||u||<=1, box |x|,|y|<=12",
                        "agents_per_gpu": N, "K": K, "parallelism": f"agents sharded x{world}"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
+                         "traffic_unit": "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE)", "traffic_source": traffic_src,
                          "kernel": "qp_ipm_kernel", "kernel_ms": qp_avg_ms,
                          "note": "FP64 VALU-bound small dense linear algebra; peak = FP64 dense peak; "
                                  "algorithmic FLOPs per DESIGN.md §4 x executed IPM iterations"},
