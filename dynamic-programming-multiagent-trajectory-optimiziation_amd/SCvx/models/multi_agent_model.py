@@ -3,6 +3,8 @@ d_min, and the linearized pairwise collision normal a_k = (p_i - p_j)/(|p_i - p_
 b_k = d_min + a_k' p_j (KAT: SCvx/multi_agent_tests/test_multi_agent_model.py:42-59)."""
 import numpy as np
 
+from ..global_parameters import K as GLOBAL_K
+from ..optimization.variables import Variable
 from .unicycle_model import UnicycleModel
 
 
@@ -26,6 +28,7 @@ class MultiAgentModel:
             m = UnicycleModel(**kw)
             if params.get("obstacles") is not None:
                 m.obstacles = params["obstacles"]
+                m.s_prime = [Variable((GLOBAL_K, 1), nonneg=True) for _ in m.obstacles]  # :40-41
             self.models.append(m)
         self.d_min = d_min
 

@@ -4,6 +4,8 @@ from typing import List, Optional, Tuple
 
 import numpy as np
 
+from ..global_parameters import K
+from ..optimization.variables import Variable
 from .base_model import BaseModel, straight_line
 
 MARGIN_OBS = 0.0  # SCvx/config/SI_default_game.py:9 (extra clearance around static obstacles)
@@ -24,7 +26,7 @@ class SingleIntegratorModel(BaseModel):
         self.lower_bound, self.upper_bound = bounds
         self.robot_radius = robot_radius
         self.obstacles = obstacles if obstacles is not None else [([-5.0, -4.0, -5.0], 2.0), ([0.0, 0.0, 4.0], 2.0)]
-        self.s_prime = []
+        self.s_prime = [Variable((K, 1), nonneg=True) for _ in self.obstacles]  # :51
         self.f = lambda x, u: np.asarray(u, float).reshape(-1).copy()
         self.A = lambda x, u: np.zeros((self.n_x, self.n_x))
         self.B = lambda x, u: np.eye(self.n_x)
@@ -36,3 +38,12 @@ class SingleIntegratorModel(BaseModel):
         straight_line(X, self.x_init, self.x_final)
         U[:] = 0
         return X, U
+
+    def scp_constraints(self):
+        """get_constraints (single_integrator_model.py:80-126) as solver template data: BCs, per-node
+        SOC ||u_k|| <= v_max, box X[0:3] within [lb + r, ub - r], linearized spheres with clearance
+        r + robot_radius + MARGIN_OBS and slack s_prime."""
+        lb, ub, r = self.lower_bound, self.upper_bound, self.robot_radius
+        return dict(pos_dim=3, x_init=self.x_init, x_final=self.x_final, u_bounds=[], u_soc=self.v_max,
+                    x_bounds=[(i, lb + r, ub - r) for i in range(3)],
+                    obs=[(np.asarray(c, float)[:3], rad + r + MARGIN_OBS) for c, rad in self.obstacles])

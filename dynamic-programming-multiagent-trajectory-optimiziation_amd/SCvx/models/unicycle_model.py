@@ -6,6 +6,8 @@ from typing import List, Optional, Tuple
 
 import numpy as np
 
+from ..global_parameters import K
+from ..optimization.variables import Variable
 from .base_model import BaseModel, straight_line
 
 
@@ -25,7 +27,8 @@ class UnicycleModel(BaseModel):
         self.robot_radius = robot_radius
         self.obstacles = obstacles if obstacles is not None else [([5.0, 4.0], 3.0), ([-5.0, -4.0], 3.0),
                                                                   ([0.0, 0.0], 2.0)]
-        self.s_prime = []  # slack variables live inside the batched solver
+        # obstacle slacks (unicycle_model.py:51); values are filled in by the batched solve
+        self.s_prime = [Variable((K, 1), nonneg=True) for _ in self.obstacles]
 
     @staticmethod
     def _f(x, u):
@@ -51,3 +54,13 @@ class UnicycleModel(BaseModel):
         straight_line(X, self.x_init, self.x_final)
         U[:] = 0
         return X, U
+
+    def scp_constraints(self):
+        """The constraint set of get_constraints (unicycle_model.py:88-114) as solver template data:
+        BCs, 0 <= v <= v_max, |w| <= w_max, box X[0:2] within [lb + r, ub - r], linearized obstacles
+        with total clearance r + robot_radius and slack s_prime."""
+        lb, ub, r = self.lower_bound, self.upper_bound, self.robot_radius
+        return dict(pos_dim=2, x_init=self.x_init, x_final=self.x_final,
+                    u_bounds=[(0, 0.0, self.v_max), (1, -self.w_max, self.w_max)], u_soc=None,
+                    x_bounds=[(i, lb + r, ub - r) for i in range(2)],
+                    obs=[(np.asarray(c, float)[:2], rad + r) for c, rad in self.obstacles])

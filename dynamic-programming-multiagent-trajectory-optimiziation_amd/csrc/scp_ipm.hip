@@ -1,0 +1,1177 @@
+// Batched SCvx convex subproblem (SCProblem / AgentSolver) for MI355X (gfx950), float64.
+//
+// Replaces the CVXPY+ECOS solve of SCvx/optimization/sc_problem.py:15-105 (SCVXSolver's subproblem,
+// scvx_solver.py:55-71) and of AgentSolver.setup/solve (agent_solver.py:43-117,
+// si_agent_solver.py:39-105), batched over N agents; the problem is stated in include/scvx_hip.h.
+// oracle/scp_cpu.py is the line-by-line CPU restatement of this kernel, oracle/scp_dense.py the
+// independent reference-formulation checker.
+//
+// Reformulation (exact), per node k: z_k = [xi_k (n) | g (4) | u_k (m) | nu_k (n)] with
+//   xi_k = x_k - C_{k-1} u_k            (FOH transform: the dynamics lose the u_{k+1} term)
+//   g    = (sigma, tau_x, tau_u, tau_nu) augmented Riccati state, g_{k+1} = g_k
+// The induced 1-norms become L1-ball facets s'(x_k - xbar_k) <= tau_x, s'(u_k - ubar_k) <= tau_u,
+// s'nu_k <= tau_nu with |sigma - sigma_ref| + tau_x + tau_u <= tr at node 0; x_{K-1} = x_final is
+// eliminated by substituting nu_{K-2} from the K-2 dynamics into its facets (the K-2 dynamics then
+// pin xi_{K-1}); u_0, u_{K-1}, nu_{K-1} (absent) and nu_{K-2} are pinned inputs; x_0 = x_init is the
+// Riccati initial state with g_0 free.  Soft rows (obstacles, ADMM collision rows) keep their slack,
+// eliminated per row.  Every cost term is divided by an objective scale cs so the duals are O(1).
+//
+// Mapping: one agent per 64-lane workgroup.  Node phases are lane-parallel (node t on lane t % 64);
+// the Riccati factor and the two solve sweeps are sequential over nodes and element-parallel over
+// lanes, with the stage matrices in LDS.  Per-node data (rows in z coordinates, iterates, scaling,
+// factor outputs) lives in an agent-private workspace block per node.  Problems are small (K <= 256,
+// |z| <= 13): this kernel targets the reference's single-agent SCVXSolver / few-agent ADMM use, not
+// the batched headline path (csrc/qp_ipm.hpp).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "common.hpp"
+#include "scvx_hip.h"
+#include "wave_ops.hpp"
+
+namespace scvx {
+namespace {
+
+constexpr int SCP_NG = 4;
+constexpr int SCP_KMAX = 256;
+
+struct SCPArgs {
+    scvx_scp_template T;
+    int N;
+    const double *disc, *Xref, *Uref, *sigma_ref, *tr, *x_init, *x_final, *nbr_pos, *nbr_Y, *nbr_Lam;
+    double *X, *U, *nu, *sigma, *s_obs, *s_nbr, *obj;
+    int32_t *status, *iters;
+    double* ws;
+    long long ws_agent;
+};
+
+// node-block layout (doubles); counts are runtime (rows depend on the template)
+struct SCPLay {
+    int RH, NS, Q, RL, ROWS, stride;
+    int o_rows, o_q, o_P, o_At, o_Bt, o_ct, o_z, o_sig, o_s, o_lam, o_wl, o_sw, o_lt, o_H, o_f, o_rd, o_rc, o_rsig,
+        o_t, o_rho, o_rhs, o_dz, o_dsig, o_ds, o_dl, o_dsa, o_dla, o_y, o_yp, o_rp, o_K, o_Pr, o_pv, o_kv, o_LD, o_nh;
+};
+
+__host__ __device__ inline SCPLay scp_layout(const scvx_scp_template& T) {
+    const int n = T.n_x, m = T.n_u;
+    const int NXA = n + SCP_NG, NUA = m + n, NZ = NXA + NUA;
+    SCPLay L{};
+    int sides = 0;
+    for (int b = 0; b < T.n_ubound; ++b) sides += (T.ub_has_lo[b] ? 1 : 0) + (T.ub_has_hi[b] ? 1 : 0);
+    L.RH = (1 << n) + (1 << m) + (1 << n) + sides + 2 * T.n_xbound + 3;
+    L.NS = T.n_obs + T.n_nbr;
+    L.Q = T.has_soc ? m + 1 : 0;
+    L.RL = L.RH + 2 * L.NS + L.Q;
+    L.ROWS = L.RH + L.NS + L.Q;
+    int o = 0;
+    auto take = [&](int sz) { const int r = o; o += sz; return r; };
+    L.o_rows = take(L.ROWS * (NZ + 1));
+    L.o_q = take(NZ);
+    L.o_P = take(NZ * NZ);
+    L.o_At = take(NXA * NXA);
+    L.o_Bt = take(NXA * NUA);
+    L.o_ct = take(NXA);
+    L.o_z = take(NZ);
+    L.o_sig = take(L.NS);
+    L.o_s = take(L.RL);
+    L.o_lam = take(L.RL);
+    L.o_wl = take(L.RH + 2 * L.NS);
+    L.o_sw = take(L.Q + 1);
+    L.o_lt = take(L.RL);
+    L.o_H = take(NZ * NZ);
+    L.o_f = take(NZ);
+    L.o_rd = take(NZ);
+    L.o_rc = take(L.RL);
+    L.o_rsig = take(L.NS);
+    L.o_t = take(L.RL);
+    L.o_rho = take(L.RL);
+    L.o_rhs = take(L.NS);
+    L.o_dz = take(NZ);
+    L.o_dsig = take(L.NS);
+    L.o_ds = take(L.RL);
+    L.o_dl = take(L.RL);
+    L.o_dsa = take(L.RL);
+    L.o_dla = take(L.RL);
+    L.o_y = take(NXA);
+    L.o_yp = take(NXA);
+    L.o_rp = take(NXA);
+    L.o_K = take(NUA * NXA);
+    L.o_Pr = take(NXA * NXA);
+    L.o_pv = take(NXA);
+    L.o_kv = take(NUA);
+    L.o_LD = take(NUA * NUA);
+    L.o_nh = take(1);
+    L.stride = (o + 7) & ~7;
+    return L;
+}
+
+// LDL' of a small symmetric block in registers, pivots clamped at rel * max|diag| (the dynamic
+// regularisation of oracle/scp_cpu.py:ldl_solve); Lm holds L below the diagonal and 1/d on it.
+template <int D>
+__device__ __forceinline__ void ldl_factor(double (&Lm)[D * D], int nn) {
+    double dmax = 0.0;
+    for (int j = 0; j < nn; ++j) dmax = fmax(dmax, fabs(Lm[j * D + j]));
+    const double dmin = 1e-13 * dmax + 1e-300;
+    double dg[D];
+    for (int j = 0; j < nn; ++j) {
+        double d = Lm[j * D + j];
+        for (int k = 0; k < j; ++k) d -= Lm[j * D + k] * Lm[j * D + k] * dg[k];
+        d = d > dmin ? d : dmin;
+        dg[j] = d;
+        const double inv = 1.0 / d;
+        for (int i = j + 1; i < nn; ++i) {
+            double v = Lm[i * D + j];
+            for (int k = 0; k < j; ++k) v -= Lm[i * D + k] * Lm[j * D + k] * dg[k];
+            Lm[i * D + j] = v * inv;
+        }
+        Lm[j * D + j] = inv;
+    }
+}
+template <int D>
+__device__ __forceinline__ void ldl_solve(const double (&Lm)[D * D], int nn, double (&x)[D]) {
+    for (int i = 0; i < nn; ++i)
+        for (int k = 0; k < i; ++k) x[i] -= Lm[i * D + k] * x[k];
+    for (int i = 0; i < nn; ++i) x[i] *= Lm[i * D + i];
+    for (int i = nn - 1; i >= 0; --i)
+        for (int k = i + 1; k < nn; ++k) x[i] -= Lm[k * D + i] * x[k];
+}
+
+// ---- second-order cone algebra (dimension Q = m + 1 <= 4), hyperbolic-rotation NT scaling
+template <int QM>
+struct Soc {
+    // W v and W^-1 v from (w, eta)
+    __device__ static void wmul(const double* w, double eta, const double* vin, double* out, int Q, bool inv) {
+        double v[QM];
+        for (int i = 0; i < Q; ++i) v[i] = vin[i];
+        double w1v1 = 0.0;
+        for (int i = 1; i < Q; ++i) w1v1 += w[i] * v[i];
+        const double sgn = inv ? -1.0 : 1.0;
+        const double sc = inv ? 1.0 / eta : eta;
+        out[0] = sc * (w[0] * v[0] + sgn * w1v1);
+        const double c = sgn * v[0] + w1v1 / (1.0 + w[0]);
+        for (int i = 1; i < Q; ++i) out[i] = sc * (v[i] + c * w[i]);
+    }
+    __device__ static void nt(const double* s, const double* z, double* w, double& eta, int Q) {
+        double js = s[0] * s[0], jz = z[0] * z[0];
+        for (int i = 1; i < Q; ++i) { js -= s[i] * s[i]; jz -= z[i] * z[i]; }
+        const double rs = 1.0 / sqrt(js), rz = 1.0 / sqrt(jz);
+        double sz = 0.0;
+        for (int i = 0; i < Q; ++i) sz += s[i] * rs * z[i] * rz;
+        const double gam = sqrt(0.5 * (1.0 + sz));
+        const double ig = 0.5 / gam;
+        w[0] = (s[0] * rs + z[0] * rz) * ig;
+        for (int i = 1; i < Q; ++i) w[i] = (s[i] * rs - z[i] * rz) * ig;
+        eta = sqrt(sqrt(js / jz));
+    }
+    __device__ static void jprod(const double* a, const double* b, double* out, int Q) {
+        double d = 0.0;
+        for (int i = 0; i < Q; ++i) d += a[i] * b[i];
+        const double a0 = a[0], b0 = b[0];
+        for (int i = 1; i < Q; ++i) out[i] = a0 * b[i] + b0 * a[i];
+        out[0] = d;
+    }
+    __device__ static void jdiv(const double* x, const double* r, double* out, int Q) {
+        double d = x[0] * x[0], xr = x[0] * r[0];
+        for (int i = 1; i < Q; ++i) { d -= x[i] * x[i]; xr -= x[i] * r[i]; }
+        const double r0 = xr / d;
+        for (int i = 1; i < Q; ++i) out[i] = (r[i] - r0 * x[i]) / x[0];
+        out[0] = r0;
+    }
+    __device__ static double step(const double* x, const double* dx, int Q) {
+        double qa = dx[0] * dx[0], qb = x[0] * dx[0], qc = x[0] * x[0];
+        for (int i = 1; i < Q; ++i) { qa -= dx[i] * dx[i]; qb -= x[i] * dx[i]; qc -= x[i] * x[i]; }
+        qb *= 2.0;
+        double a = INFINITY;
+        if (fabs(qa) > 1e-300) {
+            const double disc = qb * qb - 4.0 * qa * qc;
+            if (disc >= 0.0) {
+                const double sq = sqrt(disc);
+                const double r1 = (-qb - sq) / (2.0 * qa), r2 = (-qb + sq) / (2.0 * qa);
+                if (r1 > 0.0 && x[0] + r1 * dx[0] >= -1e-14) a = fmin(a, r1);
+                if (r2 > 0.0 && x[0] + r2 * dx[0] >= -1e-14) a = fmin(a, r2);
+            }
+        } else if (qb != 0.0 && -qc / qb > 0.0) {
+            a = fmin(a, -qc / qb);
+        }
+        if (dx[0] < 0.0) a = fmin(a, -x[0] / dx[0]);
+        return a;
+    }
+    __device__ static double mineig(const double* x, int Q) {
+        double nr = 0.0;
+        for (int i = 1; i < Q; ++i) nr += x[i] * x[i];
+        return x[0] - sqrt(nr);
+    }
+};
+
+template <int NX, int NU>
+__global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
+    constexpr int NXA = NX + SCP_NG, NUA = NU + NX, NZ = NXA + NUA, RS = NZ + 1;
+    constexpr int SIG = NX, TX = NX + 1, TU = NX + 2, TN = NX + 3, ZU = NX + SCP_NG, ZN = ZU + NU;
+    constexpr int QM = NU + 1;
+    const scvx_scp_template& T = a.T;
+    const int K = T.K, lane = threadIdx.x, pd = T.pos_dim;
+    const long long agent = blockIdx.x;
+    const SCPLay Ly = scp_layout(T);
+    const int RH = Ly.RH, NS = Ly.NS, Q = Ly.Q, RL = Ly.RL, NLP = RH + 2 * NS;
+    double* ws = a.ws + agent * a.ws_agent;
+    auto nb = [&](int t) -> double* { return ws + (long long)t * Ly.stride; };
+    const double* disc = a.disc + agent * (long long)(K - 1) * (NX * (NX + 2 * NU + 2));
+    constexpr int DSTR = NX * (NX + 2 * NU + 2);
+    const double trv = a.tr[agent], sref = a.sigma_ref[agent];
+    const double* xinit = a.x_init + agent * NX;
+    const double* xfin = a.x_final + agent * NX;
+    const bool fin = T.has_final != 0;
+
+    __shared__ double sP[NXA * NXA], sPv[NXA], sH[NZ * NZ], sAt[NXA * NXA], sBt[NXA * NUA], sPA[NXA * NXA],
+        sPB[NXA * NUA], sQxx[NXA * NXA], sQux[NUA * NXA], sQuu[NUA * NUA], sK[NUA * NXA], sV[NXA], sQ[NZ],
+        sXi[2][NXA], sU[NUA], sMisc[32];
+    // sMisc: 0..NX-1 r_init, 8..8+NX-1 y0+, 16.. scalars
+    auto pinned = [&](int t, int i) -> bool {  // i: z index
+        if (i >= ZU && i < ZN) return (t == 0 && T.pin_u_first) || (t == K - 1 && T.pin_u_last);
+        if (i >= ZN) return t == K - 1 || (fin && t == K - 2);
+        return false;
+    };
+    auto Cprev = [&](int t, int i, int j) -> double {  // C_{t-1}[i][j]
+        return t > 0 ? disc[(long long)(t - 1) * DSTR + NX * NX + NX * NU + j * NX + i] : 0.0;
+    };
+
+    // ------------------------------------------------------------------ setup (rows, dynamics)
+    // objective scale: every cost term / cs (oracle/scp_cpu.py build_nodes)
+    double csl = 0.0;
+    for (int t = lane; t < K; t += WAVE) {
+        for (int j = 0; j < T.n_nbr; ++j)
+            for (int i = 0; i < pd; ++i) {
+                const long long o = ((agent * T.n_nbr + j) * K + t) * pd + i;
+                csl = fmax(csl, fabs(a.nbr_Lam[o] - T.rho * a.nbr_Y[o]));
+            }
+    }
+    double cs = wave_max(csl);
+    cs = fmax(cs, fmax(1.0, fmax(T.w_nu, T.w_sigma)));
+    if (T.n_obs > 0) cs = fmax(cs, T.w_slack);
+    if (T.n_nbr > 0) cs = fmax(cs, fmax(T.w_coll, T.rho));
+    const double ics = 1.0 / cs;
+    const double w_obs = T.w_slack * ics, w_col = T.w_coll * ics;
+    double hmax = 0.0, qmax = 0.0, degl = 0.0;
+    for (int t = lane; t < K; t += WAVE) {
+        double* B = nb(t);
+        double xb[NX], ub[NU];
+        for (int i = 0; i < NX; ++i) xb[i] = a.Xref[(agent * K + t) * NX + i];
+        for (int j = 0; j < NU; ++j) ub[j] = a.Uref[(agent * K + t) * NU + j];
+        double Cp[NX * NU];
+        for (int i = 0; i < NX; ++i)
+            for (int j = 0; j < NU; ++j) Cp[i * NU + j] = Cprev(t, i, j);
+        const bool subst = fin && t == K - 2;
+        const double* dk = disc + (long long)t * DSTR;  // only read when t < K-1
+        // write one row given v-coordinate coefficients
+        auto put = [&](int r, double* av, double h) {
+            if (subst) {  // nu_{K-2} = x_final - (A x + B u + S sigma + z)   (u_{K-1} pinned at 0)
+                double an[NX];
+                for (int i = 0; i < NX; ++i) an[i] = av[ZN + i];
+                for (int l = 0; l < NX; ++l) {
+                    double v = 0.0;
+                    for (int i = 0; i < NX; ++i) v += dk[l * NX + i] * an[i];  // (A' an)_l, A col-major
+                    av[l] -= v;
+                }
+                for (int j = 0; j < NU; ++j) {
+                    double v = 0.0;
+                    for (int i = 0; i < NX; ++i) v += dk[NX * NX + j * NX + i] * an[i];
+                    av[ZU + j] -= v;
+                }
+                double sv = 0.0, hz = 0.0;
+                for (int i = 0; i < NX; ++i) {
+                    sv += dk[NX * NX + 2 * NX * NU + i] * an[i];
+                    hz += an[i] * (xfin[i] - dk[NX * NX + 2 * NX * NU + NX + i]);
+                    av[ZN + i] = 0.0;
+                }
+                av[SIG] -= sv;
+                h -= hz;
+            }
+            // FOH transform: a_u += C_{t-1}' a_x
+            for (int j = 0; j < NU; ++j) {
+                double v = 0.0;
+                for (int i = 0; i < NX; ++i) v += Cp[i * NU + j] * av[i];
+                av[ZU + j] += v;
+            }
+            double* rp = B + Ly.o_rows + r * RS;
+            for (int i = 0; i < NZ; ++i) rp[i] = av[i];
+            rp[NZ] = h;
+            hmax = fmax(hmax, fabs(h));
+        };
+        double av[NZ];
+        auto clr = [&]() { for (int i = 0; i < NZ; ++i) av[i] = 0.0; };
+        int r = 0;
+        for (int s = 0; s < (1 << NX); ++s) {  // TR facets on x
+            clr();
+            double h = 0.0;
+            for (int i = 0; i < NX; ++i) { const double sg = (s >> (NX - 1 - i)) & 1 ? -1.0 : 1.0; av[i] = sg; h += sg * xb[i]; }
+            av[TX] = -1.0;
+            put(r++, av, h);
+        }
+        for (int s = 0; s < (1 << NU); ++s) {  // TR facets on u
+            clr();
+            double h = 0.0;
+            for (int j = 0; j < NU; ++j) { const double sg = (s >> (NU - 1 - j)) & 1 ? -1.0 : 1.0; av[ZU + j] = sg; h += sg * ub[j]; }
+            av[TU] = -1.0;
+            put(r++, av, h);
+        }
+        if (t < K - 1)
+            for (int s = 0; s < (1 << NX); ++s) {  // ||nu_t||_1 <= tau_nu facets
+                clr();
+                for (int i = 0; i < NX; ++i) av[ZN + i] = (s >> (NX - 1 - i)) & 1 ? -1.0 : 1.0;
+                av[TN] = -1.0;
+                put(r++, av, 0.0);
+            }
+        for (int b = 0; b < T.n_ubound; ++b) {
+            const int j = T.ub_idx[b];
+            // a bound on a pinned input (u_0 = u_{K-1} = 0) is a constant row; keeping it would give
+            // the IPM an empty-interior block (s -> 0, lambda -> inf) whenever the bound is 0
+            if (pinned(t, ZU + j)) continue;
+            if (T.ub_has_hi[b]) { clr(); av[ZU + j] = 1.0; put(r++, av, T.ub_hi[b]); }
+            if (T.ub_has_lo[b]) { clr(); av[ZU + j] = -1.0; put(r++, av, -T.ub_lo[b]); }
+        }
+        for (int b = 0; b < T.n_xbound; ++b) {
+            const int i = T.xb_idx[b];
+            clr(); av[i] = 1.0; put(r++, av, T.xb_hi[b]);
+            clr(); av[i] = -1.0; put(r++, av, -T.xb_lo[b]);
+        }
+        if (t == 0) {
+            clr(); av[SIG] = -1.0; put(r++, av, 0.0);
+            clr(); av[SIG] = 1.0; av[TX] = 1.0; av[TU] = 1.0; put(r++, av, trv + sref);
+            clr(); av[SIG] = -1.0; av[TX] = 1.0; av[TU] = 1.0; put(r++, av, trv - sref);
+        }
+        B[Ly.o_nh] = (double)r;
+        degl += r + 2 * NS + (Q > 0 ? 1 : 0);
+        // soft rows: obstacles, then ADMM collision rows
+        for (int o = 0; o < T.n_obs; ++o) {
+            clr();
+            double nr = 0.0, d[3] = {0, 0, 0};
+            for (int i = 0; i < pd; ++i) { d[i] = xb[i] - T.obs_center[o][i]; nr += d[i] * d[i]; }
+            nr = sqrt(nr) + 1e-6;
+            double ac = 0.0;
+            for (int i = 0; i < pd; ++i) { av[i] = -d[i] / nr; ac += d[i] / nr * T.obs_center[o][i]; }
+            put(RH + o, av, -T.obs_radius[o] - ac);
+        }
+        for (int j = 0; j < T.n_nbr; ++j) {
+            clr();
+            const long long base = ((agent * T.n_nbr + j) * K + t) * pd;
+            double nr = 0.0, d[3] = {0, 0, 0};
+            for (int i = 0; i < pd; ++i) { d[i] = xb[i] - a.nbr_pos[base + i]; nr += d[i] * d[i]; }
+            nr = sqrt(nr) + 1e-6;
+            double ay = 0.0;
+            for (int i = 0; i < pd; ++i) { av[i] = -d[i] / nr; ay += d[i] / nr * a.nbr_Y[base + i]; }
+            put(RH + T.n_obs + j, av, -T.d_min - ay);
+        }
+        if (Q > 0) {
+            clr(); put(RH + NS, av, T.u_max);
+            for (int j = 0; j < NU; ++j) { clr(); av[ZU + j] = -1.0; put(RH + NS + 1 + j, av, 0.0); }
+        }
+        // linear / quadratic cost (z coordinates)
+        double qv[NZ];
+        for (int i = 0; i < NZ; ++i) qv[i] = 0.0;
+        if (t == 0) { qv[SIG] = T.w_sigma * ics; qv[TN] = T.w_nu * ics; }
+        double pv = 0.0;
+        for (int j = 0; j < T.n_nbr; ++j) {
+            const long long base = ((agent * T.n_nbr + j) * K + t) * pd;
+            for (int i = 0; i < pd; ++i) qv[i] += (a.nbr_Lam[base + i] - T.rho * a.nbr_Y[base + i]) * ics;
+            pv += T.rho * ics;
+        }
+        for (int j = 0; j < NU; ++j) {
+            double v = 0.0;
+            for (int i = 0; i < NX; ++i) v += Cp[i * NU + j] * qv[i];
+            qv[ZU + j] += v;
+        }
+        for (int i = 0; i < NZ; ++i) { B[Ly.o_q + i] = qv[i]; qmax = fmax(qmax, fabs(qv[i])); }
+        // P_z = T' diag(pv on positions) T
+        for (int i = 0; i < NZ; ++i)
+            for (int j = 0; j < NZ; ++j) {
+                double v = 0.0;
+                for (int l = 0; l < pd; ++l) {
+                    const double ti = i == l ? 1.0 : (i >= ZU && i < ZN ? Cp[l * NU + (i - ZU)] : 0.0);
+                    const double tj = j == l ? 1.0 : (j >= ZU && j < ZN ? Cp[l * NU + (j - ZU)] : 0.0);
+                    v += ti * pv * tj;
+                }
+                B[Ly.o_P + i * NZ + j] = v;
+            }
+        // dynamics to node t+1 (Riccati coordinates)
+        if (t < K - 1) {
+            double* At = B + Ly.o_At;
+            double* Bt = B + Ly.o_Bt;
+            double* ct = B + Ly.o_ct;
+            for (int e = 0; e < NXA * NXA; ++e) At[e] = 0.0;
+            for (int e = 0; e < NXA * NUA; ++e) Bt[e] = 0.0;
+            for (int g = 0; g < SCP_NG; ++g) { At[(NX + g) * NXA + NX + g] = 1.0; ct[NX + g] = 0.0; }
+            if (subst) {
+                for (int i = 0; i < NX; ++i) ct[i] = xfin[i];
+            } else {
+                for (int i = 0; i < NX; ++i) {
+                    for (int l = 0; l < NX; ++l) At[i * NXA + l] = dk[l * NX + i];
+                    At[i * NXA + SIG] = dk[NX * NX + 2 * NX * NU + i];
+                    for (int j = 0; j < NU; ++j) {
+                        double v = dk[NX * NX + j * NX + i];
+                        for (int l = 0; l < NX; ++l) v += dk[l * NX + i] * Cp[l * NU + j];
+                        Bt[i * NUA + j] = v;
+                    }
+                    Bt[i * NUA + NU + i] = 1.0;
+                    ct[i] = dk[NX * NX + 2 * NX * NU + NX + i];
+                }
+            }
+            for (int i = 0; i < NXA; ++i) hmax = fmax(hmax, fabs(ct[i]));
+        }
+    }
+    if (lane < NX) hmax = fmax(hmax, fabs(xinit[lane]));
+    const double pscale = 1.0 + wave_max(hmax);
+    double dsc = wave_max(qmax);
+    if (T.n_obs > 0) dsc = fmax(dsc, w_obs);
+    if (T.n_nbr > 0) dsc = fmax(dsc, w_col);
+    const double dscale = 1.0 + dsc;
+    const double deg = wave_sum(degl);
+    __syncthreads();
+
+    auto soft_w = [&](int r) -> double { return r < T.n_obs ? w_obs : w_col; };
+
+    // ------------------------------------------------------------------ Riccati factor (uses o_H)
+    auto factor = [&]() {
+        for (int e = lane; e < NXA * NXA; e += WAVE) sP[e] = 0.0;
+        __syncthreads();
+        for (int t = K - 1; t >= 0; --t) {
+            const double* B = nb(t);
+            for (int e = lane; e < NZ * NZ; e += WAVE) sH[e] = B[Ly.o_H + e];
+            const bool dyn = t < K - 1;
+            if (dyn) {
+                for (int e = lane; e < NXA * NXA; e += WAVE) sAt[e] = B[Ly.o_At + e];
+                for (int e = lane; e < NXA * NUA; e += WAVE) sBt[e] = B[Ly.o_Bt + e];
+            }
+            __syncthreads();
+            if (dyn) {
+                for (int e = lane; e < NXA * (NXA + NUA); e += WAVE) {
+                    const int i = e / (NXA + NUA), j = e % (NXA + NUA);
+                    double v = 0.0;
+                    if (j < NXA) {
+                        for (int k = 0; k < NXA; ++k) v += sP[i * NXA + k] * sAt[k * NXA + j];
+                        sPA[i * NXA + j] = v;
+                    } else {
+                        for (int k = 0; k < NXA; ++k) v += sP[i * NXA + k] * sBt[k * NUA + j - NXA];
+                        sPB[i * NUA + j - NXA] = v;
+                    }
+                }
+                __syncthreads();
+            }
+            for (int e = lane; e < NXA * NXA + NUA * NXA + NUA * NUA; e += WAVE) {
+                if (e < NXA * NXA) {
+                    const int i = e / NXA, j = e % NXA;
+                    double v = sH[i * NZ + j];
+                    if (dyn)
+                        for (int k = 0; k < NXA; ++k) v += sAt[k * NXA + i] * sPA[k * NXA + j];
+                    sQxx[e] = v;
+                } else if (e < NXA * NXA + NUA * NXA) {
+                    const int o = e - NXA * NXA, i = o / NXA, j = o % NXA;
+                    double v = sH[(NXA + i) * NZ + j];
+                    if (dyn)
+                        for (int k = 0; k < NXA; ++k) v += sBt[k * NUA + i] * sPA[k * NXA + j];
+                    sQux[o] = pinned(t, NXA + i) ? 0.0 : v;
+                } else {
+                    const int o = e - NXA * NXA - NUA * NXA, i = o / NUA, j = o % NUA;
+                    double v = sH[(NXA + i) * NZ + NXA + j];
+                    if (dyn)
+                        for (int k = 0; k < NXA; ++k) v += sBt[k * NUA + i] * sPB[k * NUA + j];
+                    if (pinned(t, NXA + i) || pinned(t, NXA + j)) v = (i == j) ? 1.0 : 0.0;
+                    sQuu[o] = v;
+                }
+            }
+            __syncthreads();
+            double Lm[NUA * NUA];
+            for (int e = 0; e < NUA * NUA; ++e) Lm[e] = sQuu[e];
+            ldl_factor<NUA>(Lm, NUA);
+            if (lane < NXA) {
+                double x[NUA];
+                for (int i = 0; i < NUA; ++i) x[i] = -sQux[i * NXA + lane];
+                ldl_solve<NUA>(Lm, NUA, x);
+                for (int i = 0; i < NUA; ++i) {
+                    sK[i * NXA + lane] = x[i];
+                    nb(t)[Ly.o_K + i * NXA + lane] = x[i];
+                }
+            }
+            if (lane == 0)
+                for (int e = 0; e < NUA * NUA; ++e) nb(t)[Ly.o_LD + e] = Lm[e];
+            __syncthreads();
+            for (int e = lane; e < NXA * NXA; e += WAVE) {
+                const int i = e / NXA, j = e % NXA, p = i < j ? i : j, q = i < j ? j : i;
+                double v = sQxx[p * NXA + q];
+                for (int k = 0; k < NUA; ++k) v += sQux[k * NXA + p] * sK[k * NXA + q];
+                sP[e] = v;
+                nb(t)[Ly.o_Pr + e] = v;
+            }
+            __syncthreads();
+        }
+    };
+
+    // ------------------------------------------------------------------ LQ solve
+    // In: o_f (per node), o_rp (t < K-1), sMisc[0..NX) = r_init.  Out: o_dz, o_yp (costates y+),
+    // sMisc[8..8+NX) = y0+.
+    auto lqsolve = [&]() {
+        // backward: v = P_{t+1} rp_t + p_{t+1}; qx = fx + At'v; qu = fu + Bt'v; k = -Quu^-1 qu; p = qx + K'qu
+        for (int t = K - 1; t >= 0; --t) {
+            const double* B = nb(t);
+            const bool dyn = t < K - 1;
+            if (lane < NXA) {
+                double v = 0.0;
+                if (dyn) {
+                    const double* Bn = nb(t + 1);
+                    v = sPv[lane];
+                    for (int k = 0; k < NXA; ++k) v += Bn[Ly.o_Pr + lane * NXA + k] * B[Ly.o_rp + k];
+                }
+                sV[lane] = v;
+            }
+            __syncthreads();
+            if (lane < NZ) {
+                double v = B[Ly.o_f + lane];
+                if (dyn) {
+                    if (lane < NXA)
+                        for (int k = 0; k < NXA; ++k) v += B[Ly.o_At + k * NXA + lane] * sV[k];
+                    else
+                        for (int k = 0; k < NXA; ++k) v += B[Ly.o_Bt + k * NUA + lane - NXA] * sV[k];
+                }
+                if (pinned(t, lane)) v = 0.0;
+                sQ[lane] = v;
+            }
+            __syncthreads();
+            {
+                double Lm[NUA * NUA], x[NUA];
+                for (int e = 0; e < NUA * NUA; ++e) Lm[e] = B[Ly.o_LD + e];
+                for (int i = 0; i < NUA; ++i) x[i] = -sQ[NXA + i];
+                ldl_solve<NUA>(Lm, NUA, x);
+                if (lane < NUA) {
+                    // (select x[lane] without dynamic register indexing)
+                    double xv = 0.0;
+                    for (int i = 0; i < NUA; ++i) xv = (i == lane) ? x[i] : xv;
+                    nb(t)[Ly.o_kv + lane] = xv;
+                }
+            }
+            double pn = 0.0;
+            if (lane < NXA) {
+                pn = sQ[lane];
+                for (int k = 0; k < NUA; ++k) pn += B[Ly.o_K + k * NXA + lane] * sQ[NXA + k];
+                nb(t)[Ly.o_pv + lane] = pn;
+            }
+            __syncthreads();
+            if (lane < NXA) sPv[lane] = pn;
+            __syncthreads();
+        }
+        // stage 0: x part fixed (-r_init), g part free: P_gg dg = -(p_g + P_gx dx)
+        {
+            const double* B0 = nb(0);
+            double dx[NX];
+            for (int i = 0; i < NX; ++i) dx[i] = -sMisc[i];
+            double Lm[SCP_NG * SCP_NG], g[SCP_NG];
+            for (int i = 0; i < SCP_NG; ++i) {
+                double v = B0[Ly.o_pv + NX + i];
+                for (int k = 0; k < NX; ++k) v += B0[Ly.o_Pr + (NX + i) * NXA + k] * dx[k];
+                g[i] = -v;
+                for (int j = 0; j < SCP_NG; ++j) Lm[i * SCP_NG + j] = B0[Ly.o_Pr + (NX + i) * NXA + NX + j];
+            }
+            ldl_factor<SCP_NG>(Lm, SCP_NG);
+            ldl_solve<SCP_NG>(Lm, SCP_NG, g);
+            for (int i = 0; i < NX; ++i)
+                if (lane == i) sXi[0][lane] = dx[i];
+            for (int i = 0; i < SCP_NG; ++i)
+                if (lane == NX + i) sXi[0][lane] = g[i];
+            __syncthreads();
+            if (lane < NX) {
+                double v = B0[Ly.o_pv + lane];
+                for (int k = 0; k < NXA; ++k) v += B0[Ly.o_Pr + lane * NXA + k] * sXi[0][k];
+                sMisc[8 + lane] = v;
+            }
+        }
+        __syncthreads();
+        int cur = 0;
+        for (int t = 0; t < K; ++t) {
+            double* B = nb(t);
+            if (lane < NUA) {
+                double v = B[Ly.o_kv + lane];
+                for (int k = 0; k < NXA; ++k) v += B[Ly.o_K + lane * NXA + k] * sXi[cur][k];
+                sU[lane] = v;
+                B[Ly.o_dz + NXA + lane] = v;
+            }
+            if (lane < NXA) B[Ly.o_dz + lane] = sXi[cur][lane];
+            __syncthreads();
+            if (t < K - 1) {
+                if (lane < NXA) {
+                    double v = B[Ly.o_rp + lane];
+                    for (int k = 0; k < NXA; ++k) v += B[Ly.o_At + lane * NXA + k] * sXi[cur][k];
+                    for (int k = 0; k < NUA; ++k) v += B[Ly.o_Bt + lane * NUA + k] * sU[k];
+                    sXi[cur ^ 1][lane] = v;
+                }
+                __syncthreads();
+                cur ^= 1;
+                if (lane < NXA) {
+                    const double* Bn = nb(t + 1);
+                    double v = Bn[Ly.o_pv + lane];
+                    for (int k = 0; k < NXA; ++k) v += Bn[Ly.o_Pr + lane * NXA + k] * sXi[cur][k];
+                    B[Ly.o_yp + lane] = v;
+                }
+            }
+        }
+        __syncthreads();
+    };
+
+    // row helpers (node t, block B)
+    auto rowp = [&](const double* B, int r) -> const double* { return B + Ly.o_rows + r * RS; };
+    auto dot = [&](const double* a0, const double* z) -> double {
+        double v = 0.0;
+        for (int i = 0; i < NZ; ++i) v += a0[i] * z[i];
+        return v;
+    };
+
+    // ------------------------------------------------------------------ starting point (W = I)
+    for (int t = lane; t < K; t += WAVE) {
+        double* B = nb(t);
+        const int nh = (int)B[Ly.o_nh];
+        double Hu[NZ * NZ], f[NZ];
+        for (int e = 0; e < NZ * NZ; ++e) Hu[e] = B[Ly.o_P + e];
+        for (int i = 0; i < NZ; ++i) f[i] = B[Ly.o_q + i];
+        for (int r = 0; r < nh; ++r) {
+            const double* ar = rowp(B, r);
+            const double h = ar[NZ];
+            for (int i = 0; i < NZ; ++i) {
+                f[i] -= ar[i] * h;
+                for (int j = 0; j < NZ; ++j) Hu[i * NZ + j] += ar[i] * ar[j];
+            }
+        }
+        for (int r = 0; r < NS; ++r) {
+            const double* ar = rowp(B, RH + r);
+            const double h = ar[NZ];
+            const double rhs = -soft_w(r) - h;
+            B[Ly.o_rhs + r] = rhs;
+            for (int i = 0; i < NZ; ++i) {
+                f[i] -= ar[i] * (h + 0.5 * rhs);
+                for (int j = 0; j < NZ; ++j) Hu[i * NZ + j] += 0.5 * ar[i] * ar[j];
+            }
+        }
+        for (int r = 0; r < Q; ++r) {
+            const double* ar = rowp(B, RH + NS + r);
+            const double h = ar[NZ];
+            for (int i = 0; i < NZ; ++i) {
+                f[i] -= ar[i] * h;
+                for (int j = 0; j < NZ; ++j) Hu[i * NZ + j] += ar[i] * ar[j];
+            }
+        }
+        for (int i = 0; i < NZ; ++i) Hu[i * NZ + i] += T.reg;
+        for (int e = 0; e < NZ * NZ; ++e) B[Ly.o_H + e] = Hu[e];
+        for (int i = 0; i < NZ; ++i) B[Ly.o_f + i] = f[i];
+        if (t < K - 1)
+            for (int i = 0; i < NXA; ++i) B[Ly.o_rp + i] = B[Ly.o_ct + i];
+    }
+    if (lane < NX) sMisc[lane] = -xinit[lane];
+    __syncthreads();
+    factor();
+    lqsolve();
+    double mins = INFINITY, minl = INFINITY;
+    for (int t = lane; t < K; t += WAVE) {
+        double* B = nb(t);
+        const int nh = (int)B[Ly.o_nh];
+        double z[NZ];
+        for (int i = 0; i < NZ; ++i) { z[i] = B[Ly.o_dz + i]; B[Ly.o_z + i] = z[i]; }
+        for (int r = 0; r < nh; ++r) {
+            const double* ar = rowp(B, r);
+            const double sv = ar[NZ] - dot(ar, z);
+            B[Ly.o_s + r] = sv; B[Ly.o_lam + r] = -sv;
+            mins = fmin(mins, sv); minl = fmin(minl, -sv);
+        }
+        for (int r = 0; r < NS; ++r) {
+            const double* ar = rowp(B, RH + r);
+            const double az = dot(ar, z);
+            const double sg = 0.5 * (B[Ly.o_rhs + r] + az);
+            B[Ly.o_sig + r] = sg;
+            const double s1 = ar[NZ] - az + sg, s2 = sg;
+            B[Ly.o_s + RH + 2 * r] = s1; B[Ly.o_lam + RH + 2 * r] = -s1;
+            B[Ly.o_s + RH + 2 * r + 1] = s2; B[Ly.o_lam + RH + 2 * r + 1] = -s2;
+            mins = fmin(mins, fmin(s1, s2)); minl = fmin(minl, fmin(-s1, -s2));
+        }
+        if (Q > 0) {
+            double sv[QM], lv[QM];
+            for (int r = 0; r < Q; ++r) {
+                const double* ar = rowp(B, RH + NS + r);
+                sv[r] = ar[NZ] - dot(ar, z);
+                lv[r] = -sv[r];
+                B[Ly.o_s + NLP + r] = sv[r]; B[Ly.o_lam + NLP + r] = lv[r];
+            }
+            mins = fmin(mins, Soc<QM>::mineig(sv, Q));
+            minl = fmin(minl, Soc<QM>::mineig(lv, Q));
+        }
+        for (int i = 0; i < NXA; ++i) B[Ly.o_y + i] = 0.0;
+    }
+    {
+        const double as = wave_min(mins), al = wave_min(minl);
+        const double sh_s = fmax(0.0, 1.0 - as), sh_l = fmax(0.0, 1.0 - al);
+        for (int t = lane; t < K; t += WAVE) {
+            double* B = nb(t);
+            const int nh = (int)B[Ly.o_nh];
+            for (int r = 0; r < NLP; ++r) {
+                if (r >= nh && r < RH) continue;
+                B[Ly.o_s + r] += sh_s; B[Ly.o_lam + r] += sh_l;
+            }
+            if (Q > 0) { B[Ly.o_s + NLP] += sh_s; B[Ly.o_lam + NLP] += sh_l; }
+        }
+    }
+    double y0[NX];
+    for (int i = 0; i < NX; ++i) y0[i] = 0.0;
+    __syncthreads();
+
+    // ------------------------------------------------------------------ IPM iterations
+    int status = 1, it = 0;
+    bool near_ok = false;
+    for (it = 0; it < T.max_iter; ++it) {
+        // ---- residuals (node-parallel); rp needs xi~_{t+1}
+        double gapl = 0.0, pobjl = 0.0, presl = 0.0, dresl = 0.0;
+        for (int t = lane; t < K; t += WAVE) {
+            double* B = nb(t);
+            const int nh = (int)B[Ly.o_nh];
+            double z[NZ], rd[NZ];
+            for (int i = 0; i < NZ; ++i) z[i] = B[Ly.o_z + i];
+            for (int i = 0; i < NZ; ++i) {
+                double v = B[Ly.o_q + i];
+                for (int j = 0; j < NZ; ++j) v += B[Ly.o_P + i * NZ + j] * z[j];
+                pobjl += z[i] * (B[Ly.o_q + i] + 0.5 * (v - B[Ly.o_q + i]));
+                rd[i] = v;
+            }
+            for (int r = 0; r < nh; ++r) {
+                const double* ar = rowp(B, r);
+                const double l = B[Ly.o_lam + r], s = B[Ly.o_s + r];
+                for (int i = 0; i < NZ; ++i) rd[i] += ar[i] * l;
+                const double rc = dot(ar, z) + s - ar[NZ];
+                B[Ly.o_rc + r] = rc;
+                presl = fmax(presl, fabs(rc));
+                gapl += s * l;
+            }
+            for (int r = 0; r < NS; ++r) {
+                const double* ar = rowp(B, RH + r);
+                const double l1 = B[Ly.o_lam + RH + 2 * r], l2 = B[Ly.o_lam + RH + 2 * r + 1];
+                const double s1 = B[Ly.o_s + RH + 2 * r], s2 = B[Ly.o_s + RH + 2 * r + 1];
+                const double sg = B[Ly.o_sig + r];
+                for (int i = 0; i < NZ; ++i) rd[i] += ar[i] * l1;
+                const double rs = soft_w(r) - l1 - l2;
+                B[Ly.o_rsig + r] = rs;
+                dresl = fmax(dresl, fabs(rs));
+                const double rc1 = dot(ar, z) - sg + s1 - ar[NZ], rc2 = -sg + s2;
+                B[Ly.o_rc + RH + 2 * r] = rc1; B[Ly.o_rc + RH + 2 * r + 1] = rc2;
+                presl = fmax(presl, fmax(fabs(rc1), fabs(rc2)));
+                gapl += s1 * l1 + s2 * l2;
+                pobjl += soft_w(r) * sg;
+            }
+            for (int r = 0; r < Q; ++r) {
+                const double* ar = rowp(B, RH + NS + r);
+                const double l = B[Ly.o_lam + NLP + r], s = B[Ly.o_s + NLP + r];
+                for (int i = 0; i < NZ; ++i) rd[i] += ar[i] * l;
+                const double rc = dot(ar, z) + s - ar[NZ];
+                B[Ly.o_rc + NLP + r] = rc;
+                presl = fmax(presl, fabs(rc));
+                gapl += s * l;
+            }
+            // rd0 (no multipliers) -> o_rd; the full residual adds the dynamics multipliers
+            for (int i = 0; i < NZ; ++i) B[Ly.o_rd + i] = pinned(t, i) ? 0.0 : rd[i];
+            if (t < K - 1) {
+                double y[NXA];
+                for (int i = 0; i < NXA; ++i) y[i] = B[Ly.o_y + i];
+                for (int j = 0; j < NXA; ++j)
+                    for (int i = 0; i < NXA; ++i) rd[j] += B[Ly.o_At + i * NXA + j] * y[i];
+                for (int j = 0; j < NUA; ++j)
+                    for (int i = 0; i < NXA; ++i) rd[NXA + j] += B[Ly.o_Bt + i * NUA + j] * y[i];
+                const double* Bn = nb(t + 1);
+                for (int i = 0; i < NXA; ++i) {
+                    double v = B[Ly.o_ct + i] - Bn[Ly.o_z + i];
+                    for (int k = 0; k < NXA; ++k) v += B[Ly.o_At + i * NXA + k] * z[k];
+                    for (int k = 0; k < NUA; ++k) v += B[Ly.o_Bt + i * NUA + k] * z[NXA + k];
+                    B[Ly.o_rp + i] = v;
+                    presl = fmax(presl, fabs(v));
+                }
+            }
+            if (t > 0) {
+                const double* Bp = nb(t - 1);
+                for (int i = 0; i < NXA; ++i) rd[i] -= Bp[Ly.o_y + i];
+            } else {
+                for (int i = 0; i < NX; ++i) {
+                    rd[i] -= y0[i];
+                    const double ri = z[i] - xinit[i];
+                    presl = fmax(presl, fabs(ri));
+                }
+            }
+            for (int i = 0; i < NZ; ++i)
+                if (!pinned(t, i)) dresl = fmax(dresl, fabs(rd[i]));
+        }
+        const double gap = wave_sum(gapl), pobj = wave_sum(pobjl), pres = wave_max(presl), dres = wave_max(dresl);
+        if (!(gap == gap) || !(pres == pres) || !(dres == dres)) { status = 2; break; }
+        if (pres < T.tol * pscale && dres < T.tol * dscale && gap < T.tol * fmax(1.0, fabs(pobj))) { status = 0; break; }
+        // ECOS-style reduced tolerances: an iterate meeting them is reported "optimal_inaccurate"
+        // if the iteration cap or a numerical breakdown ends the solve before full accuracy
+        const double tol_i = fmax(1e-6, 1e3 * T.tol);
+        near_ok = pres < tol_i * pscale && dres < tol_i * dscale && gap < tol_i * fmax(1.0, fabs(pobj));
+        const double mu = gap / deg;
+        if (lane < NX) sMisc[lane] = nb(0)[Ly.o_z + lane] - xinit[lane];  // r_init
+        // ---- scaling and node Hessians
+        for (int t = lane; t < K; t += WAVE) {
+            double* B = nb(t);
+            const int nh = (int)B[Ly.o_nh];
+            double Hu[NZ * NZ];
+            for (int e = 0; e < NZ * NZ; ++e) Hu[e] = B[Ly.o_P + e];
+            for (int r = 0; r < NLP; ++r) {
+                if (r >= nh && r < RH) continue;
+                const double s = B[Ly.o_s + r], l = B[Ly.o_lam + r];
+                const double wl = sqrt(s / l);
+                B[Ly.o_wl + r] = wl;
+                B[Ly.o_lt + r] = sqrt(s * l);
+            }
+            for (int r = 0; r < nh; ++r) {
+                const double* ar = rowp(B, r);
+                const double d = B[Ly.o_lam + r] / B[Ly.o_s + r];
+                for (int i = 0; i < NZ; ++i) {
+                    const double di = d * ar[i];
+                    for (int j = 0; j < NZ; ++j) Hu[i * NZ + j] += di * ar[j];
+                }
+            }
+            for (int r = 0; r < NS; ++r) {
+                const double* ar = rowp(B, RH + r);
+                const double d1 = B[Ly.o_lam + RH + 2 * r] / B[Ly.o_s + RH + 2 * r];
+                const double d2 = B[Ly.o_lam + RH + 2 * r + 1] / B[Ly.o_s + RH + 2 * r + 1];
+                const double d = d1 * d2 / (d1 + d2);
+                for (int i = 0; i < NZ; ++i) {
+                    const double di = d * ar[i];
+                    for (int j = 0; j < NZ; ++j) Hu[i * NZ + j] += di * ar[j];
+                }
+            }
+            if (Q > 0) {
+                double s[QM], l[QM], w[QM], eta;
+                for (int r = 0; r < Q; ++r) { s[r] = B[Ly.o_s + NLP + r]; l[r] = B[Ly.o_lam + NLP + r]; }
+                Soc<QM>::nt(s, l, w, eta, Q);
+                for (int r = 0; r < Q; ++r) B[Ly.o_sw + r] = w[r];
+                B[Ly.o_sw + Q] = eta;
+                double lt[QM];
+                Soc<QM>::wmul(w, eta, l, lt, Q, false);
+                for (int r = 0; r < Q; ++r) B[Ly.o_lt + NLP + r] = lt[r];
+                // Wi^2 (Q x Q) column by column, then H += Gs' Wi^2 Gs
+                double M[QM * QM];
+                for (int c = 0; c < Q; ++c) {
+                    double e[QM], t1[QM], t2[QM];
+                    for (int r = 0; r < Q; ++r) e[r] = r == c ? 1.0 : 0.0;
+                    Soc<QM>::wmul(w, eta, e, t1, Q, true);
+                    Soc<QM>::wmul(w, eta, t1, t2, Q, true);
+                    for (int r = 0; r < Q; ++r) M[r * QM + c] = t2[r];
+                }
+                for (int r1 = 0; r1 < Q; ++r1) {
+                    const double* a1 = rowp(B, RH + NS + r1);
+                    for (int r2 = 0; r2 < Q; ++r2) {
+                        const double* a2 = rowp(B, RH + NS + r2);
+                        const double mm = M[r1 * QM + r2];
+                        if (mm == 0.0) continue;
+                        for (int i = 0; i < NZ; ++i) {
+                            const double di = mm * a1[i];
+                            for (int j = 0; j < NZ; ++j) Hu[i * NZ + j] += di * a2[j];
+                        }
+                    }
+                }
+            }
+            for (int i = 0; i < NZ; ++i) Hu[i * NZ + i] += T.reg;
+            for (int e = 0; e < NZ * NZ; ++e) B[Ly.o_H + e] = Hu[e];
+        }
+        __syncthreads();
+        factor();
+
+        // ---- one Newton direction: corrector = false -> affine (predictor)
+        auto direction = [&](bool corr, double sgmu) -> double {
+            for (int t = lane; t < K; t += WAVE) {
+                double* B = nb(t);
+                const int nh = (int)B[Ly.o_nh];
+                double f[NZ];
+                for (int i = 0; i < NZ; ++i) f[i] = B[Ly.o_rd + i];
+                // LP rows: lt = sqrt(s l), wl = sqrt(s/l); rcomp = -lt^2 [- (ds_a/wl)(wl dl_a) + sg mu]
+                for (int r = 0; r < NLP; ++r) {
+                    if (r >= nh && r < RH) continue;
+                    const double lt = B[Ly.o_lt + r], wl = B[Ly.o_wl + r];
+                    double rcv = -lt * lt;
+                    if (corr) rcv += -(B[Ly.o_dsa + r] * B[Ly.o_dla + r]) + sgmu;
+                    const double rho = rcv / lt;
+                    const double tv = rho / wl + B[Ly.o_rc + r] / (wl * wl);
+                    B[Ly.o_rho + r] = rho;
+                    B[Ly.o_t + r] = tv;
+                    if (r < nh) {
+                        const double* ar = rowp(B, r);
+                        for (int i = 0; i < NZ; ++i) f[i] += ar[i] * tv;
+                    }
+                }
+                for (int r = 0; r < NS; ++r) {
+                    const double* ar = rowp(B, RH + r);
+                    const double wl1 = B[Ly.o_wl + RH + 2 * r], wl2 = B[Ly.o_wl + RH + 2 * r + 1];
+                    const double d1 = 1.0 / (wl1 * wl1), d2 = 1.0 / (wl2 * wl2);
+                    const double t1 = B[Ly.o_t + RH + 2 * r], t2 = B[Ly.o_t + RH + 2 * r + 1];
+                    const double rhs = -B[Ly.o_rsig + r] + t1 + t2;
+                    B[Ly.o_rhs + r] = rhs;
+                    const double c = t1 - d1 * rhs / (d1 + d2);
+                    for (int i = 0; i < NZ; ++i) f[i] += ar[i] * c;
+                }
+                if (Q > 0) {
+                    double w[QM], lt[QM], rc[QM], rcv[QM], rho[QM], tmp[QM], tv[QM];
+                    for (int r = 0; r < Q; ++r) {
+                        w[r] = B[Ly.o_sw + r]; lt[r] = B[Ly.o_lt + NLP + r]; rc[r] = B[Ly.o_rc + NLP + r];
+                    }
+                    const double eta = B[Ly.o_sw + Q];
+                    Soc<QM>::jprod(lt, lt, rcv, Q);
+                    for (int r = 0; r < Q; ++r) rcv[r] = -rcv[r];
+                    if (corr) {
+                        double dsa[QM], dla[QM], u1[QM], u2[QM], cp[QM];
+                        for (int r = 0; r < Q; ++r) { dsa[r] = B[Ly.o_dsa + NLP + r]; dla[r] = B[Ly.o_dla + NLP + r]; }
+                        Soc<QM>::wmul(w, eta, dsa, u1, Q, true);
+                        Soc<QM>::wmul(w, eta, dla, u2, Q, false);
+                        Soc<QM>::jprod(u1, u2, cp, Q);
+                        for (int r = 0; r < Q; ++r) rcv[r] -= cp[r];
+                        rcv[0] += sgmu;
+                    }
+                    Soc<QM>::jdiv(lt, rcv, rho, Q);
+                    Soc<QM>::wmul(w, eta, rho, tv, Q, true);
+                    Soc<QM>::wmul(w, eta, rc, tmp, Q, true);
+                    Soc<QM>::wmul(w, eta, tmp, tmp, Q, true);
+                    for (int r = 0; r < Q; ++r) {
+                        tv[r] += tmp[r];
+                        B[Ly.o_rho + NLP + r] = rho[r];
+                        B[Ly.o_t + NLP + r] = tv[r];
+                        const double* ar = rowp(B, RH + NS + r);
+                        for (int i = 0; i < NZ; ++i) f[i] += ar[i] * tv[r];
+                    }
+                }
+                for (int i = 0; i < NZ; ++i) B[Ly.o_f + i] = pinned(t, i) ? 0.0 : f[i];
+            }
+            __syncthreads();
+            lqsolve();
+            // recover slack steps, step length
+            double amax = INFINITY;
+            for (int t = lane; t < K; t += WAVE) {
+                double* B = nb(t);
+                const int nh = (int)B[Ly.o_nh];
+                double dz[NZ];
+                for (int i = 0; i < NZ; ++i) dz[i] = B[Ly.o_dz + i];
+                auto lpstep = [&](int r, double gdz) {
+                    const double wl = B[Ly.o_wl + r];
+                    const double rc = B[Ly.o_rc + r];
+                    const double ds = -rc - gdz;
+                    const double dl = B[Ly.o_rho + r] / wl + (rc + gdz) / (wl * wl);
+                    B[Ly.o_ds + r] = ds; B[Ly.o_dl + r] = dl;
+                    if (ds < 0.0) amax = fmin(amax, -B[Ly.o_s + r] / ds);
+                    if (dl < 0.0) amax = fmin(amax, -B[Ly.o_lam + r] / dl);
+                };
+                for (int r = 0; r < nh; ++r) lpstep(r, dot(rowp(B, r), dz));
+                for (int r = 0; r < NS; ++r) {
+                    const double* ar = rowp(B, RH + r);
+                    const double wl1 = B[Ly.o_wl + RH + 2 * r], wl2 = B[Ly.o_wl + RH + 2 * r + 1];
+                    const double d1 = 1.0 / (wl1 * wl1), d2 = 1.0 / (wl2 * wl2);
+                    const double adz = dot(ar, dz);
+                    const double dsg = (B[Ly.o_rhs + r] + d1 * adz) / (d1 + d2);
+                    B[Ly.o_dsig + r] = dsg;
+                    lpstep(RH + 2 * r, adz - dsg);
+                    lpstep(RH + 2 * r + 1, -dsg);
+                }
+                if (Q > 0) {
+                    double w[QM], gdz[QM], rc[QM], rho[QM], ds[QM], dl[QM], tmp[QM], sv[QM], lv[QM];
+                    for (int r = 0; r < Q; ++r) {
+                        w[r] = B[Ly.o_sw + r];
+                        gdz[r] = dot(rowp(B, RH + NS + r), dz);
+                        rc[r] = B[Ly.o_rc + NLP + r];
+                        rho[r] = B[Ly.o_rho + NLP + r];
+                        sv[r] = B[Ly.o_s + NLP + r];
+                        lv[r] = B[Ly.o_lam + NLP + r];
+                    }
+                    const double eta = B[Ly.o_sw + Q];
+                    for (int r = 0; r < Q; ++r) { ds[r] = -rc[r] - gdz[r]; tmp[r] = rc[r] + gdz[r]; }
+                    Soc<QM>::wmul(w, eta, tmp, tmp, Q, true);
+                    Soc<QM>::wmul(w, eta, tmp, tmp, Q, true);
+                    Soc<QM>::wmul(w, eta, rho, dl, Q, true);
+                    for (int r = 0; r < Q; ++r) {
+                        dl[r] += tmp[r];
+                        B[Ly.o_ds + NLP + r] = ds[r];
+                        B[Ly.o_dl + NLP + r] = dl[r];
+                    }
+                    amax = fmin(amax, fmin(Soc<QM>::step(sv, ds, Q), Soc<QM>::step(lv, dl, Q)));
+                }
+            }
+            return wave_min(amax);
+        };
+
+        const double aa = fmin(1.0, direction(false, 0.0));
+        double mual = 0.0;
+        for (int t = lane; t < K; t += WAVE) {
+            double* B = nb(t);
+            const int nh = (int)B[Ly.o_nh];
+            for (int r = 0; r < RL; ++r) {
+                if (r >= nh && r < RH) continue;
+                const double ds = B[Ly.o_ds + r], dl = B[Ly.o_dl + r];
+                mual += (B[Ly.o_s + r] + aa * ds) * (B[Ly.o_lam + r] + aa * dl);
+            }
+            // Mehrotra corrector terms in scaled coordinates: LP (ds_a / wl) * (wl dl_a) = ds_a dl_a;
+            // SOC: keep ds_a, dl_a raw (scaled inside direction())
+            for (int r = 0; r < RL; ++r) {
+                B[Ly.o_dsa + r] = B[Ly.o_ds + r];
+                B[Ly.o_dla + r] = B[Ly.o_dl + r];
+            }
+        }
+        const double mu_a = wave_sum(mual) / deg;
+        const double sg = (mu_a / mu) * (mu_a / mu) * (mu_a / mu);
+        __syncthreads();
+        const double al = fmin(1.0, 0.99 * direction(true, sg * mu));
+        // ---- breakdown guard: a non-finite direction (Riccati overflow in the end-game) ends the
+        // solve on the current, finite iterate instead of corrupting it
+        double badl = (al > 0.0) ? 0.0 : 1.0;
+        for (int t = lane; t < K; t += WAVE) {
+            const double* B = nb(t);
+            const int nh = (int)B[Ly.o_nh];
+            double acc = 0.0;
+            for (int i = 0; i < NZ; ++i) acc += B[Ly.o_dz + i];
+            for (int r = 0; r < NS; ++r) acc += B[Ly.o_dsig + r];
+            for (int r = 0; r < RL; ++r) {
+                if (r >= nh && r < RH) continue;
+                acc += B[Ly.o_ds + r] + B[Ly.o_dl + r];
+            }
+            if (t < K - 1)
+                for (int i = 0; i < NXA; ++i) acc += B[Ly.o_yp + i];
+            if (!(fabs(acc) < INFINITY)) badl = 1.0;
+        }
+        for (int i = 0; i < NX; ++i)
+            if (!(fabs(sMisc[8 + i]) < INFINITY)) badl = 1.0;
+        if (wave_max(badl) > 0.0) { status = near_ok ? 1 : 2; break; }
+        // ---- update
+        for (int t = lane; t < K; t += WAVE) {
+            double* B = nb(t);
+            const int nh = (int)B[Ly.o_nh];
+            for (int i = 0; i < NZ; ++i) B[Ly.o_z + i] += al * B[Ly.o_dz + i];
+            for (int r = 0; r < NS; ++r) B[Ly.o_sig + r] += al * B[Ly.o_dsig + r];
+            for (int r = 0; r < RL; ++r) {
+                if (r >= nh && r < RH) continue;
+                B[Ly.o_s + r] += al * B[Ly.o_ds + r];
+                B[Ly.o_lam + r] += al * B[Ly.o_dl + r];
+            }
+            if (t < K - 1)
+                for (int i = 0; i < NXA; ++i) B[Ly.o_y + i] += al * (B[Ly.o_yp + i] - B[Ly.o_y + i]);
+        }
+        for (int i = 0; i < NX; ++i) y0[i] += al * (sMisc[8 + i] - y0[i]);
+        __syncthreads();
+    }
+
+    if (status == 1 && it == T.max_iter && !near_ok) status = 2;   // cap reached far from optimal
+    // ------------------------------------------------------------------ outputs
+    double sigv = nb(0)[Ly.o_z + SIG];
+    double numaxl = 0.0, softl = 0.0, admml = 0.0;
+    for (int t = lane; t < K; t += WAVE) {
+        double* B = nb(t);
+        double u[NU], x[NX];
+        for (int j = 0; j < NU; ++j) u[j] = B[Ly.o_z + ZU + j];
+        for (int i = 0; i < NX; ++i) {
+            double v = B[Ly.o_z + i];
+            for (int j = 0; j < NU; ++j) v += Cprev(t, i, j) * u[j];
+            x[i] = v;
+            a.X[(agent * K + t) * NX + i] = v;
+        }
+        for (int j = 0; j < NU; ++j) a.U[(agent * K + t) * NU + j] = u[j];
+        for (int o = 0; o < T.n_obs; ++o) {
+            const double sg = B[Ly.o_sig + o];
+            a.s_obs[(agent * T.n_obs + o) * K + t] = sg;
+            softl += T.w_slack * sg;
+        }
+        for (int j = 0; j < T.n_nbr; ++j) {
+            const double sg = B[Ly.o_sig + T.n_obs + j];
+            a.s_nbr[(agent * T.n_nbr + j) * K + t] = sg;
+            softl += T.w_coll * sg;
+            const long long base = ((agent * T.n_nbr + j) * K + t) * pd;
+            for (int i = 0; i < pd; ++i) {
+                const double df = x[i] - a.nbr_Y[base + i];
+                admml += a.nbr_Lam[base + i] * df + 0.5 * T.rho * df * df;
+            }
+        }
+        if (t < K - 1 && !(fin && t == K - 2)) {
+            double s1 = 0.0;
+            for (int i = 0; i < NX; ++i) {
+                const double v = B[Ly.o_z + ZN + i];
+                a.nu[(agent * (K - 1) + t) * NX + i] = v;
+                s1 += fabs(v);
+            }
+            numaxl = fmax(numaxl, s1);
+        }
+    }
+    __syncthreads();
+    // nu_{K-2} from the dynamics (x_{K-1} = x_final)
+    if (fin && K >= 2 && lane == 0) {
+        const int t = K - 2;
+        const double* dk = disc + (long long)t * DSTR;
+        const double* xk = a.X + (agent * K + t) * NX;
+        const double* uk = a.U + (agent * K + t) * NU;
+        const double* uk1 = a.U + (agent * K + t + 1) * NU;
+        double s1 = 0.0;
+        for (int i = 0; i < NX; ++i) {
+            double v = xfin[i] - dk[NX * NX + 2 * NX * NU + i] * sigv - dk[NX * NX + 2 * NX * NU + NX + i];
+            for (int l = 0; l < NX; ++l) v -= dk[l * NX + i] * xk[l];
+            for (int j = 0; j < NU; ++j) v -= dk[NX * NX + j * NX + i] * uk[j] + dk[NX * NX + NX * NU + j * NX + i] * uk1[j];
+            a.nu[(agent * (K - 1) + t) * NX + i] = v;
+            s1 += fabs(v);
+        }
+        numaxl = fmax(numaxl, s1);
+    }
+    const double numax = wave_max(numaxl), soft = wave_sum(softl), admm = wave_sum(admml);
+    if (lane == 0) {
+        a.sigma[agent] = sigv;
+        a.obj[agent] = T.w_nu * numax + soft + T.w_sigma * sigv + admm;
+        a.status[agent] = status;
+        a.iters[agent] = it;
+    }
+}
+
+}  // namespace
+}  // namespace scvx
+
+using namespace scvx;
+
+extern "C" size_t scvx_scp_workspace_bytes(const scvx_scp_template* T, int N) {
+    if (!T || N < 0) return 0;
+    const SCPLay L = scp_layout(*T);
+    return sizeof(double) * (size_t)N * (size_t)L.stride * (size_t)T->K;
+}
+
+extern "C" int scvx_scp_solve_batched(const scvx_scp_template* T, int N, const double* disc, const double* Xref,
+                                      const double* Uref, const double* sigma_ref, const double* tr,
+                                      const double* x_init, const double* x_final, const double* nbr_pos,
+                                      const double* nbr_Y, const double* nbr_Lam, double* X, double* U, double* nu,
+                                      double* sigma, double* s_obs, double* s_nbr, double* obj, int32_t* status,
+                                      int32_t* iters, void* workspace, size_t workspace_bytes, void* stream) {
+    if (!T || N < 0) return set_error(SCVX_EINVAL, "scp: null template");
+    if (N == 0) return SCVX_OK;
+    if (T->K < 3 || T->K > SCP_KMAX) return set_error(SCVX_EUNSUPPORTED, "scp: K must be in [3, 256]");
+    if (T->pos_dim < 1 || T->pos_dim > 3 || T->pos_dim > T->n_x) return set_error(SCVX_EINVAL, "scp: pos_dim");
+    if (T->n_ubound < 0 || T->n_ubound > SCVX_MAX_BOX || T->n_xbound < 0 || T->n_xbound > SCVX_MAX_BOX ||
+        T->n_obs < 0 || T->n_obs > SCVX_MAX_OBS || T->n_nbr < 0 || T->n_nbr > SCVX_MAX_NBR)
+        return set_error(SCVX_EINVAL, "scp: bound / obstacle / neighbour counts");
+    for (int b = 0; b < T->n_ubound; ++b)
+        if (T->ub_idx[b] < 0 || T->ub_idx[b] >= T->n_u) return set_error(SCVX_EINVAL, "scp: input bound index");
+    for (int b = 0; b < T->n_xbound; ++b)
+        if (T->xb_idx[b] < 0 || T->xb_idx[b] >= T->n_x) return set_error(SCVX_EINVAL, "scp: state bound index");
+    if (T->has_final && !T->pin_u_last) return set_error(SCVX_EUNSUPPORTED, "scp: has_final requires pin_u_last");
+    if (T->max_iter < 1) return set_error(SCVX_EINVAL, "scp: max_iter");
+    if (!disc || !Xref || !Uref || !sigma_ref || !tr || !x_init || !x_final || !X || !U || !nu || !sigma || !obj ||
+        !status || !iters || (T->n_obs && !s_obs) || (T->n_nbr && (!nbr_pos || !nbr_Y || !nbr_Lam || !s_nbr)))
+        return set_error(SCVX_EINVAL, "scp: null buffer");
+    const size_t need = scvx_scp_workspace_bytes(T, N);
+    if (!workspace || workspace_bytes < need) return set_error(SCVX_EWORKSPACE, "scp: workspace too small");
+    SCPArgs a{};
+    a.T = *T;
+    a.N = N;
+    a.disc = disc; a.Xref = Xref; a.Uref = Uref; a.sigma_ref = sigma_ref; a.tr = tr; a.x_init = x_init;
+    a.x_final = x_final; a.nbr_pos = nbr_pos; a.nbr_Y = nbr_Y; a.nbr_Lam = nbr_Lam;
+    a.X = X; a.U = U; a.nu = nu; a.sigma = sigma; a.s_obs = s_obs; a.s_nbr = s_nbr; a.obj = obj;
+    a.status = status; a.iters = iters;
+    a.ws = (double*)workspace;
+    a.ws_agent = (long long)scp_layout(*T).stride * T->K;
+    hipStream_t st = (hipStream_t)stream;
+    if (T->model_id == SCVX_MODEL_UNICYCLE && T->n_x == 3 && T->n_u == 2) {
+        if (T->has_soc) return set_error(SCVX_EUNSUPPORTED, "scp: SOC rows need n_u + 1 <= 4");
+        hipLaunchKernelGGL((scp_ipm_kernel<3, 2>), dim3(N), dim3(WAVE), 0, st, a);
+    } else if (T->model_id == SCVX_MODEL_SINGLE_INTEGRATOR && T->n_x == 3 && T->n_u == 3) {
+        hipLaunchKernelGGL((scp_ipm_kernel<3, 3>), dim3(N), dim3(WAVE), 0, st, a);
+    } else {
+        return set_error(SCVX_EUNSUPPORTED, "scp: model (unicycle n=3 m=2, single integrator n=3 m=3)");
+    }
+    return check_launch("scp_ipm_kernel");
+}

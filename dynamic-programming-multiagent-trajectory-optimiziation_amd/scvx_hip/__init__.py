@@ -9,20 +9,22 @@ kernels run on torch's current HIP stream, nothing falls back to the CPU.
     collision_rows         linearized pairwise collision rows (Distributed_opt/dist_scvx_3d.py:93-107)
     qp_solve_batched       the per-agent trust-region subproblem (dist_scvx_3d.py:51-111)
     QPSpec                 problem template of qp_solve_batched
+    SCPSpec / SCPSolver    the SCvx convex subproblem SCProblem (+ AgentSolver ADMM terms)
+                           (SCvx/optimization/sc_problem.py:15-83, agent_solver.py:78-102)
 """
 import ctypes
 from dataclasses import dataclass, field
 from typing import Optional, Sequence, Tuple
 
 from . import _lib
-from ._lib import MODEL_DIMS, MODEL_IDS, STATUS, QPTemplate, ScvxError, check, lib
+from ._lib import MODEL_DIMS, MODEL_IDS, STATUS, QPTemplate, SCPTemplate, ScvxError, check, lib
 
 # RK4 substeps per FOH interval.  1 is exact for the (linear) integrators; 16 keeps the
 # unicycle / quadrotor within 1e-7 of the reference's LSODA (tests/test_foh_oracle.py).
 DEFAULT_NSUB = {"di": 1, "si": 1, "unicycle": 16, "quad": 16}
 QUAD_PARAMS = (1.0, 9.81, 0.02, 0.02, 0.04)
 
-__all__ = ["foh_batched", "integrate_nonlinear", "collision_rows", "qp_solve_batched", "QPSpec",
+__all__ = ["foh_batched", "integrate_nonlinear", "collision_rows", "qp_solve_batched", "QPSpec", "SCPSpec", "SCPSolver",
            "disc_stride", "unpack_disc", "ScvxError", "MODEL_DIMS", "DEFAULT_NSUB"]
 
 
@@ -202,3 +204,103 @@ def qp_solve_batched(spec: QPSpec, disc, sigma, Xref, Uref, x_init, x_final, tr,
     s = QPSolver(spec, Xref.shape[0], device=Xref.device)
     out = s.solve(disc, sigma, Xref, Uref, x_init, x_final, tr, coll_rows, coll_count)
     return {k: v.clone() for k, v in out.items()}
+
+
+@dataclass
+class SCPSpec:
+    """Template of the batched SCProblem solve (include/scvx_hip.h scvx_scp_template).  The
+    constraint data come from the model (SCvx/models/*.scp_constraints())."""
+    model: str = "unicycle"
+    K: int = 100
+    pos_dim: int = 2
+    has_final: bool = True
+    pin_u_first: bool = True
+    pin_u_last: bool = True
+    u_bounds: Sequence[Tuple[int, Optional[float], Optional[float]]] = ()
+    u_soc: Optional[float] = None
+    x_bounds: Sequence[Tuple[int, float, float]] = ()
+    obs: Sequence[Tuple[Sequence[float], float]] = ()   # (center, total clearance r_o)
+    w_nu: float = 1e4
+    w_slack: float = 1e6
+    w_sigma: float = 100.0
+    n_nbr: int = 0
+    rho: float = 0.0
+    d_min: float = 1.0
+    w_coll: float = 1e5
+    max_iter: int = 100
+    tol: float = 1e-9
+    reg: float = 1e-10
+
+    def to_c(self):
+        n, m = MODEL_DIMS[self.model]
+        t = SCPTemplate()
+        t.model_id, t.n_x, t.n_u, t.K, t.pos_dim = MODEL_IDS[self.model], n, m, int(self.K), int(self.pos_dim)
+        t.has_final, t.pin_u_first, t.pin_u_last = int(self.has_final), int(self.pin_u_first), int(self.pin_u_last)
+        if len(self.u_bounds) > _lib.SCVX_MAX_BOX or len(self.x_bounds) > _lib.SCVX_MAX_BOX:
+            raise ValueError("too many bound constraints")
+        if len(self.obs) > _lib.SCVX_MAX_OBS or self.n_nbr > _lib.SCVX_MAX_NBR:
+            raise ValueError("too many obstacles / neighbours")
+        t.n_ubound = len(self.u_bounds)
+        for b, (j, lo, hi) in enumerate(self.u_bounds):
+            t.ub_idx[b] = int(j)
+            t.ub_has_lo[b], t.ub_has_hi[b] = int(lo is not None), int(hi is not None)
+            t.ub_lo[b] = 0.0 if lo is None else float(lo)
+            t.ub_hi[b] = 0.0 if hi is None else float(hi)
+        t.has_soc = int(self.u_soc is not None)
+        t.u_max = 0.0 if self.u_soc is None else float(self.u_soc)
+        t.n_xbound = len(self.x_bounds)
+        for b, (i, lo, hi) in enumerate(self.x_bounds):
+            t.xb_idx[b], t.xb_lo[b], t.xb_hi[b] = int(i), float(lo), float(hi)
+        t.n_obs = len(self.obs)
+        for o, (c, r) in enumerate(self.obs):
+            for i in range(len(c)):
+                t.obs_center[o][i] = float(c[i])
+            t.obs_radius[o] = float(r)
+        t.w_nu, t.w_slack, t.w_sigma = float(self.w_nu), float(self.w_slack), float(self.w_sigma)
+        t.n_nbr, t.rho, t.d_min, t.w_coll = int(self.n_nbr), float(self.rho), float(self.d_min), float(self.w_coll)
+        t.max_iter, t.tol, t.reg = int(self.max_iter), float(self.tol), float(self.reg)
+        return t
+
+
+class SCPSolver:
+    """Reusable batched SCProblem solver (scvx_scp_solve_batched): C template, device workspace and
+    output buffers for N agents."""
+
+    def __init__(self, spec: SCPSpec, N: int, device="cuda"):
+        torch = _torch()
+        self.spec, self.N = spec, N
+        self.ctpl = spec.to_c()
+        nbytes = lib().scvx_scp_workspace_bytes(ctypes.byref(self.ctpl), N)
+        self.workspace = torch.empty(max(nbytes // 8, 1), dtype=torch.float64, device=device)
+        n, m = MODEL_DIMS[spec.model]
+        K, f64 = spec.K, torch.float64
+        self.X = torch.empty((N, K, n), dtype=f64, device=device)
+        self.U = torch.empty((N, K, m), dtype=f64, device=device)
+        self.nu = torch.empty((N, K - 1, n), dtype=f64, device=device)
+        self.sigma = torch.empty(N, dtype=f64, device=device)
+        self.s_obs = torch.empty((N, max(len(spec.obs), 1), K), dtype=f64, device=device)
+        self.s_nbr = torch.empty((N, max(spec.n_nbr, 1), K), dtype=f64, device=device)
+        self.obj = torch.empty(N, dtype=f64, device=device)
+        self.status = torch.empty(N, dtype=torch.int32, device=device)
+        self.iters = torch.empty(N, dtype=torch.int32, device=device)
+        self._dummy = torch.zeros(1, dtype=f64, device=device)
+
+    def solve(self, disc, Xref, Uref, sigma_ref, tr, x_init, x_final, nbr_pos=None, nbr_Y=None, nbr_Lam=None,
+              stream=None):
+        """disc (N,K-1,n(n+2m+2)), Xref (N,K,n), Uref (N,K,m), sigma_ref (N,), tr (N,), x_init/x_final (N,n);
+        nbr_* (N,n_nbr,K,pos_dim) when spec.n_nbr > 0.  Returns dict of device tensors (reused buffers)."""
+        if self.spec.n_nbr > 0 and (nbr_pos is None or nbr_Y is None or nbr_Lam is None):
+            raise ValueError("ADMM terms need nbr_pos, nbr_Y and nbr_Lam")
+        d = self._dummy
+        rc = lib().scvx_scp_solve_batched(
+            ctypes.byref(self.ctpl), self.N, _dev(disc, name="disc"), _dev(Xref, name="Xref"), _dev(Uref, name="Uref"),
+            _dev(sigma_ref, name="sigma_ref"), _dev(tr, name="tr"), _dev(x_init, name="x_init"),
+            _dev(x_final, name="x_final"), _dev(nbr_pos if nbr_pos is not None else d, name="nbr_pos"),
+            _dev(nbr_Y if nbr_Y is not None else d, name="nbr_Y"),
+            _dev(nbr_Lam if nbr_Lam is not None else d, name="nbr_Lam"), _dev(self.X), _dev(self.U), _dev(self.nu),
+            _dev(self.sigma), _dev(self.s_obs), _dev(self.s_nbr), _dev(self.obj), _dev(self.status, _torch().int32),
+            _dev(self.iters, _torch().int32), _dev(self.workspace), ctypes.c_size_t(self.workspace.numel() * 8),
+            _stream(stream))
+        check(rc, "scvx_scp_solve_batched")
+        return dict(X=self.X, U=self.U, nu=self.nu, sigma=self.sigma, s_obs=self.s_obs[:, :len(self.spec.obs)],
+                    s_nbr=self.s_nbr[:, :self.spec.n_nbr], obj=self.obj, status=self.status, iters=self.iters)

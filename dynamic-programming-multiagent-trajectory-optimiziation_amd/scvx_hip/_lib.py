@@ -9,7 +9,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SCVX_HIP_LIB") or os.path.join(HERE, "libscvx_hip.so")  # override: diagnostics builds
 
-SCVX_MAX_BOX, SCVX_MAX_OBS = 4, 16
+SCVX_MAX_BOX, SCVX_MAX_OBS, SCVX_MAX_NBR = 4, 16, 32
 MODEL_IDS = {"di": 0, "unicycle": 1, "si": 2, "quad": 3}
 MODEL_DIMS = {"di": (6, 3), "unicycle": (3, 2), "si": (3, 3), "quad": (12, 4)}
 STATUS = {0: "optimal", 1: "optimal_inaccurate", 2: "solver_error"}
@@ -17,7 +17,7 @@ STATUS = {0: "optimal", 1: "optimal_inaccurate", 2: "solver_error"}
 # every symbol declared in include/scvx_hip.h
 EXPORTS = ("scvx_version", "scvx_last_error", "scvx_foh_batched", "scvx_integrate_nonlinear_batched",
            "scvx_qp_solve_batched", "scvx_qp_workspace_bytes", "scvx_qp_set_trace",
-           "scvx_collision_rows_batched")
+           "scvx_collision_rows_batched", "scvx_scp_solve_batched", "scvx_scp_workspace_bytes")
 
 
 class ScvxError(RuntimeError):
@@ -36,6 +36,24 @@ class QPTemplate(ctypes.Structure):
         ("w_obs", ctypes.c_double), ("j_max", ctypes.c_int32), ("w_coll", ctypes.c_double),
         ("has_soc", ctypes.c_int32), ("u_max", ctypes.c_double), ("max_iter", ctypes.c_int32),
         ("tol", ctypes.c_double),
+    ]
+
+
+class SCPTemplate(ctypes.Structure):
+    """Mirror of scvx_scp_template (include/scvx_hip.h)."""
+    _fields_ = [
+        ("model_id", ctypes.c_int32), ("n_x", ctypes.c_int32), ("n_u", ctypes.c_int32), ("K", ctypes.c_int32),
+        ("pos_dim", ctypes.c_int32), ("has_final", ctypes.c_int32), ("pin_u_first", ctypes.c_int32),
+        ("pin_u_last", ctypes.c_int32), ("n_ubound", ctypes.c_int32), ("ub_idx", ctypes.c_int32 * SCVX_MAX_BOX),
+        ("ub_has_lo", ctypes.c_int32 * SCVX_MAX_BOX), ("ub_has_hi", ctypes.c_int32 * SCVX_MAX_BOX),
+        ("ub_lo", ctypes.c_double * SCVX_MAX_BOX), ("ub_hi", ctypes.c_double * SCVX_MAX_BOX),
+        ("has_soc", ctypes.c_int32), ("u_max", ctypes.c_double), ("n_xbound", ctypes.c_int32),
+        ("xb_idx", ctypes.c_int32 * SCVX_MAX_BOX), ("xb_lo", ctypes.c_double * SCVX_MAX_BOX),
+        ("xb_hi", ctypes.c_double * SCVX_MAX_BOX), ("n_obs", ctypes.c_int32),
+        ("obs_center", (ctypes.c_double * 3) * SCVX_MAX_OBS), ("obs_radius", ctypes.c_double * SCVX_MAX_OBS),
+        ("w_nu", ctypes.c_double), ("w_slack", ctypes.c_double), ("w_sigma", ctypes.c_double),
+        ("n_nbr", ctypes.c_int32), ("rho", ctypes.c_double), ("d_min", ctypes.c_double), ("w_coll", ctypes.c_double),
+        ("max_iter", ctypes.c_int32), ("tol", ctypes.c_double), ("reg", ctypes.c_double),
     ]
 
 
@@ -60,8 +78,12 @@ def lib():
         L.scvx_qp_solve_batched.argtypes = [ctypes.POINTER(QPTemplate), i32] + [vp] * 15 + [vp, sz, vp]
         L.scvx_qp_set_trace.argtypes = [vp, i32, i32]
         L.scvx_collision_rows_batched.argtypes = [i32, i32, i32, i32, vp, i32, i32, dbl, dbl, vp, vp, vp]
+        L.scvx_scp_workspace_bytes.argtypes = [ctypes.POINTER(SCPTemplate), i32]
+        L.scvx_scp_workspace_bytes.restype = sz
+        L.scvx_scp_solve_batched.argtypes = [ctypes.POINTER(SCPTemplate), i32] + [vp] * 19 + [vp, sz, vp]
+        sized = ("scvx_last_error", "scvx_qp_workspace_bytes", "scvx_scp_workspace_bytes")
         for fn in EXPORTS:
-            getattr(L, fn).restype = getattr(L, fn).restype if fn in ("scvx_last_error", "scvx_qp_workspace_bytes") else i32
+            getattr(L, fn).restype = getattr(L, fn).restype if fn in sized else i32
         _lib = L
     return _lib
 

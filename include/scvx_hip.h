@@ -150,6 +150,74 @@ int scvx_collision_rows_batched(int K, int pos_dim, int n_x, int N_total, const 
                                 int N_local, double R, double cull_radius, int j_max, double* rows,
                                 int32_t* count, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Batched SCvx convex subproblem: the reference's SCProblem (SCvx/optimization/sc_problem.py:15-83)
+ * with the constraints of its models (unicycle_model.py:88-114, single_integrator_model.py:80-126)
+ * and, when n_nbr > 0, the ADMM terms of AgentSolver (agent_solver.py:78-102, si_agent_solver.py:70-92):
+ *
+ *   min  w_nu ||nu||_{1,ind} + w_slack sum_{o,k} s'_{o,k} + w_sigma sigma
+ *        + sum_j [ sum Lam_j o (p - Y_j) + rho/2 ||p - Y_j||_F^2 + w_coll sum_k S_{j,k} ]
+ *   s.t. x_{k+1} = A_k x_k + B_k u_k + C_k u_{k+1} + S_k sigma + z_k + nu_k      (:53-68)
+ *        ||X - Xref||_{1,ind} + ||U - Uref||_{1,ind} + |sigma - sigma_ref| <= tr    (:71-74)
+ *        sigma >= 0; x_0 = x_init; x_{K-1} = x_final (has_final); u_0 = 0 (pin_u_first);
+ *        u_{K-1} = 0 (pin_u_last); ub_lo <= u_k[ub_idx] <= ub_hi; xb_lo <= x_k[xb_idx] <= xb_hi;
+ *        ||u_k||_2 <= u_max (has_soc); a_{o,k}'(p_k - c_o) >= r_o - s'_{o,k}, s' >= 0 with
+ *        a_{o,k} = (pbar_k - c_o)/(||pbar_k - c_o|| + 1e-6);  a_{j,k}'(p_k - Y_{j,k}) + S_{j,k} >= d_min,
+ *        S >= 0 with a_{j,k} = (pbar_k - P_{j,k})/(||pbar_k - P_{j,k}|| + 1e-6) (multi_agent_model.py:61-79),
+ * p_k = x_k[0:pos_dim], ||M||_{1,ind} = max_k ||M[:,k]||_1 (the induced norm cvx.norm(M, 1) computes).
+ * Solved by a primal-dual interior-point method (Mehrotra, Nesterov-Todd SOC scaling) whose Newton
+ * systems go through a Riccati recursion with (sigma, tau_x, tau_u, tau_nu) as augmented states.
+ * Supported models: unicycle (n=3, m=2), single integrator (n=3, m=3).  K <= 256.
+ * ------------------------------------------------------------------------------------------ */
+#define SCVX_MAX_NBR 32
+
+typedef struct scvx_scp_template {
+    int32_t model_id;
+    int32_t n_x, n_u, K;
+    int32_t pos_dim;
+    int32_t has_final;      /* X[:,-1] == x_final (requires pin_u_last) */
+    int32_t pin_u_first;    /* U[:,0] == 0  */
+    int32_t pin_u_last;     /* U[:,-1] == 0 */
+    int32_t n_ubound;
+    int32_t ub_idx[SCVX_MAX_BOX];
+    int32_t ub_has_lo[SCVX_MAX_BOX];
+    int32_t ub_has_hi[SCVX_MAX_BOX];
+    double ub_lo[SCVX_MAX_BOX];
+    double ub_hi[SCVX_MAX_BOX];
+    int32_t has_soc;
+    double u_max;
+    int32_t n_xbound;
+    int32_t xb_idx[SCVX_MAX_BOX];
+    double xb_lo[SCVX_MAX_BOX];
+    double xb_hi[SCVX_MAX_BOX];
+    int32_t n_obs;
+    double obs_center[SCVX_MAX_OBS][3];
+    double obs_radius[SCVX_MAX_OBS];   /* total clearance r_o (obstacle + robot radius [+ margin]) */
+    double w_nu, w_slack, w_sigma;
+    int32_t n_nbr;
+    double rho, d_min, w_coll;
+    int32_t max_iter;
+    double tol;
+    double reg;             /* primal regularisation of the Newton systems (scaled units), e.g. 1e-10 */
+} scvx_scp_template;
+
+/*
+ * Inputs (device, agent-major): disc [N][K-1][n(n+2m+2)], Xref [N][K][n], Uref [N][K][m],
+ *   sigma_ref [N], tr [N], x_init [N][n], x_final [N][n],
+ *   nbr_pos / nbr_Y / nbr_Lam [N][n_nbr][K][pos_dim]  (neighbour reference positions X_ref_j[0:pd],
+ *   consensus Y_j, duals Lambda_j; ignored when n_nbr = 0).
+ * Outputs (device): X [N][K][n], U [N][K][m], nu [N][K-1][n], sigma [N], s_obs [N][n_obs][K],
+ *   s_nbr [N][n_nbr][K], obj [N] (the reference objective at the solution), status [N], iters [N].
+ */
+int scvx_scp_solve_batched(const scvx_scp_template* tpl, int N, const double* disc, const double* Xref,
+                           const double* Uref, const double* sigma_ref, const double* tr, const double* x_init,
+                           const double* x_final, const double* nbr_pos, const double* nbr_Y, const double* nbr_Lam,
+                           double* X, double* U, double* nu, double* sigma, double* s_obs, double* s_nbr, double* obj,
+                           int32_t* status, int32_t* iters, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Bytes of caller-owned device scratch scvx_scp_solve_batched needs for N agents. */
+size_t scvx_scp_workspace_bytes(const scvx_scp_template* tpl, int N);
+
 #ifdef __cplusplus
 }
 #endif

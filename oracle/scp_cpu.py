@@ -21,6 +21,7 @@ Newton systems are solved by a Riccati recursion over the nodes (state n+4, inpu
 import itertools
 
 import numpy as np
+from scipy.linalg import solve_triangular
 
 NG = 4  # sigma, tau_x, tau_u, tau_nu
 
@@ -77,6 +78,8 @@ def build_nodes(p):
                 a = row([(L.TN, -1.0)]); a[L.N] = s
                 hard.append((a, 0.0))
         for (j, lo, hi) in p.get("u_bounds") or []:
+            if k == 0 or k == K - 1:                   # pinned inputs: constant rows dropped (kernel too)
+                continue
             if hi is not None:
                 hard.append((row([(L.U[j], 1.0)]), hi))
             if lo is not None:
@@ -172,9 +175,11 @@ def ldl_solve(M, b, rel=1e-13):
         d[j] = dj
         for i in range(j + 1, nn):
             Lm[i, j] = (A[i, j] - (Lm[i, :j] * Lm[j, :j]) @ d[:j]) / dj
-    y = np.linalg.solve(Lm, b)
+    if not np.isfinite(Lm).all():          # the kernel propagates the non-finite values to its guard
+        return np.full(np.shape(b), np.nan)
+    y = solve_triangular(Lm, b, lower=True, unit_diagonal=True, check_finite=False)
     y = (y.T / d).T
-    return np.linalg.solve(Lm.T, y)
+    return solve_triangular(Lm.T, y, lower=False, unit_diagonal=True, check_finite=False)
 
 
 # ---- cone helpers (per node: LP part then SOC blocks)
@@ -232,7 +237,7 @@ def _soc_step(x, dx):
 class SCPSolver:
     """Structured Mehrotra predictor-corrector IPM with Riccati KKT solves (the kernel's algorithm)."""
 
-    def __init__(self, p, tol=1e-9, max_iter=100, reg=1e-8):
+    def __init__(self, p, tol=1e-9, max_iter=100, reg=1e-10):
         self.p, self.tol, self.max_iter, self.reg = p, tol, max_iter, reg
         self.nodes, self.L = build_nodes(p)
         self.K = len(self.nodes)
@@ -290,7 +295,7 @@ class SCPSolver:
         qmax = max(max(np.abs(nd["q"]).max() for nd in nodes), max((w for nd in nodes for _, _, w in nd["soft"]),
                                                                      default=0.0))
         pscale, dscale = 1.0 + hmax, 1.0 + qmax
-        status, it = "max_iter", 0
+        status, it, near_ok = "max_iter", 0, False
         self.trace = []
         for it in range(self.max_iter):
             # residuals
@@ -329,6 +334,9 @@ class SCPSolver:
             if pres < self.tol * pscale and dres < self.tol * dscale and gap < self.tol * max(1.0, abs(pobj)):
                 status = "optimal"
                 break
+            # reduced (ECOS-style "inaccurate") tolerances, used if the solve ends early (kernel: near_ok)
+            tol_i = max(1e-6, 1e3 * self.tol)
+            near_ok = pres < tol_i * pscale and dres < tol_i * dscale and gap < tol_i * max(1.0, abs(pobj))
             # scaling
             Wn = [self._nt(nd, s[k], lam[k]) for k, nd in enumerate(nodes)]
             lt = [self._Wmul(nd, Wn[k], lam[k], 0) for k, nd in enumerate(nodes)]   # lambda~ = W lam
@@ -397,6 +405,12 @@ class SCPSolver:
             dz, dsg, ds, dl, yp, y0p = direction(rcomp)
             alpha = min(1.0, 0.99 * min(min(self._step(nd, s[k], ds[k]), self._step(nd, lam[k], dl[k]))
                                         for k, nd in enumerate(nodes)))
+            # breakdown guard (kernel: wave_max(badl)): stop on the current finite iterate
+            fin = np.isfinite(alpha) and alpha > 0 and np.isfinite(dz).all() and np.isfinite(yp).all() and \
+                np.isfinite(y0p).all() and all(np.isfinite(x).all() for x in dsg + ds + dl)
+            if not fin:
+                status = "inaccurate" if near_ok else "numerical"
+                break
             z = z + alpha * dz
             for k in range(K):
                 sig[k] = sig[k] + alpha * dsg[k]
@@ -404,6 +418,10 @@ class SCPSolver:
                 lam[k] = lam[k] + alpha * dl[k]
             y = y + alpha * (yp - y)
             y0 = y0 + alpha * (y0p - y0)
+        else:
+            it = self.max_iter
+            if not near_ok:
+                status = "numerical"
         self.z, self.sig, self.s, self.lam = z, sig, s, lam
         return self._outputs(status, it)
 

@@ -150,3 +150,74 @@ def test_first_order_hold_rejects_models_without_device_dynamics():
 
     with pytest.raises(ValueError):
         FirstOrderHold(Custom(), 10)
+
+
+# ---------------------------------------------------------------- SCProblem / AgentSolver host logic
+def test_scproblem_surface_and_errors():
+    """sc_problem.py:15-128 surface: var / par names and shapes, KeyError on unknown names,
+    parameter shape validation, and the template data the kernel receives."""
+    from SCvx.global_parameters import K
+    from SCvx.models.unicycle_model import UnicycleModel
+    from SCvx.optimization.sc_problem import SCProblem
+    from SCvx.optimization.variables import ParameterError
+    m = UnicycleModel()
+    scp = SCProblem(m)
+    assert set(scp.var) == {"X", "U", "nu", "sigma"}
+    assert scp.var["X"].shape == (3, K) and scp.var["nu"].shape == (3, K - 1) and scp.var["sigma"].shape == ()
+    assert set(scp.par) == {"A_bar", "B_bar", "C_bar", "S_bar", "z_bar", "X_ref", "U_ref", "sigma_ref", "weight_nu",
+                            "weight_sigma", "tr_radius", "weight_slack"}
+    assert scp.par["A_bar"].shape == (9, K - 1) and scp.par["B_bar"].shape == (6, K - 1)
+    with pytest.raises(KeyError):
+        scp.set_parameters(bogus=1.0)
+    with pytest.raises(KeyError):
+        scp.get_variable("Y")
+    with pytest.raises(ValueError):
+        scp.set_parameters(X_ref=np.zeros((2, K)))
+    with pytest.raises(ValueError):
+        scp.set_parameters(sigma_ref=-1.0)
+    assert scp.get_variable("X") is None
+    with pytest.raises(ParameterError):
+        scp.spec()
+    scp.set_parameters(weight_nu=1e4, weight_slack=1e6, weight_sigma=100.0)
+    t = scp.spec().to_c()
+    assert (t.n_x, t.n_u, t.K, t.pos_dim, t.n_obs, t.n_ubound, t.n_xbound) == (3, 2, K, 2, 3, 2, 2)
+    assert t.obs_radius[0] == pytest.approx(3.5) and t.xb_lo[0] == pytest.approx(-9.5)
+    assert (t.has_final, t.pin_u_first, t.pin_u_last, t.has_soc) == (1, 1, 1, 0)
+
+
+def test_si_scproblem_template_has_soc():
+    from SCvx.models.single_integrator_model import SingleIntegratorModel
+    from SCvx.optimization.sc_problem import SCProblem
+    scp = SCProblem(SingleIntegratorModel())
+    scp.set_parameters(weight_nu=1e4, weight_slack=1e6, weight_sigma=100.0)
+    t = scp.spec().to_c()
+    assert (t.n_u, t.pos_dim, t.has_soc, t.n_obs, t.n_xbound) == (3, 3, 1, 2, 3)
+    assert t.u_max == pytest.approx(1.0)
+
+
+def test_agent_solver_surface():
+    """agent_solver.py:10-41 / si_agent_solver.py:16-37: Y / Lambda / S per neighbour."""
+    from SCvx.global_parameters import K
+    from SCvx.models.SI_multi_agent_model import SI_MultiAgentModel
+    from SCvx.models.multi_agent_model import MultiAgentModel
+    from SCvx.optimization.agent_solver import AgentSolver
+    from SCvx.optimization.si_agent_solver import SI_AgentSolver
+    mam = MultiAgentModel([{"r_init": np.zeros(3), "r_final": np.ones(3)}] * 3, d_min=1.0)
+    s = AgentSolver(1, mam, rho_admm=1.0)
+    assert sorted(s.Y) == [0, 2] and s.Y[0].shape == (2, K) and s.S[2].shape == (K, 1)
+    sim = SI_MultiAgentModel([{"r_init": np.zeros(3), "r_final": np.ones(3)}] * 2, d_min=1.0)
+    s3 = SI_AgentSolver(0, sim, rho_admm=1.0)
+    assert list(s3.Y) == [1] and s3.Lambda[1].shape == (3, K)
+    with pytest.raises(RuntimeError):
+        s3.solve()
+
+
+def test_multi_agent_logging_format(capsys):
+    from SCvx.utils.multi_agent_logging import print_iteration, print_summary
+    print_iteration(3, 0.0, 0.0, 1.5, 0.25, 0.0, 0.0, 1.0, 1.0)
+    print_summary(4, 1.0, runtime=2.5)
+    out = capsys.readouterr().out
+    assert out.startswith("Iter  3 | v=0.000e+00 | slack=0.000e+00 | p_res=1.500e+00 | d_res=2.500e-01 "
+                          "| Δx=0.00e+00 | Δs=0.00e+00 | o= 1.000 | tr= 1.000\n")
+    assert "\n=== SCvx+ADMM Summary ===\n  Total iterations: 4\n  Final time scale o: 1.000\n" in out
+    assert "  Total runtime:    2.50s\n=========================\n" in out
