@@ -15,9 +15,20 @@ collective); `value` counts the N_gpus * 1024-agent SCvx iterations completed pe
 Also reported: roofline of the dominant kernel (qp_ipm_kernel, FP64 FLOP rate vs the FP64 peak,
 timed with HIP events on the launch stream) and a CPU baseline (the C++ restatement of the same
 algorithm, oracle/scvx_cpu.cpp + oracle/foh_ref.c, on a bounded agent sample).
+
+Optional workloads (--config; the default c3 is the headline line the driver records):
+  c4  N=4096 double-integrator agents in total on a 16^3 lattice (spacing 6 > 2R, R=2.3) with
+      permuted goals, pairwise collision coupling (dist_scvx_3d.py:93-107, one shared slack per node,
+      the j_max=8 nearest neighbours per node kept), global trust-region rule (:248-252).  Agents
+      are sharded contiguously over ranks; one RCCL all_gather of the states per iteration feeds the
+      collision linearization (strong scaling: the 4096-agent problem is fixed).
+  c5  N=1024 12-state quadrotors (models.hpp) from hover, 8 obstacles, coupling as c4 with R=0.5
+      (strong scaling).
 """
 import argparse
 import json
+
+import numpy as np
 import os
 import sys
 import time
@@ -62,10 +73,30 @@ def committed_traffic(kernel_prefix="scvx::qp_ipm_kernel<scvx::QPCfg<6, 3, 2, 8,
 
 def make_workload(N, seed, device):
     import torch
-    from oracle import problems as pb
-    sc = pb.synthetic_di(N, K=K, seed=seed, sigma=SIGMA, obstacles=N_OBS)
+    from scvx_hip import workloads
+    sc = workloads.synthetic_di(N, K=K, seed=seed, sigma=SIGMA, obstacles=N_OBS)
     t = {k: torch.tensor(sc[k], device=device) for k in ("X", "U", "x_init", "x_final", "sigma")}
     return sc, t
+
+
+def make_coupled(config, world, rank, device):
+    """c4 / c5: the full problem is built identically on every rank, each rank keeps its block."""
+    import torch
+    from scvx_hip import workloads
+    if config == "c4":
+        sc = workloads.synthetic_lattice(side=16, K=K, seed=2, sigma=SIGMA)
+        model, R, obs, box, j_max = "di", 2.3, [], [(0, -50.0, 50.0), (1, -50.0, 50.0)], 8   # lattice spans +-45
+    else:
+        sc = workloads.synthetic_quad(1024, K=K, seed=3, sigma=SIGMA, obstacles=N_OBS)
+        model, R, obs, box, j_max = "quad", 0.5, sc["obs"], BOX, 8
+    N_total = sc["X"].shape[0]
+    if N_total % world:
+        raise SystemExit(f"{config}: {N_total} agents do not shard over {world} ranks")
+    n_loc = N_total // world
+    sl = slice(rank * n_loc, (rank + 1) * n_loc)
+    t = {k: torch.tensor(np.ascontiguousarray(sc[k][sl]), device=device)
+         for k in ("X", "U", "x_init", "x_final", "sigma")}
+    return sc, t, dict(model=model, R=R, obs=obs, box=box, j_max=j_max, N_total=N_total, n_loc=n_loc)
 
 
 def cpu_baseline(sc, n_sample, threads, min_seconds=10.0):
@@ -99,7 +130,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--agents", type=int, default=N_AGENTS)
+    ap.add_argument("--config", choices=("c3", "c4", "c5"), default="c3")
+    ap.add_argument("--agents", type=int, default=N_AGENTS, help="c3: agents per GPU")
     ap.add_argument("--cpu-sample", type=int, default=1024)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -107,7 +139,7 @@ def main():
     import torch
     import torch.distributed as dist
     import scvx_hip
-    from scvx_hip.scvx import JacobiSCvx
+    from scvx_hip.scvx import CouplingSpec, JacobiSCvx
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -116,10 +148,23 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
-    N = args.agents
-    sc, w = make_workload(N, seed=1 + rank, device=device)
-    spec = scvx_hip.QPSpec(model="di", K=K, box=BOX, obs=sc["obs"], w_obs=1e6, u_max=U_MAX, tol=1e-9, max_iter=60)
-    drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, tr_rule="per_agent")
+    if args.config == "c3":
+        N = args.agents
+        sc, w = make_workload(N, seed=1 + rank, device=device)
+        model, box, j_max, n, m = "di", BOX, 0, 6, 3
+        spec = scvx_hip.QPSpec(model="di", K=K, box=BOX, obs=sc["obs"], w_obs=1e6, u_max=U_MAX, tol=1e-9,
+                               max_iter=60)
+        drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, tr_rule="per_agent")
+        n_obs = N_OBS
+    else:
+        sc, w, cfg = make_coupled(args.config, world, rank, device)
+        N, model, box, j_max = cfg["n_loc"], cfg["model"], cfg["box"], cfg["j_max"]
+        n, m = scvx_hip.MODEL_DIMS[model]
+        n_obs = len(cfg["obs"])
+        spec = scvx_hip.QPSpec(model=model, K=K, box=box, obs=cfg["obs"], w_obs=1e6, j_max=j_max, w_coll=1e4,
+                               tol=1e-9, max_iter=60)
+        drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, coupling=CouplingSpec(R=cfg["R"]),
+                         tr_rule="global")
     X, U = w["X"].clone(), w["U"].clone()
 
     def step(X, U, ev=None):
@@ -154,17 +199,31 @@ def main():
     qp_avg_ms = sum(a.elapsed_time(b) for a, b in qp_ms) / len(qp_ms)
     ipm_iters = float(torch.stack(iters).sum().item())
     status = out["status"].cpu()
-    rows = (1 << 3) + 2 * len(BOX) + 2 * N_OBS
-    flops = qp_flops_per_ipm_iter(6, 3, K, rows) * ipm_iters / args.steps
+    rows = (1 << m) + 2 * len(box) + 2 * n_obs + 2 * j_max
+    flops = qp_flops_per_ipm_iter(n, m, K, rows) * ipm_iters / args.steps
     achieved = flops / (qp_avg_ms * 1e-3) / 1e12
-    traffic, traffic_src = committed_traffic()
+    traffic, traffic_src = committed_traffic() if args.config == "c3" else (None, None)
     if rank == 0:
         cpu = None
-        if not args.no_cpu:
+        if not args.no_cpu and args.config == "c3":
             cpu = cpu_baseline(sc, min(args.cpu_sample, N), threads=min(16, os.cpu_count() or 1))
-        value = world * args.steps / el
+        if args.config == "c3":
+            value, scaling = world * args.steps / el, "weak"
+            metric = "SCvx-iterations/sec, N agents x K=50 nodes (N=1024 per GPU)"
+            data = "synthetic (C3 construction, SURVEY §8d: seeded random starts/goals, 8 spheres)"
+            workload = ("C3: N=1024 agents/GPU, 3-D double integrator n=6 m=3, K=50, FOH sigma=30, tr=0.25, "
+                        "8 obstacles (soft), SOC ||u||<=1, box |x|,|y|<=12")
+        else:
+            value, scaling = args.steps / el, "strong"
+            metric = f"SCvx-iterations/sec, N={cfg['N_total']} agents x K=50 nodes (whole problem)"
+            data = ("synthetic (C4 construction, SURVEY §8d: 16^3 lattice, spacing 6, permuted goals)"
+                    if args.config == "c4" else
+                    "synthetic (C5 construction: quadrotors from hover, seeded starts/goals, 8 spheres)")
+            workload = (f"{args.config.upper()}: N={cfg['N_total']} agents ({N}/GPU), model {model} n={n} m={m}, "
+                        f"K=50, pairwise coupling R={cfg['R']} (j_max={j_max} nearest per node, one shared slack), "
+                        f"{n_obs} obstacles, box |x|,|y|<={box[0][2]:g}, global trust-region rule, RCCL all_gather of states")
         line = {
-            "metric": "SCvx-iterations/sec, N agents x K=50 nodes (N=1024 per GPU)",
+            "metric": metric,
             "value": value,
             "unit": "SCvx-iterations/s",
             "n_gpus": world,
@@ -172,13 +231,11 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1e3 * el / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (C3 construction, SURVEY §8d: seeded random starts/goals, 8 spheres)",
-            "config": {"workload": "C3: N=1024 agents/GPU, 3-D double integrator n=6 m=3, K=50, FOH sigma=30, "
-                                   "tr=0.25, 8 obstacles (soft), SOC ||u||<=1, box |x|,|y|<=12",
-                       "agents_per_gpu": N, "K": K, "parallelism": f"agents sharded x{world}"},
+            "data": data,
+            "config": {"workload": workload, "agents_per_gpu": N, "K": K, "parallelism": f"agents sharded x{world}"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                          "traffic_unit": "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE)", "traffic_source": traffic_src,

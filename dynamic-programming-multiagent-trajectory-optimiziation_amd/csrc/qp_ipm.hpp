@@ -1469,8 +1469,10 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             status = SCVX_STATUS_OPTIMAL;
             break;
         }
-        // ECOS-style reduced accuracy: what a numerical breakdown below leaves is still usable
-        const bool near = pres <= 1e-6 * hsc && dres <= 1e-6 * qscl && gap <= 1e-6 * fmax(1.0, fabs(pobj));
+        // reduced accuracy ("optimal_inaccurate"): what a numerical breakdown below leaves is still
+        // usable if it meets the reduced tolerances of the reference's solvers (Clarabel / ECOS:
+        // feasibility 1e-4, gap 5e-5 relative)
+        const bool near = pres <= 1e-4 * hsc && dres <= 1e-4 * qscl && gap <= 5e-5 * fmax(1.0, fabs(pobj));
         // SOC Nesterov-Todd scaling (hyperbolic-rotation form, W lam = W^-1 s)
         double Wi2uu[NU * NU];
 #pragma unroll
@@ -1694,7 +1696,21 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             double chk = al;
 #pragma unroll
             for (int i = 0; i < NZ; ++i) chk += 0.0 * dz[i];
-            chk = wave_sum(chk);  // NaN anywhere in the direction poisons the sum
+            if (act) {  // slack / dual directions of the live rows (unused group / costate slots excluded)
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    if (row_on(r)) {
+                        double dsr, dlr;
+                        row_dir(r, true, dsr, dlr);
+                        chk += 0.0 * (dsr + dlr);
+                    }
+                }
+                if (soc) {
+#pragma unroll
+                    for (int j = 0; j < NQ; ++j) chk += 0.0 * (dsq[j] + dlq[j]);
+                }
+            }
+            chk = wave_sum(chk);  // NaN / Inf anywhere in the direction poisons the sum
             if (!(chk == chk) || !(al > 0.0)) {
                 status = near ? SCVX_STATUS_MAX_ITER : SCVX_STATUS_NUMERICAL;
                 fail_code = 4.0;

@@ -85,7 +85,7 @@ class JacobiSCvx:
         return self.X_all
 
     def step(self, X, U, qp_events=None):
-        """One SCvx iteration; returns the new (X, U) (device tensors owned by the solver).
+        """One SCvx iteration; returns the new (X, U) and the raw solver outputs.
         qp_events: optional list; a (start, end) pair of timing events recorded on the launch
         stream around the QP kernel is appended to it."""
         torch = self.torch
@@ -103,7 +103,13 @@ class JacobiSCvx:
         if qp_events is not None:
             e1.record(torch.cuda.current_stream())
             qp_events.append((e0, e1))
-        Xn, Un = out["X"], out["U"]
+        # an agent whose subproblem failed numerically (status 2) rejects the step: it keeps its
+        # iterate (its output may be non-finite and would otherwise reach every other agent through
+        # the collision all-gather) and halves its own trust radius so the next subproblem differs.
+        # The reference aborts the whole run instead (cvxpy raises SolverError, dist_scvx_3d.py:110).
+        failed = out["status"] == 2
+        ok = (~failed)[:, None, None]
+        Xn, Un = torch.where(ok, out["X"], X), torch.where(ok, out["U"], U)
         # cost_fcn (dist_scvx_3d.py:131-138) and the trust-region halving rule (:250-252)
         cost = (Un[:, :-1, :] * Un[:, :-1, :]).sum(dim=(1, 2))
         if self.tr_rule == "global":
@@ -117,4 +123,5 @@ class JacobiSCvx:
             shrink = (cost > self.prev_cost).to(torch.float64)
             self.tr.mul_(1.0 - 0.5 * shrink)
             self.prev_cost.copy_(cost)
+        self.tr.mul_(1.0 - 0.5 * failed.to(torch.float64))
         return Xn, Un, out

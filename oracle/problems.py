@@ -85,21 +85,8 @@ def dense_prob_from_rows(Ad_seq, Bd_seq, Xref, Uref, x_final, tr, rows, R_unused
 
 
 def synthetic_di(N, K=50, seed=0, sigma=30.0, spread=10.0, obstacles=0, obs_seed=11):
-    """C2/C3 construction: random starts/goals in [-spread, spread]^3, v=0,
-    straight-line warm start (as x_initial, dist_scvx_3d.py:122-128), U=0; M spheres."""
-    rng = np.random.default_rng(seed)
-    p0 = rng.uniform(-spread, spread, (N, 3))
-    pf = rng.uniform(-spread, spread, (N, 3))
-    a = np.linspace(0, 1, K)
-    X = np.zeros((N, K, 6))
-    X[:, :, 0:3] = p0[:, None, :] * (1 - a)[None, :, None] + pf[:, None, :] * a[None, :, None]
-    U = np.zeros((N, K, 3))
-    x_init = X[:, 0, :].copy()
-    x_final = X[:, -1, :].copy()
-    obs = []
-    if obstacles:
-        ro = np.random.default_rng(obs_seed)
-        ctr = ro.uniform(-8, 8, (obstacles, 3))
-        rad = ro.uniform(0.5, 1.5, obstacles)
-        obs = [(ctr[o], rad[o]) for o in range(obstacles)]
-    return dict(X=X, U=U, x_init=x_init, x_final=x_final, sigma=np.full(N, sigma), obs=obs)
+    """C2/C3 construction -- the same data the bench feeds the kernels
+    (scvx_hip/workloads.py, host-side data construction only)."""
+    from scvx_hip import workloads
+    return workloads.synthetic_di(N, K=K, seed=seed, sigma=sigma, spread=spread, obstacles=obstacles,
+                                  obs_seed=obs_seed)

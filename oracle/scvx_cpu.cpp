@@ -734,6 +734,9 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
             status = SCVX_STATUS_OPTIMAL;
             break;
         }
+        // reduced tolerances (kernel: `near`): a breakdown below ends with MAX_ITER ("inaccurate")
+        const bool near = pres <= 1e-4 * hscale && dres <= 1e-4 * qscale && gap <= 5e-5 * std::max(1.0, std::fabs(pobj));
+        const int fail_status = near ? SCVX_STATUS_MAX_ITER : SCVX_STATUS_NUMERICAL;
         // ---- scaling and node Hessians (aux eliminated)
         for (int t = 0; t < K; ++t) {
             Node& N = ag.nd[t];
@@ -768,7 +771,7 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
                 for (int i = 0; i < nz; ++i)
                     for (int j = 0; j < na; ++j) l.Hza(i, j) = Hf(i, nz + j);
                 l.Haa_L = Haa;
-                if (!chol(l.Haa_L)) { status = SCVX_STATUS_NUMERICAL; goto done; }
+                if (!chol(l.Haa_L)) { status = fail_status; goto done; }
                 Mat X = chol_solve_mat(l.Haa_L, tr(l.Hza));  // na x nz
                 Mat corr = mul(l.Hza, X);
                 for (size_t i = 0; i < l.Hxu.a.size(); ++i) l.Hxu.a[i] -= corr.a[i];
@@ -776,7 +779,7 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
             H[t] = l.Hxu;
         }
         riccati_factor(ag, H, R);
-        if (!R.ok) { status = SCVX_STATUS_NUMERICAL; break; }
+        if (!R.ok) { status = fail_status; break; }
         {
             // ---- one Newton solve for a given complementarity rhs (orthant rco, SOC rcs2)
             auto newton = [&](const std::vector<Vec>& rco, const std::vector<Vec>& rcq, std::vector<Vec>& dz,
@@ -922,7 +925,7 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
             }
             std::vector<Vec> dz, ds, dl, dsq, dlq;
             Vec dy, dyi, dyf;
-            if (!newton(rco, rcq, dz, ds, dl, dsq, dlq, dy, dyi, dyf)) { status = SCVX_STATUS_NUMERICAL; break; }
+            if (!newton(rco, rcq, dz, ds, dl, dsq, dlq, dy, dyi, dyf)) { status = fail_status; break; }
             if (it == 0 && std::getenv("SCVX_DUMP")) {
                 FILE* fp = std::fopen(std::getenv("SCVX_DUMP"), "wb");
                 for (int t = 0; t < K; ++t) { double buf[40] = {0}; for (int j = 0; j < ag.nd[t].nv && j < 40; ++j) buf[j] = dz[t][j]; std::fwrite(buf, sizeof(double), 40, fp); }
@@ -950,7 +953,7 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
                     rcq[t][0] += sig * mu;
                 }
             }
-            if (!newton(rco, rcq, dz, ds, dl, dsq, dlq, dy, dyi, dyf)) { status = SCVX_STATUS_NUMERICAL; break; }
+            if (!newton(rco, rcq, dz, ds, dl, dsq, dlq, dy, dyi, dyf)) { status = fail_status; break; }
             double al = std::min(1.0, 0.99 * max_step(ds, dl, dsq, dlq));
             if (std::getenv("SCVX_DEBUG")) {
                 std::fprintf(stderr, "   alpha_aff %.3e sigma %.3e alpha %.3e\n", aa, sig, al);

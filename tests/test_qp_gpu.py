@@ -115,3 +115,45 @@ def test_collision_rows_match_reference_formula(cuda):
             got = rows[a, t, :cnt[a, t]]
             np.testing.assert_allclose(got[np.lexsort(got.T)], ref[t][np.lexsort(ref[t].T)], rtol=1e-13, atol=1e-13)
         assert cnt[a, K - 1] == 0
+
+
+@pytest.mark.parametrize("j_max", [0, 8])
+def test_quad_family_matches_cpu_and_dense(cuda, j_max):
+    """C5 family: 12-state quadrotor from hover (scvx_hip/workloads.synthetic_quad), 8 obstacles,
+    optionally collision rows (R=0.5) -- GPU vs the C++ restatement and the dense oracle."""
+    import torch
+    from scvx_hip import workloads
+    N, K = 8, 50
+    sc = workloads.synthetic_quad(N, K=K, seed=3, obstacles=8)
+    X, U, sig = _t(sc["X"], cuda), _t(sc["U"], cuda), _t(sc["sigma"], cuda)
+    disc = scvx_hip.foh_batched("quad", X, U, sig)
+    box = [(0, -12, 12), (1, -12, 12)]
+    rows = cnt = None
+    if j_max:
+        rows, cnt = scvx_hip.collision_rows(X, 0, N, 0.5, j_max=j_max)
+    spec = scvx_hip.QPSpec(model="quad", K=K, box=box, obs=sc["obs"], w_obs=1e6, j_max=j_max, w_coll=1e4,
+                           tol=1e-9, max_iter=80)
+    tr = np.full(N, 0.25)
+    out = scvx_hip.qp_solve_batched(spec, disc, sig, X, U, _t(sc["x_init"], cuda), _t(sc["x_final"], cuda),
+                                    _t(tr, cuda), rows, cnt)
+    st = out["status"].cpu().numpy()
+    assert (st == 0).all(), st
+    tpl = qp_cpu.make_template(12, 4, K, box=box, obs=sc["obs"], w_obs=1e6, j_max=j_max, w_coll=1e4, tol=1e-9, model_id=3,
+                               max_iter=80)
+    dn = disc.cpu().numpy()
+    cpu = qp_cpu.solve_batched(tpl, dn, sc["sigma"], sc["X"], sc["U"], sc["x_init"], sc["x_final"], tr,
+                               None if rows is None else rows.cpu().numpy(),
+                               None if cnt is None else cnt.cpu().numpy())
+    assert (cpu["status"] == 0).all()
+    og = out["obj"].cpu().numpy()
+    np.testing.assert_allclose(og, cpu["obj"], rtol=1e-8)
+    assert np.abs(out["X"].cpu().numpy() - cpu["X"]).max() < 1e-6
+    if not j_max:
+        A, B, C, S, z = pb.unpack_disc(dn[0], 12, 4)
+        prob = dict(A=A, B=B, C=C, c=S * sc["sigma"][0] + z, Xref=sc["X"][0], Uref=sc["U"][0],
+                    x_final=sc["x_final"][0], tr=0.25, box=box, obs=sc["obs"], w_obs=1e6, umax=None,
+                    fix_last_input=True)
+        with np.errstate(all="ignore"):
+            Xd, Ud, objd, info = qd.solve_agent(prob, tol=1e-10, maxit=150)
+        assert info["status"] == "optimal"
+        assert abs(og[0] - objd) <= 1e-7 * max(1.0, abs(objd))
