@@ -128,4 +128,14 @@ struct Quadrotor12 {
     }
 };
 
+// host-side: parameter block of a model id (quadrotor defaults: mass 1, g 9.81, J = diag(.02,.02,.04))
+inline ModelParams model_params(int model_id, const double* params) {
+    ModelParams P{};
+    if (model_id == Quadrotor12::ID) {
+        const double dflt[5] = {1.0, 9.81, 0.02, 0.02, 0.04};
+        for (int i = 0; i < 5; ++i) P.p[i] = params ? params[i] : dflt[i];
+    }
+    return P;
+}
+
 }  // namespace scvx

@@ -10,6 +10,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SCVX_HIP_LIB") or os.path.join(HERE, "libscvx_hip.so")  # override: diagnostics builds
 
 SCVX_MAX_BOX, SCVX_MAX_OBS, SCVX_MAX_NBR = 4, 16, 32
+SCVX_IS_MAX_PROJ, SCVX_IS_MAX_STATE = 3, 12
 MODEL_IDS = {"di": 0, "unicycle": 1, "si": 2, "quad": 3}
 MODEL_DIMS = {"di": (6, 3), "unicycle": (3, 2), "si": (3, 3), "quad": (12, 4)}
 STATUS = {0: "optimal", 1: "optimal_inaccurate", 2: "solver_error"}
@@ -17,7 +18,8 @@ STATUS = {0: "optimal", 1: "optimal_inaccurate", 2: "solver_error"}
 # every symbol declared in include/scvx_hip.h
 EXPORTS = ("scvx_version", "scvx_last_error", "scvx_foh_batched", "scvx_integrate_nonlinear_batched",
            "scvx_qp_solve_batched", "scvx_qp_workspace_bytes", "scvx_qp_set_trace",
-           "scvx_collision_rows_batched", "scvx_scp_solve_batched", "scvx_scp_workspace_bytes")
+           "scvx_collision_rows_batched", "scvx_scp_solve_batched", "scvx_scp_workspace_bytes",
+           "scvx_intersample_batched")
 
 
 class ScvxError(RuntimeError):
@@ -57,6 +59,17 @@ class SCPTemplate(ctypes.Structure):
     ]
 
 
+class IntersampleTemplate(ctypes.Structure):
+    """Mirror of scvx_intersample_template (include/scvx_hip.h)."""
+    _fields_ = [
+        ("model_id", ctypes.c_int32), ("n_obs", ctypes.c_int32),
+        ("obs_center", (ctypes.c_double * SCVX_IS_MAX_PROJ) * SCVX_MAX_OBS), ("obs_radius", ctypes.c_double * SCVX_MAX_OBS),
+        ("proj_rows", ctypes.c_int32), ("proj", ctypes.c_double * (SCVX_IS_MAX_PROJ * SCVX_IS_MAX_STATE)),
+        ("dt", ctypes.c_double), ("seg_dt", ctypes.c_double), ("eps", ctypes.c_double), ("tol", ctypes.c_double),
+        ("num_samples", ctypes.c_int32), ("max_crit", ctypes.c_int32), ("nsub", ctypes.c_int32),
+    ]
+
+
 _lib = None
 
 
@@ -81,6 +94,7 @@ def lib():
         L.scvx_scp_workspace_bytes.argtypes = [ctypes.POINTER(SCPTemplate), i32]
         L.scvx_scp_workspace_bytes.restype = sz
         L.scvx_scp_solve_batched.argtypes = [ctypes.POINTER(SCPTemplate), i32] + [vp] * 19 + [vp, sz, vp]
+        L.scvx_intersample_batched.argtypes = [ctypes.POINTER(IntersampleTemplate), vp, i32, i32] + [vp] * 9
         sized = ("scvx_last_error", "scvx_qp_workspace_bytes", "scvx_scp_workspace_bytes")
         for fn in EXPORTS:
             getattr(L, fn).restype = getattr(L, fn).restype if fn in sized else i32

@@ -218,6 +218,45 @@ int scvx_scp_solve_batched(const scvx_scp_template* tpl, int N, const double* di
 /* Bytes of caller-owned device scratch scvx_scp_solve_batched needs for N agents. */
 size_t scvx_scp_workspace_bytes(const scvx_scp_template* tpl, int N);
 
+/* ------------------------------------------------------------------------------------------
+ * Batched inter-sample obstacle clearance: SCvx/utils/intersample_collision.py (make_segment_f
+ * :104-126, h_i :7-26, find_critical_times :29-67, linearize_h :70-101) for every (agent, segment k,
+ * obstacle) of N agents, as called per segment by SCvx/models/game_si_model.py:156-176.
+ * For segment k of agent a: x(t) rolls out dx/dtau = f(x, u_k + tau/dt_phys (u_{k+1} - u_k)) from
+ * X[a][k] to tau = t dt_phys (dt_phys = seg_dt * sigma[a]; FirstOrderHold._dx); h(t) = ||proj x(t) -
+ * c_o|| - r_o; the interior minima t* in (0, dt) of h are located by the reference's scan
+ * (num_samples central differences phi with step eps on [eps, dt - eps], bisection to tol, phi2 > 0);
+ * at each t*: h0 = h(t*), grad_x = central differences of h w.r.t. x_k, grad_u = 0 (the segment
+ * roll-out ignores u_k, as in the reference).
+ * ------------------------------------------------------------------------------------------ */
+#define SCVX_IS_MAX_PROJ 3
+#define SCVX_IS_MAX_STATE 12
+
+typedef struct scvx_intersample_template {
+    int32_t model_id;
+    int32_t n_obs;
+    double obs_center[SCVX_MAX_OBS][SCVX_IS_MAX_PROJ];
+    double obs_radius[SCVX_MAX_OBS];
+    int32_t proj_rows;                                   /* rows of T (projection), <= 3 */
+    double proj[SCVX_IS_MAX_PROJ * SCVX_IS_MAX_STATE];   /* T row-major, row stride SCVX_IS_MAX_STATE */
+    double dt;            /* find_critical_times' dt (normalised segment length; the reference passes 1.0) */
+    double seg_dt;        /* FirstOrderHold.dt = 1 / (K_foh - 1) */
+    double eps;           /* central-difference step (reference 1e-4) */
+    double tol;           /* bisection tolerance (reference 1e-6) */
+    int32_t num_samples;  /* scan points (reference 100) */
+    int32_t max_crit;     /* minima stored per (agent, segment, obstacle) */
+    int32_t nsub;         /* RK4 steps per roll-out */
+} scvx_intersample_template;
+
+/*
+ * Inputs (device): X [N][K][n], U [N][K][m], sigma [N]; params as scvx_foh_batched.
+ * Outputs (device): n_crit [N][K-1][n_obs] (minima found; only the first max_crit are stored),
+ *   t_crit / h0 [N][K-1][n_obs][max_crit], grad_x [..][max_crit][n], grad_u [..][max_crit][m].
+ */
+int scvx_intersample_batched(const scvx_intersample_template* tpl, const double* params, int K, int N,
+                             const double* X, const double* U, const double* sigma, int32_t* n_crit,
+                             double* t_crit, double* h0, double* grad_x, double* grad_u, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

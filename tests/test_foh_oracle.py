@@ -50,3 +50,29 @@ def test_double_integrator_foh_is_exact_zoh_sum():
         np.testing.assert_allclose(A[:, k].reshape(6, 6, order="F"), Ad, atol=1e-13)
         np.testing.assert_allclose((B[:, k] + C[:, k]).reshape(6, 3, order="F"), Bd, atol=1e-13)
     np.testing.assert_allclose(S * sigma + z, 0.0, atol=1e-12)
+
+
+# ---------------------------------------------------------------- inter-sample clearance scan
+INTERSAMPLE = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "intersample_*.npz")))
+
+
+@pytest.mark.parametrize("path", INTERSAMPLE, ids=[os.path.basename(p) for p in INTERSAMPLE])
+def test_intersample_oracle_matches_reference_goldens(path):
+    """oracle/intersample_np.py (RK4 roll-outs) vs the reference's own find_critical_times /
+    linearize_h (odeint): same minima; t* within 1e-5 (bisection tol 1e-6 + LSODA noise through
+    the eps=1e-4 differences), h0 within 1e-6 (LSODA rtol 1.49e-8 on positions of size ~10), grad_x within 1e-4 (central differences of an ODE
+    solved to 1.49e-8 carry ~1e-4 noise in the reference itself), grad_u identically 0."""
+    from oracle import intersample_np
+    d = np.load(path)
+    model, K, sigma = str(d["model"]), int(d["K"]), float(d["sigma"])
+    X, U, T = d["X"], d["U"], d["T"]
+    for k in range(K - 1):
+        for o in range(d["obs_center"].shape[0]):
+            got = intersample_np.segment(model, X[:, k], U[:, k], U[:, k + 1], sigma / (K - 1), T, d["obs_center"][o],
+                                         d["obs_radius"][o], nsub=NSUB[model])
+            assert len(got) == d["count"][k, o], (k, o)
+            for c, (t, h0, gx, gu) in enumerate(got):
+                assert abs(t - d["t_crit"][k, o, c]) < 1e-5
+                assert abs(h0 - d["h0"][k, o, c]) < 1e-6
+                assert np.abs(gx - d["grad_x"][k, o, c]).max() < 1e-4
+                assert np.all(gu == 0.0) and np.all(d["grad_u"][k, o, c] == 0.0)
