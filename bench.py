@@ -125,12 +125,81 @@ def cpu_baseline(sc, n_sample, threads, min_seconds=10.0):
                        f"IPM C++), {el:.1f} s wall, -O3 x86-64-v3, OpenMP over agents")
 
 
+def is_flops_per_rollout(n, m, nsub):
+    """Single-integrator roll-out to t: nsub RK4 steps (4 f-evals of m interpolation FMAs, 3 stage
+    updates + final combination over n) + projection and norm."""
+    return nsub * (4 * 2 * m + 3 * 2 * n + 4 * n) + 3 * n + 2
+
+
+def bench_intersample(args, world, rank, device):
+    """--config is: the inter-sample clearance scan (scvx_intersample_batched) over C3-sized data --
+    N=1024 single-integrator agents (the reference's intersample user, game_si_model.py:156-176),
+    K=50, the 8 C3 spheres, T = I, dt = 1, 100 samples.  value = segment x obstacle scans / s."""
+    import torch
+    import scvx_hip
+    from scvx_hip import workloads
+    N = args.agents
+    sc = workloads.synthetic_di(N, K=K, seed=1 + rank, sigma=1.0, obstacles=N_OBS)
+    X = np.ascontiguousarray(sc["X"][:, :, 0:3])
+    U = np.repeat(((sc["x_final"] - sc["x_init"])[:, 0:3])[:, None, :], K, 1)   # straight-line velocities
+    U = U + np.random.default_rng(7).normal(0, 0.5, U.shape)
+    T = lambda a: torch.tensor(np.ascontiguousarray(a), dtype=torch.float64, device=device)  # noqa: E731
+    Xd, Ud, sd = T(X), T(U), T(np.ones(N))
+    obs = sc["obs"]
+    run = lambda: scvx_hip.intersample_batched("si", Xd, Ud, sd, obs, max_crit=8)  # noqa: E731
+    for _ in range(args.warmup):
+        out = run()
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(st)
+    for _ in range(args.steps):
+        out = run()
+    e1.record(st)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    kms = e0.elapsed_time(e1) / args.steps
+    scans = N * (K - 1) * len(obs)
+    minima = int(out["n_crit"].sum().item())
+    flops = scans * 2 * 100 * is_flops_per_rollout(3, 3, 1)   # grid phi only: a lower bound
+    achieved = flops / (kms * 1e-3) / 1e12
+    cpu = None
+    if not args.no_cpu:
+        from oracle import intersample_np
+        t1, done = time.perf_counter(), 0
+        while time.perf_counter() - t1 < 10.0:
+            a, rem = divmod(done, (K - 1) * len(obs))
+            k, o = divmod(rem, len(obs))
+            a %= N
+            intersample_np.segment("si", X[a, k], U[a, k], U[a, k + 1], 1.0 / (K - 1), np.eye(3), obs[o][0],
+                                   obs[o][1], nsub=1)
+            done += 1
+        cel = time.perf_counter() - t1
+        cpu = dict(value=done / cel, unit="segment-obstacle scans/s", cores=1, kind="port",
+                   sample=f"{done} scans of the same workload (oracle/intersample_np.py, numpy, 1 thread), {cel:.1f} s")
+    if rank != 0:
+        return
+    print(json.dumps({
+        "metric": "inter-sample clearance scans/sec (segment x obstacle), N=1024 agents x K=50 x 8 obstacles",
+        "value": scans / (el / args.steps), "unit": "scans/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": 1e3 * el / args.steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic (C3 starts/goals and spheres, SI velocities + noise)",
+        "config": {"workload": "intersample: N=1024 SI agents, K=50, 8 spheres, T=I, dt=1, 100 samples, eps 1e-4",
+                   "agents_per_gpu": N, "K": K, "parallelism": f"agents sharded x{world}"},
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None, "kernel": "intersample_kernel",
+                     "kernel_ms": kms, "note": "FP64 VALU; algorithmic FLOPs = grid central differences only "
+                                               "(lower bound: bisection / linearisation roll-outs not counted)"},
+        "minima_found": minima, "cpu_baseline": cpu}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=("c3", "c4", "c5"), default="c3")
+    ap.add_argument("--config", choices=("c3", "c4", "c5", "is"), default="c3")
     ap.add_argument("--agents", type=int, default=N_AGENTS, help="c3: agents per GPU")
     ap.add_argument("--cpu-sample", type=int, default=1024)
     ap.add_argument("--no-cpu", action="store_true")
@@ -148,6 +217,8 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
+    if args.config == "is":
+        return bench_intersample(args, world, rank, device)
     if args.config == "c3":
         N = args.agents
         sc, w = make_workload(N, seed=1 + rank, device=device)
