@@ -99,12 +99,12 @@ def make_coupled(config, world, rank, device):
     return sc, t, dict(model=model, R=R, obs=obs, box=box, j_max=j_max, N_total=N_total, n_loc=n_loc)
 
 
-def cpu_baseline(sc, n_sample, threads, min_seconds=10.0):
+def cpu_baseline(sc, n_sample, threads, min_seconds=10.0, tol=1e-9):
     """Time the CPU restatement (oracle) on n_sample agents: FOH + QP for one SCvx iteration,
     repeated until about min_seconds of wall time (a bounded sample of the same workload)."""
     import numpy as np
     from oracle import foh_oracle, qp_cpu
-    tpl = qp_cpu.make_template(6, 3, K, box=BOX, obs=sc["obs"], w_obs=1e6, u_max=U_MAX, tol=1e-9, max_iter=60)
+    tpl = qp_cpu.make_template(6, 3, K, box=BOX, obs=sc["obs"], w_obs=1e6, u_max=U_MAX, tol=tol, max_iter=60)
     reps = 0
     t0 = time.perf_counter()
     while True:
@@ -203,6 +203,7 @@ def main():
     ap.add_argument("--agents", type=int, default=N_AGENTS, help="c3: agents per GPU")
     ap.add_argument("--cpu-sample", type=int, default=1024)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--tol", type=float, default=1e-9, help="IPM stopping tolerance (Clarabel's default is 1e-8)")
     args = ap.parse_args()
 
     import torch
@@ -223,7 +224,7 @@ def main():
         N = args.agents
         sc, w = make_workload(N, seed=1 + rank, device=device)
         model, box, j_max, n, m = "di", BOX, 0, 6, 3
-        spec = scvx_hip.QPSpec(model="di", K=K, box=BOX, obs=sc["obs"], w_obs=1e6, u_max=U_MAX, tol=1e-9,
+        spec = scvx_hip.QPSpec(model="di", K=K, box=BOX, obs=sc["obs"], w_obs=1e6, u_max=U_MAX, tol=args.tol,
                                max_iter=60)
         drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, tr_rule="per_agent")
         n_obs = N_OBS
@@ -233,7 +234,7 @@ def main():
         n, m = scvx_hip.MODEL_DIMS[model]
         n_obs = len(cfg["obs"])
         spec = scvx_hip.QPSpec(model=model, K=K, box=box, obs=cfg["obs"], w_obs=1e6, j_max=j_max, w_coll=1e4,
-                               tol=1e-9, max_iter=60)
+                               tol=args.tol, max_iter=60)
         drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, coupling=CouplingSpec(R=cfg["R"]),
                          tr_rule="global")
     X, U = w["X"].clone(), w["U"].clone()
@@ -277,7 +278,7 @@ def main():
     if rank == 0:
         cpu = None
         if not args.no_cpu and args.config == "c3":
-            cpu = cpu_baseline(sc, min(args.cpu_sample, N), threads=min(16, os.cpu_count() or 1))
+            cpu = cpu_baseline(sc, min(args.cpu_sample, N), threads=min(16, os.cpu_count() or 1), tol=args.tol)
         if args.config == "c3":
             value, scaling = world * args.steps / el, "weak"
             metric = "SCvx-iterations/sec, N agents x K=50 nodes (N=1024 per GPU)"
@@ -314,6 +315,9 @@ def main():
                          "note": "FP64 VALU-bound small dense linear algebra; peak = FP64 dense peak; "
                                  "algorithmic FLOPs per DESIGN.md §4 x executed IPM iterations"},
             "ipm_iters_per_agent": ipm_iters / (args.steps * N),
+            "ipm_iters_max_last": int(out["iters"].max().item()),
+            "ipm_iters_hist_last": {str(int(v)): int(c) for v, c in zip(*np.unique(out["iters"].cpu().numpy(),
+                                                                                  return_counts=True))},
             "status_counts": {str(k): int((status == k).sum()) for k in (0, 1, 2)},
             "cpu_baseline": cpu,
         }
