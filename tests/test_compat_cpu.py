@@ -221,3 +221,20 @@ def test_multi_agent_logging_format(capsys):
                           "| Δx=0.00e+00 | Δs=0.00e+00 | o= 1.000 | tr= 1.000\n")
     assert "\n=== SCvx+ADMM Summary ===\n  Total iterations: 4\n  Final time scale o: 1.000\n" in out
     assert "  Total runtime:    2.50s\n=========================\n" in out
+
+
+# ---------------------------------------------------------------- bench workloads (host data)
+def test_workload_constructions():
+    """SURVEY §8d constructions: C4 lattice spacing exceeds 2R (no initial contact) and its goals are
+    a permutation of the sites; C5 starts at hover thrust; C3 obstacles match the seeded spheres."""
+    from scvx_hip import workloads
+    c4 = workloads.synthetic_lattice(side=4, K=10, spacing=6.0)
+    s, g = c4["x_init"][:, 0:3], c4["x_final"][:, 0:3]
+    assert s.shape == (64, 6 // 2) and np.allclose(np.sort(s, 0), np.sort(g, 0))
+    d = np.linalg.norm(s[:, None] - s[None], axis=-1) + np.eye(64) * 1e9
+    assert d.min() > 2 * 2.3
+    c5 = workloads.synthetic_quad(5, K=10, obstacles=3)
+    assert c5["X"].shape == (5, 10, 12) and np.allclose(c5["U"][:, :, 0], 9.81) and len(c5["obs"]) == 3
+    c3 = workloads.synthetic_di(7, K=10, obstacles=8)
+    r = np.array([o[1] for o in c3["obs"]])
+    assert c3["X"].shape == (7, 10, 6) and ((r >= 0.5) & (r <= 1.5)).all()

@@ -157,3 +157,56 @@ def test_quad_family_matches_cpu_and_dense(cuda, j_max):
             Xd, Ud, objd, info = qd.solve_agent(prob, tol=1e-10, maxit=150)
         assert info["status"] == "optimal"
         assert abs(og[0] - objd) <= 1e-7 * max(1.0, abs(objd))
+
+
+@pytest.mark.parametrize("model", ["unicycle", "si"])
+def test_unicycle_and_si_classes_match_cpu_and_dense(cuda, model):
+    """The unicycle (n=3, m=2, planar positions) and single-integrator (n=3, m=3, SOC ||u|| <= 3)
+    instantiations of the trust-region QP kernel -- GPU vs the C++ restatement and the dense oracle."""
+    N, K = 6, 30
+    rng = np.random.default_rng(11)
+    n, m = scvx_hip.MODEL_DIMS[model]
+    pd = 2 if model == "unicycle" else 3
+    a = np.linspace(0, 1, K)[None, :, None]
+    p0 = rng.uniform(-8, -5, (N, 1, n))
+    p1 = rng.uniform(5, 8, (N, 1, n))
+    X = p0 * (1 - a) + p1 * a
+    if model == "unicycle":
+        X[:, :, 2] = np.pi / 4 + rng.normal(0, 0.1, (N, K))
+        U = np.stack([np.full((N, K), 0.8), rng.normal(0, 0.1, (N, K))], -1)
+        sig = np.full(N, 24.0)
+        obs = [(np.array([0.5, -0.5]), 1.5), (np.array([-3.0, -2.0]), 1.0)]
+        umax = None
+    else:
+        U = np.repeat(((p1 - p0)[:, 0] / 12.0)[:, None, :], K, 1) + rng.normal(0, 0.05, (N, K, 3))
+        sig = np.full(N, 12.0)
+        obs = [(np.array([0.3, -0.4, 0.2]), 1.5), (np.array([-4.0, -3.0, -4.0]), 1.0)]
+        umax = 3.0
+    box = [(0, -10, 10), (1, -10, 10)]
+    Xt, Ut, st_ = _t(X, cuda), _t(U, cuda), _t(sig, cuda)
+    disc = scvx_hip.foh_batched(model, Xt, Ut, st_)
+    tr = np.full(N, 0.5)
+    spec = scvx_hip.QPSpec(model=model, K=K, pos_dim=pd, box=box, obs=obs, w_obs=1e6, u_max=umax, tol=1e-10,
+                           max_iter=80)
+    out = scvx_hip.qp_solve_batched(spec, disc, st_, Xt, Ut, _t(X[:, 0], cuda), _t(X[:, -1], cuda), _t(tr, cuda))
+    dn = disc.cpu().numpy()
+    tpl = qp_cpu.make_template(n, m, K, pos_dim=pd, box=box, obs=obs, w_obs=1e6, u_max=umax, tol=1e-10, max_iter=80,
+                               model_id=scvx_hip.MODEL_IDS[model])
+    cpu = qp_cpu.solve_batched(tpl, dn, sig, X, U, X[:, 0], X[:, -1], tr)
+    st = out["status"].cpu().numpy()
+    ok = cpu["status"] == 0
+    assert ok.sum() >= N // 2, cpu["status"]
+    assert (st[ok] == 0).all(), st
+    og, Xg = out["obj"].cpu().numpy(), out["X"].cpu().numpy()
+    for i in np.nonzero(ok)[0]:
+        assert abs(og[i] - cpu["obj"][i]) <= 1e-8 * max(1.0, abs(cpu["obj"][i]))
+        assert np.abs(Xg[i] - cpu["X"][i]).max() < 1e-6
+    i = int(np.nonzero(ok)[0][0])
+    A, B, C, S, z = pb.unpack_disc(dn[i], n, m)
+    prob = dict(A=A, B=B, C=C, c=S * sig[i] + z, Xref=X[i], Uref=U[i], x_final=X[i, -1], tr=0.5, box=box, obs=obs,
+                w_obs=1e6, umax=umax, fix_last_input=True, pos_dim=pd)
+    with np.errstate(all="ignore"):
+        Xd, Ud, objd, info = qd.solve_agent(prob, tol=1e-11, maxit=150)
+    assert info["status"] == "optimal"
+    assert abs(og[i] - objd) <= 1e-7 * max(1.0, abs(objd))
+    assert max(qd.constraint_violation(prob, Xg[i], out["U"].cpu().numpy()[i]).values()) < 1e-7
