@@ -1,0 +1,13 @@
+#!/bin/bash
+# Diagnostics: build libscvx_hip.so with extra -D flags into dbg/<name>/ (load it with SCVX_HIP_LIB=...).
+# usage: tools/build_variant.sh <name> [-DFLAG ...]
+set -e
+NAME=$1; shift
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+PKG=$ROOT/dynamic-programming-multiagent-trajectory-optimiziation_amd
+OUT=$ROOT/dbg/$NAME
+mkdir -p $OUT
+ls $PKG/csrc/*.hip | xargs -P 8 -I{} sh -c "/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$ROOT/include -Wno-pass-failed $* -c {} -o $OUT/\$(basename {} .hip).o"
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $OUT/libscvx_hip.so $OUT/*.o
+rm -f $OUT/*.o
+echo $OUT/libscvx_hip.so
