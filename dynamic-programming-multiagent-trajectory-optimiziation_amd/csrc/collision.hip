@@ -12,10 +12,14 @@
 // per node (the closest ones, i.e. the rows with the largest violation S); the QP is then exact
 // whenever the culled rows stay inactive, which the host layer verifies after the solve.
 //
-// Mapping: one 64-lane workgroup per local agent, lane = node t; every lane streams all N_total
-// positions of its node (X_all rows are read with consecutive lanes on consecutive nodes) and
-// keeps its current top-j_max list in the output rows (the list's worst entry tracked in
-// registers).  X_all is the all-gathered [N_total][K][n_x] state (RCCL all_gather over xGMI).
+// Mapping: one workgroup per (node t, block of 64 local agents), lane = local agent.  All lanes scan
+// the same neighbour sequence j = 0..N_total-1, so node t's positions of a tile of TJ neighbours are
+// staged in LDS once per workgroup (cooperative loads) and read back as LDS broadcasts; the X_all
+// traffic is then ~N_total*pos_dim*8 bytes per workgroup instead of per agent.  Each lane keeps its
+// top-j_max list (S values and neighbour indices) in registers, with the same insertion / eviction
+// order as a sequential scan (so the kept set and the slot of every row are those of the
+// reference-order scan), and writes its rows once at the end.  X_all is the all-gathered
+// [N_total][K][n_x] state (RCCL all_gather over xGMI).
 #include <hip/hip_runtime.h>
 
 #include "common.hpp"
@@ -23,60 +27,92 @@
 
 namespace scvx {
 
-__global__ __launch_bounds__(64) void collision_rows_kernel(int K, int pd, int nx, int N_total,
+constexpr int COLL_TJ = 512;  // neighbours staged per LDS tile
+
+template <int JM>
+__global__ __launch_bounds__(64) void collision_rows_kernel(int K, int pd, int nx, int N_total, int N_local,
                                                             const double* __restrict__ X_all, int i0, double R,
                                                             double cull, int j_max, double* __restrict__ rows,
                                                             int32_t* __restrict__ count) {
-    const int t = threadIdx.x;
-    const long long a = blockIdx.x;  // local agent
-    const long long gi = i0 + a;     // global agent index
-    if (t >= K) return;
-    int32_t* cnt = count + a * K + t;
-    if (t >= K - 1) { *cnt = 0; return; }
+    __shared__ double tile[COLL_TJ * 3];
+    const int lane = threadIdx.x;
+    const int t = blockIdx.y;
+    const long long a = (long long)blockIdx.x * 64 + lane;  // local agent
+    const bool live = a < N_local;
+    const long long gi = i0 + a;  // global agent index
+    if (t >= K - 1) {             // no rows at the last node
+        if (live) count[a * K + t] = 0;
+        return;
+    }
     double pi[3] = {0, 0, 0};
-    for (int d = 0; d < pd; ++d) pi[d] = X_all[(gi * K + t) * nx + d];
-    double* out = rows + (a * K + t) * (long long)j_max * (pd + 1);
-    int n = 0;
-    int worst = 0;
-    double worst_c = 1e300;  // smallest S among kept rows (the one to evict)
+    if (live)
+        for (int d = 0; d < pd; ++d) pi[d] = X_all[(gi * K + t) * nx + d];
+    // selection on squared distances: S = 2R - |d| is decreasing in |d|^2, so "largest S kept,
+    // evict the smallest" is "smallest |d|^2 kept, evict the largest" (no sqrt in the scan)
+    double kd[JM];
+    int kj[JM];
+#pragma unroll
+    for (int k = 0; k < JM; ++k) { kd[k] = 0.0; kj[k] = -1; }
+    int n = 0, worst = 0;
+    double worst_d2 = -1.0;  // largest |d|^2 among kept rows (the one to evict)
     const double cull2 = cull > 0 ? cull * cull : -1.0;
-    for (long long j = 0; j < N_total; ++j) {
-        if (j == gi) continue;
+    for (int j0 = 0; j0 < N_total; j0 += COLL_TJ) {
+        const int nt = min(COLL_TJ, N_total - j0);
+        __syncthreads();
+        for (int e = lane; e < nt * pd; e += 64) {
+            const int jj = e / pd, d = e - jj * pd;
+            tile[jj * 3 + d] = X_all[((long long)(j0 + jj) * K + t) * nx + d];
+        }
+        __syncthreads();
+        if (!live) continue;
+#pragma unroll 4
+        for (int jj = 0; jj < nt; ++jj) {
+            const long long j = j0 + jj;
+            double d2 = 0.0;
+            for (int d = 0; d < pd; ++d) {
+                const double df = pi[d] - tile[jj * 3 + d];
+                d2 += df * df;
+            }
+            if (j == gi || (cull2 > 0 && !(d2 < cull2))) continue;
+            int slot;
+            if (n < j_max) {
+                slot = n++;
+            } else {
+                if (!(d2 < worst_d2)) continue;
+                slot = worst;
+            }
+#pragma unroll
+            for (int k = 0; k < JM; ++k)
+                if (k == slot) { kd[k] = d2; kj[k] = (int)j; }
+            if (n == j_max) {  // recompute the eviction candidate (first maximum, as a sequential scan)
+                worst_d2 = -1.0;
+#pragma unroll
+                for (int k = 0; k < JM; ++k)
+                    if (k < j_max && kd[k] > worst_d2) { worst_d2 = kd[k]; worst = k; }
+            }
+        }
+    }
+    if (!live) return;
+    double* out = rows + (a * K + t) * (long long)j_max * (pd + 1);
+#pragma unroll
+    for (int k = 0; k < JM; ++k) {
+        if (k >= n) break;
+        const long long j = kj[k];
         double diff[3] = {0, 0, 0}, d2 = 0.0;
         for (int d = 0; d < pd; ++d) {
             diff[d] = pi[d] - X_all[(j * K + t) * nx + d];
             d2 += diff[d] * diff[d];
         }
-        if (cull2 > 0 && !(d2 < cull2)) continue;
         const double nr = sqrt(d2);
-        const double c = 2.0 * R - nr;
-        int slot;
-        if (n < j_max) {
-            slot = n++;
-        } else {
-            if (!(c > worst_c)) continue;
-            slot = worst;
-        }
-        double* row = out + slot * (pd + 1);
-        double b = c;
+        double b = 2.0 * R - nr;
         for (int d = 0; d < pd; ++d) {
             const double g = diff[d] / nr;
-            row[d] = g;
+            out[k * (pd + 1) + d] = g;
             b += g * pi[d];
         }
-        row[pd] = b;
-        // S of the stored row: c = b - g'pbar_i
-        if (n == j_max) {  // recompute the eviction candidate
-            worst_c = 1e300;
-            for (int k = 0; k < j_max; ++k) {
-                const double* rk = out + k * (pd + 1);
-                double ck = rk[pd];
-                for (int d = 0; d < pd; ++d) ck -= rk[d] * pi[d];
-                if (ck < worst_c) { worst_c = ck; worst = k; }
-            }
-        }
+        out[k * (pd + 1) + pd] = b;
     }
-    *cnt = n;
+    count[a * K + t] = n;
 }
 
 }  // namespace scvx
@@ -85,10 +121,19 @@ extern "C" int scvx_collision_rows_batched(int K, int pos_dim, int n_x, int N_to
                                            int N_local, double R, double cull_radius, int j_max, double* rows,
                                            int32_t* count, void* stream) {
     if (K < 2 || K > 64 || pos_dim < 1 || pos_dim > 3 || pos_dim > n_x || N_total < 0 || N_local < 0 || i0 < 0 ||
-        i0 + N_local > N_total || j_max < 1 || !X_all || !rows || !count)
+        i0 + N_local > N_total || j_max < 1 || j_max > 32 || !X_all || !rows || !count)
         return scvx::set_error(SCVX_EINVAL, "collision: bad args");
     if (N_local == 0) return SCVX_OK;
-    hipLaunchKernelGGL(scvx::collision_rows_kernel, dim3(N_local), dim3(64), 0, (hipStream_t)stream, K, pos_dim,
-                       n_x, N_total, X_all, i0, R, cull_radius, j_max, rows, count);
+    const dim3 grid((unsigned)((N_local + 63) / 64), (unsigned)K);
+    hipStream_t st = (hipStream_t)stream;
+    if (j_max <= 8)
+        hipLaunchKernelGGL(scvx::collision_rows_kernel<8>, grid, dim3(64), 0, st, K, pos_dim, n_x, N_total, N_local,
+                           X_all, i0, R, cull_radius, j_max, rows, count);
+    else if (j_max <= 16)
+        hipLaunchKernelGGL(scvx::collision_rows_kernel<16>, grid, dim3(64), 0, st, K, pos_dim, n_x, N_total, N_local,
+                           X_all, i0, R, cull_radius, j_max, rows, count);
+    else
+        hipLaunchKernelGGL(scvx::collision_rows_kernel<32>, grid, dim3(64), 0, st, K, pos_dim, n_x, N_total, N_local,
+                           X_all, i0, R, cull_radius, j_max, rows, count);
     return scvx::check_launch("collision_rows_kernel");
 }
