@@ -34,11 +34,13 @@ __global__ __launch_bounds__(256) void foh_kernel(const double* __restrict__ X, 
                                                   const double* __restrict__ sigma, double* __restrict__ out,
                                                   int K, int N, int nsub, ModelParams P) {
     constexpr int n = Mdl::N, m = Mdl::M, ncol = n + 2 * m + 2;
+    __shared__ double stage[256 * n];
     const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     const long long total = (long long)N * (K - 1) * ncol;
-    if (tid >= total) return;
-    const int col = (int)(tid % ncol);
-    const long long iv = tid / ncol;  // agent * (K-1) + interval
+    const bool live = tid < total;
+    const long long tidc = live ? tid : total - 1;  // dead lanes recompute a valid column, store nothing
+    const int col = (int)(tidc % ncol);
+    const long long iv = tidc / ncol;  // agent * (K-1) + interval
     const int k = (int)(iv % (K - 1));
     const long long agent = iv / (K - 1);
 
@@ -109,9 +111,18 @@ __global__ __launch_bounds__(256) void foh_kernel(const double* __restrict__ X, 
             c[i] += h / 6.0 * (ac[i] + kc[i]);
         }
     }
-    double* o = out + tid * n;
+    // the block's columns are one contiguous range of out: stage them in LDS, then store with
+    // consecutive lanes on consecutive doubles (full-line coalesced writes)
 #pragma unroll
-    for (int i = 0; i < n; ++i) o[i] = c[i];
+    for (int i = 0; i < n; ++i) stage[threadIdx.x * n + i] = c[i];
+    __syncthreads();
+    const long long base = (long long)blockIdx.x * blockDim.x * n;
+    const long long lim = total * n - base;
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+        const int e = i * (int)blockDim.x + threadIdx.x;
+        if (e < lim) out[base + e] = stage[e];
+    }
 }
 
 // integrate_nonlinear_piecewise (first_order_hold.py:127-140): one lane per (agent, interval),
