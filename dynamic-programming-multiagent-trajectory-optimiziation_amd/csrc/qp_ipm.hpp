@@ -82,7 +82,7 @@ constexpr int qp_ncol(int nx, int nu, int nb, int ns, int ng) {
 // factor outputs per stage (stage-major block): K, kappa, LD, W2, P, Pi, u, Acl
 constexpr int qp_fbs(int nx, int nu) { return 3 * nu * nx + nu * nu + 3 * nx * nx + nx; }
 constexpr long long qp_ws_doubles(int nx, int nu, int nb, int ns, int ng) {
-    return (long long)qp_ncol(nx, nu, nb, ns, ng) * 64 + 64LL * qp_pkt(nx, nu) + 64LL * qp_fbs(nx, nu);
+    return (long long)qp_ncol(nx, nu, nb, ns, ng) * 64 + 64LL * qp_pkt(nx, nu) + 64LL * qp_fbs(nx, nu) + 64;
 }
 
 template <int NX_, int NU_, int NB_, int NO_, int NC_>
@@ -155,6 +155,12 @@ __host__ __device__ constexpr int qp_dpk(int off, int slot) { return off | (slot
 // VGPR (voffset) and the column part as a (rematerialisable) SGPR constant (soffset), so no
 // per-column 64-bit address is ever materialised in vector registers.
 typedef unsigned int qp_u2 __attribute__((ext_vector_type(2)));
+// Every memory op of the factor sweep is unconditional: lanes with nothing to store write to a
+// per-lane sink block at the end of the agent's own workspace, and prefetch loads of padding
+// elements read a clamped in-bounds element.  A load or store under a divergent branch makes the
+// compiler's vmcnt accounting fall back to vmcnt(0), which drains the packet prefetches issued
+// stages ahead (measured: most of the factor's per-stage time).
+constexpr int QP_SINK_DOUBLES = 64;
 struct QPBuf {
     __amdgpu_buffer_rsrc_t rs;
     __device__ __forceinline__ double ld(int voff, int soff) const {
@@ -198,7 +204,7 @@ __device__ __forceinline__ double qp_dot(const double* lds, int L, int R, int so
 // pressure) nor serialised between the repetitions.
 template <int KK, int NREP>
 __device__ __forceinline__ void qp_phase(double* lds, const int (&d)[NREP][4], int soff, bool last, int acl_off,
-                                         const QPBuf& wb, int fbo) {
+                                         const QPBuf& wb, int fbo, int lsink, int vsink) {
     int Ld[NREP], Rd[NREP], Od[NREP], Bd[NREP];
 #pragma unroll
     for (int r = 0; r < NREP; ++r) {
@@ -215,15 +221,14 @@ __device__ __forceinline__ void qp_phase(double* lds, const int (&d)[NREP][4], i
 #pragma unroll
     for (int r = 0; r < NREP; ++r) {
         const int O = Od[r];
-        if (O >= 0) {
-            const int oo = (O & 0x7FFF) + ((O >> 16) & 1) * acl_off;
-            const double old = lds[oo];
-            lds[oo] = ((O >> 15) & 1) ? old + val[r] : val[r];
-            const int g = (O >> 17) - 1;
+        const bool on = O >= 0;
+        const int oo = on ? (O & 0x7FFF) + ((O >> 16) & 1) * acl_off : lsink;
+        const double old = lds[oo];
+        lds[oo] = (on && ((O >> 15) & 1)) ? old + val[r] : val[r];
+        const int g = on ? (O >> 17) - 1 : -1;
 #ifndef QPX_NOGST
-            if (g >= 0) wb.st(g * 8, fbo, val[r]);
+        wb.st(g >= 0 ? g * 8 : vsink, fbo, val[r]);
 #endif
-        }
     }
 }
 
@@ -258,6 +263,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     const int vt = t * 8;  // this lane's element of a stage-minor column
     constexpr int PKB = C::NCOL * WAVE * 8;  // byte offset of the packets [t][PKT]
     constexpr int FBB = PKB + WAVE * PKT * 8;  // byte offset of the factor output blocks [t][FBS]
+    constexpr int SKB = FBB + WAVE * C::FBS * 8;  // byte offset of the per-lane store sink (past every block)
     const int vpk = t * PKT * 8;
     const int vfb = t * C::FBS * 8;
     // Loads go through `vcur`, this lane's offset re-derived (opaquely) at the start of every
@@ -488,14 +494,14 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
             for (int k = 0; k < PFN; ++k) {
                 const int e = lane + WAVE * k;
-                b[k] = (e < PKT && ts >= 0) ? wb.ld(e * 8, PKB + (ts > 0 ? ts : 0) * PKT * 8) : 0.0;
+                b[k] = wb.ld((e < PKT ? e : PKT - 1) * 8, PKB + (ts > 0 ? ts : 0) * PKT * 8);  // in bounds
             }
         };
         auto pf_store = [&](int ts, const double* b) __attribute__((always_inline)) {
 #pragma unroll
             for (int k = 0; k < PFN; ++k) {
                 const int e = lane + WAVE * k;
-                if (e < PKT) lds[C::F_RING + (ts & 1) * PKT + e] = b[k];
+                lds[e < PKT ? C::F_RING + (ts & 1) * PKT + e : C::F_SINK] = b[k];
             }
         };
         pf_load(K - 1, pf[0]);
@@ -511,15 +517,15 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             const bool last = ts == K - 1;
             const int acl_off = ts * NX * NX;
             const int fbo = FBB + ts * C::FBS * 8;  // byte offset of this stage's output block
-            if (ts - 3 >= 0 && ts < K - 1) pf_load(ts - 3, nb);  // (stage K-1 issued K-4 before the loop)
+            pf_load(ts - 3, nb);  // unconditional: stage K-1 re-issues K-4, ts-3 < 0 reads zeros
             const bool fst = ts >= 20 && ts < 30;
             if (fst) stamp(-1);
             // ---- phase 1: T1 = P'A, T2 = P'Bt, W1 = A'Pi', W2 = Bt'Pi', u = P'e, xe += Pi''e
-            qp_phase<NX, R1>(lds, d1, soff, last, acl_off, wb, fbo);
+            qp_phase<NX, R1>(lds, d1, soff, last, acl_off, wb, fbo, C::F_SINK, SKB - fbo + lane * 8);
             wsync();
             if (fst) stamp(11);
             // ---- phase 2: Qh = Q + A'T1, Sh = S' + Bt'T1, Rh = R + Bt'T2
-            qp_phase<NX, R2>(lds, d2, soff, last, acl_off, wb, fbo);
+            qp_phase<NX, R2>(lds, d2, soff, last, acl_off, wb, fbo, C::F_SINK, SKB - fbo + lane * 8);
             wsync();
             if (fst) stamp(12);
             // ---- phase 3: Rh = L D L' in registers (every lane); [K | kappa] = -Rh^-1 [Sh | W2]
@@ -559,8 +565,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                     for (int j = 0; j < NU; ++j) dinv[j] = 1.0;
                 }
-                if (lane < 2 * NX) {
-                    const int c = lane;
+                {  // every lane runs the solve (lanes >= 2 NX on a copy of column 0, results to the sinks)
+                    const bool kl = lane < 2 * NX;
+                    const int c = kl ? lane : 0;
                     const int off = c < NX ? C::F_SH + c * NU : C::F_W2 + (c - NX) * NU;
                     double x[NU];
 #pragma unroll
@@ -583,13 +590,13 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                     for (int i = 0; i < NU; ++i) {
                         const double v = fx ? 0.0 : -x[i];
-                        lds[C::F_KK + c * NU + i] = v;
+                        lds[kl ? C::F_KK + c * NU + i : C::F_SINK] = v;
 #ifndef QPX_NOGST
-                        wb.st((g + i * NX) * 8, fbo, v);
+                        wb.st(kl ? (g + i * NX) * 8 : SKB - fbo + lane * 8, fbo, v);
 #endif
                     }
                 }
-                if (lane < NU * NU) {
+                {
                     double v = 0.0;
 #pragma unroll
                     for (int e = 0; e < NU * NU; ++e) {
@@ -597,14 +604,14 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                         v = fma(qp_mask(e, lane), (ei > ej) ? Lm[e] : (ei == ej ? dinv[ei] : 0.0), v);
                     }
 #ifndef QPX_NOGST
-                    wb.st((C::B_LD + lane) * 8, fbo, v);
+                    wb.st(lane < NU * NU ? (C::B_LD + lane) * 8 : SKB - fbo + lane * 8, fbo, v);
 #endif
                 }
             }
             wsync();
             if (fst) stamp(13);
             // ---- phase 4: P = Qh + Sh'K, Pi = W1 + Sh'kappa, M += W2'kappa, Acl = A + Bt K
-            qp_phase<NU, R4>(lds, d4, soff, last, acl_off, wb, fbo);
+            qp_phase<NU, R4>(lds, d4, soff, last, acl_off, wb, fbo, C::F_SINK, SKB - fbo + lane * 8);
             if (ts > 0) pf_store(ts - 1, cb);
             wsync();
             if (fst) stamp(14);
