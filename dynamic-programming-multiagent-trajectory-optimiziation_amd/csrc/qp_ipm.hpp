@@ -744,15 +744,18 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 ldA(ts - 4, a, g);
                 --ts;
             };
-            while (ts >= 0) {
+            // groups of four steps with no exit inside the loop body (a mid-body exit makes the
+            // compiler's vmcnt tracking fall back to vmcnt(0) and drain the prefetches), then the
+            // 0-3 remaining steps continuing the buffer rotation
+            while (ts >= 3) {
                 step(ab[0], gb[0]);
-                if (ts < 0) break;
                 step(ab[1], gb[1]);
-                if (ts < 0) break;
                 step(ab[2], gb[2]);
-                if (ts < 0) break;
                 step(ab[3], gb[3]);
             }
+            if (ts >= 0) step(ab[0], gb[0]);
+            if (ts >= 0) step(ab[1], gb[1]);
+            if (ts >= 0) step(ab[2], gb[2]);
         }
         wsync();
         stamp(5);
@@ -905,15 +908,15 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 ldA(ts + 4, a, f);
                 ++ts;
             };
-            while (ts < K - 1) {
+            while (ts <= K - 5) {  // four steps per trip, no exit inside (see the backward chain)
                 step(ab[0], fb[0]);
-                if (ts >= K - 1) break;
                 step(ab[1], fb[1]);
-                if (ts >= K - 1) break;
                 step(ab[2], fb[2]);
-                if (ts >= K - 1) break;
                 step(ab[3], fb[3]);
             }
+            if (ts < K - 1) step(ab[0], fb[0]);
+            if (ts < K - 1) step(ab[1], fb[1]);
+            if (ts < K - 1) step(ab[2], fb[2]);
         }
         wsync();
         stamp(8);
