@@ -194,12 +194,62 @@ def bench_intersample(args, world, rank, device):
         "minima_found": minima, "cpu_baseline": cpu}), flush=True)
 
 
+def bench_scproblem(args, world, rank, device):
+    """--config scp: the SCProblem path (SCvx/optimization/sc_problem.py + scvx_solver.py) -- N=1024
+    independent unicycle agents (the reference's UnicycleModel, K=100 = global_parameters.K, 3
+    obstacles) stepping BatchedSCVXSolver in lockstep: one FOH launch + one scvx_scp_solve_batched
+    launch + device metrics per step.  Convergence is disabled so exactly `steps` iterations run."""
+    import torch
+    sys.path.insert(0, os.path.join(REPO, "dynamic-programming-multiagent-trajectory-optimiziation_amd"))
+    from SCvx.models.unicycle_model import UnicycleModel
+    from SCvx.optimization.scvx_solver import BatchedSCVXSolver
+    N = args.agents
+    rng = np.random.default_rng(1 + rank)
+    models = [UnicycleModel(r_init=np.array([-8.0, -8.0, 0.0]) + np.r_[rng.uniform(-1, 1, 2), 0.0],
+                            r_final=np.array([8.0, 8.0, 0.0]) + np.r_[rng.uniform(-1, 1, 2), 0.0]) for _ in range(N)]
+    bat = BatchedSCVXSolver(models, device=device)
+    bat.conv_tol = -1.0
+    bat.max_iter = args.warmup
+    bat.solve()
+    torch.cuda.synchronize()
+    bat.max_iter = args.steps
+    t0 = time.perf_counter()
+    bat.solve()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    iters = np.concatenate(bat.ipm_iters) if bat.ipm_iters else np.zeros(1)
+    cpu = None
+    if not args.no_cpu:
+        from oracle import scp_problems as sp_, scp_cpu
+        t1, done = time.perf_counter(), 0
+        while time.perf_counter() - t1 < 10.0:
+            m = models[done % N]
+            p = sp_.scp_instance("unicycle", K=100, x_init=m.x_init, x_final=m.x_final)
+            scp_cpu.SCPSolver(p, tol=1e-9).solve()
+            done += 1
+        cel = time.perf_counter() - t1
+        cpu = dict(value=done / cel / N, unit="SCvx-iterations/s (N=1024-agent equivalent)", cores=1, kind="port",
+                   sample=f"{done} SCProblem solves (oracle/scp_cpu.py numpy restatement, 1 thread; FOH excluded), "
+                          f"{cel:.1f} s")
+    if rank != 0:
+        return
+    print(json.dumps({
+        "metric": "SCvx-iterations/sec of the SCProblem path, N=1024 unicycle agents x K=100",
+        "value": world * args.steps / el, "unit": "SCvx-iterations/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": 1e3 * el / args.steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic (reference UnicycleModel defaults, jittered BCs)",
+        "config": {"workload": "scp: BatchedSCVXSolver, N=1024 unicycle agents, K=100, 3 obstacles, ECOS-form LP",
+                   "agents_per_gpu": N, "K": 100, "parallelism": f"agents sharded x{world}"},
+        "ipm_iters_per_agent": float(iters.mean()), "ipm_iters_max": int(iters.max()),
+        "cpu_baseline": cpu}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=("c3", "c4", "c5", "is"), default="c3")
+    ap.add_argument("--config", choices=("c3", "c4", "c5", "is", "scp"), default="c3")
     ap.add_argument("--agents", type=int, default=N_AGENTS, help="c3: agents per GPU")
     ap.add_argument("--cpu-sample", type=int, default=1024)
     ap.add_argument("--no-cpu", action="store_true")
@@ -220,6 +270,8 @@ def main():
     device = torch.device("cuda", local)
     if args.config == "is":
         return bench_intersample(args, world, rank, device)
+    if args.config == "scp":
+        return bench_scproblem(args, world, rank, device)
     if args.config == "c3":
         N = args.agents
         sc, w = make_workload(N, seed=1 + rank, device=device)
