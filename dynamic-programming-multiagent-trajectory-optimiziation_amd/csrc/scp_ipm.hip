@@ -256,10 +256,14 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
     for (int t = lane; t < K; t += WAVE) {
         double* B = nb(t);
         double xb[NX], ub[NU];
+        #pragma unroll
         for (int i = 0; i < NX; ++i) xb[i] = a.Xref[(agent * K + t) * NX + i];
+        #pragma unroll
         for (int j = 0; j < NU; ++j) ub[j] = a.Uref[(agent * K + t) * NU + j];
         double Cp[NX * NU];
+        #pragma unroll
         for (int i = 0; i < NX; ++i)
+            #pragma unroll
             for (int j = 0; j < NU; ++j) Cp[i * NU + j] = Cprev(t, i, j);
         const bool subst = fin && t == K - 2;
         const double* dk = disc + (long long)t * DSTR;  // only read when t < K-1
@@ -267,18 +271,23 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
         auto put = [&](int r, double* av, double h) {
             if (subst) {  // nu_{K-2} = x_final - (A x + B u + S sigma + z)   (u_{K-1} pinned at 0)
                 double an[NX];
+                #pragma unroll
                 for (int i = 0; i < NX; ++i) an[i] = av[ZN + i];
                 for (int l = 0; l < NX; ++l) {
                     double v = 0.0;
+                    #pragma unroll
                     for (int i = 0; i < NX; ++i) v += dk[l * NX + i] * an[i];  // (A' an)_l, A col-major
                     av[l] -= v;
                 }
+                #pragma unroll
                 for (int j = 0; j < NU; ++j) {
                     double v = 0.0;
+                    #pragma unroll
                     for (int i = 0; i < NX; ++i) v += dk[NX * NX + j * NX + i] * an[i];
                     av[ZU + j] -= v;
                 }
                 double sv = 0.0, hz = 0.0;
+                #pragma unroll
                 for (int i = 0; i < NX; ++i) {
                     sv += dk[NX * NX + 2 * NX * NU + i] * an[i];
                     hz += an[i] * (xfin[i] - dk[NX * NX + 2 * NX * NU + NX + i]);
@@ -288,12 +297,15 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
                 h -= hz;
             }
             // FOH transform: a_u += C_{t-1}' a_x
+            #pragma unroll
             for (int j = 0; j < NU; ++j) {
                 double v = 0.0;
+                #pragma unroll
                 for (int i = 0; i < NX; ++i) v += Cp[i * NU + j] * av[i];
                 av[ZU + j] += v;
             }
             double* rp = B + Ly.o_rows + r * RS;
+            #pragma unroll
             for (int i = 0; i < NZ; ++i) rp[i] = av[i];
             rp[NZ] = h;
             hmax = fmax(hmax, fabs(h));
@@ -304,6 +316,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
         for (int s = 0; s < (1 << NX); ++s) {  // TR facets on x
             clr();
             double h = 0.0;
+            #pragma unroll
             for (int i = 0; i < NX; ++i) { const double sg = (s >> (NX - 1 - i)) & 1 ? -1.0 : 1.0; av[i] = sg; h += sg * xb[i]; }
             av[TX] = -1.0;
             put(r++, av, h);
@@ -311,6 +324,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
         for (int s = 0; s < (1 << NU); ++s) {  // TR facets on u
             clr();
             double h = 0.0;
+            #pragma unroll
             for (int j = 0; j < NU; ++j) { const double sg = (s >> (NU - 1 - j)) & 1 ? -1.0 : 1.0; av[ZU + j] = sg; h += sg * ub[j]; }
             av[TU] = -1.0;
             put(r++, av, h);
@@ -318,6 +332,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
         if (t < K - 1)
             for (int s = 0; s < (1 << NX); ++s) {  // ||nu_t||_1 <= tau_nu facets
                 clr();
+                #pragma unroll
                 for (int i = 0; i < NX; ++i) av[ZN + i] = (s >> (NX - 1 - i)) & 1 ? -1.0 : 1.0;
                 av[TN] = -1.0;
                 put(r++, av, 0.0);
@@ -364,10 +379,12 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
         }
         if (Q > 0) {
             clr(); put(RH + NS, av, T.u_max);
+            #pragma unroll
             for (int j = 0; j < NU; ++j) { clr(); av[ZU + j] = -1.0; put(RH + NS + 1 + j, av, 0.0); }
         }
         // linear / quadratic cost (z coordinates)
         double qv[NZ];
+        #pragma unroll
         for (int i = 0; i < NZ; ++i) qv[i] = 0.0;
         if (t == 0) { qv[SIG] = T.w_sigma * ics; qv[TN] = T.w_nu * ics; }
         double pv = 0.0;
@@ -376,14 +393,19 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
             for (int i = 0; i < pd; ++i) qv[i] += (a.nbr_Lam[base + i] - T.rho * a.nbr_Y[base + i]) * ics;
             pv += T.rho * ics;
         }
+        #pragma unroll
         for (int j = 0; j < NU; ++j) {
             double v = 0.0;
+            #pragma unroll
             for (int i = 0; i < NX; ++i) v += Cp[i * NU + j] * qv[i];
             qv[ZU + j] += v;
         }
+        #pragma unroll
         for (int i = 0; i < NZ; ++i) { B[Ly.o_q + i] = qv[i]; qmax = fmax(qmax, fabs(qv[i])); }
         // P_z = T' diag(pv on positions) T
+        #pragma unroll
         for (int i = 0; i < NZ; ++i)
+            #pragma unroll
             for (int j = 0; j < NZ; ++j) {
                 double v = 0.0;
                 for (int l = 0; l < pd; ++l) {
@@ -398,15 +420,20 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
             double* At = B + Ly.o_At;
             double* Bt = B + Ly.o_Bt;
             double* ct = B + Ly.o_ct;
+            #pragma unroll
             for (int e = 0; e < NXA * NXA; ++e) At[e] = 0.0;
+            #pragma unroll
             for (int e = 0; e < NXA * NUA; ++e) Bt[e] = 0.0;
             for (int g = 0; g < SCP_NG; ++g) { At[(NX + g) * NXA + NX + g] = 1.0; ct[NX + g] = 0.0; }
             if (subst) {
+                #pragma unroll
                 for (int i = 0; i < NX; ++i) ct[i] = xfin[i];
             } else {
+                #pragma unroll
                 for (int i = 0; i < NX; ++i) {
                     for (int l = 0; l < NX; ++l) At[i * NXA + l] = dk[l * NX + i];
                     At[i * NXA + SIG] = dk[NX * NX + 2 * NX * NU + i];
+                    #pragma unroll
                     for (int j = 0; j < NU; ++j) {
                         double v = dk[NX * NX + j * NX + i];
                         for (int l = 0; l < NX; ++l) v += dk[l * NX + i] * Cp[l * NU + j];
@@ -416,6 +443,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
                     ct[i] = dk[NX * NX + 2 * NX * NU + NX + i];
                 }
             }
+            #pragma unroll
             for (int i = 0; i < NXA; ++i) hmax = fmax(hmax, fabs(ct[i]));
         }
     }
@@ -481,18 +509,22 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
             }
             __syncthreads();
             double Lm[NUA * NUA];
+            #pragma unroll
             for (int e = 0; e < NUA * NUA; ++e) Lm[e] = sQuu[e];
             ldl_factor<NUA>(Lm, NUA);
             if (lane < NXA) {
                 double x[NUA];
+                #pragma unroll
                 for (int i = 0; i < NUA; ++i) x[i] = -sQux[i * NXA + lane];
                 ldl_solve<NUA>(Lm, NUA, x);
+                #pragma unroll
                 for (int i = 0; i < NUA; ++i) {
                     sK[i * NXA + lane] = x[i];
                     nb(t)[Ly.o_K + i * NXA + lane] = x[i];
                 }
             }
             if (lane == 0)
+                #pragma unroll
                 for (int e = 0; e < NUA * NUA; ++e) nb(t)[Ly.o_LD + e] = Lm[e];
             __syncthreads();
             for (int e = lane; e < NXA * NXA; e += WAVE) {
@@ -538,12 +570,15 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
             __syncthreads();
             {
                 double Lm[NUA * NUA], x[NUA];
+                #pragma unroll
                 for (int e = 0; e < NUA * NUA; ++e) Lm[e] = B[Ly.o_LD + e];
+                #pragma unroll
                 for (int i = 0; i < NUA; ++i) x[i] = -sQ[NXA + i];
                 ldl_solve<NUA>(Lm, NUA, x);
                 if (lane < NUA) {
                     // (select x[lane] without dynamic register indexing)
                     double xv = 0.0;
+                    #pragma unroll
                     for (int i = 0; i < NUA; ++i) xv = (i == lane) ? x[i] : xv;
                     nb(t)[Ly.o_kv + lane] = xv;
                 }
@@ -562,6 +597,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
         {
             const double* B0 = nb(0);
             double dx[NX];
+            #pragma unroll
             for (int i = 0; i < NX; ++i) dx[i] = -sMisc[i];
             double Lm[SCP_NG * SCP_NG], g[SCP_NG];
             for (int i = 0; i < SCP_NG; ++i) {
@@ -572,6 +608,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
             }
             ldl_factor<SCP_NG>(Lm, SCP_NG);
             ldl_solve<SCP_NG>(Lm, SCP_NG, g);
+            #pragma unroll
             for (int i = 0; i < NX; ++i)
                 if (lane == i) sXi[0][lane] = dx[i];
             for (int i = 0; i < SCP_NG; ++i)
@@ -619,6 +656,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
     auto rowp = [&](const double* B, int r) -> const double* { return B + Ly.o_rows + r * RS; };
     auto dot = [&](const double* a0, const double* z) -> double {
         double v = 0.0;
+        #pragma unroll
         for (int i = 0; i < NZ; ++i) v += a0[i] * z[i];
         return v;
     };
@@ -628,13 +666,17 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
         double* B = nb(t);
         const int nh = (int)B[Ly.o_nh];
         double Hu[NZ * NZ], f[NZ];
+        #pragma unroll
         for (int e = 0; e < NZ * NZ; ++e) Hu[e] = B[Ly.o_P + e];
+        #pragma unroll
         for (int i = 0; i < NZ; ++i) f[i] = B[Ly.o_q + i];
         for (int r = 0; r < nh; ++r) {
             const double* ar = rowp(B, r);
             const double h = ar[NZ];
+            #pragma unroll
             for (int i = 0; i < NZ; ++i) {
                 f[i] -= ar[i] * h;
+                #pragma unroll
                 for (int j = 0; j < NZ; ++j) Hu[i * NZ + j] += ar[i] * ar[j];
             }
         }
@@ -643,23 +685,31 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
             const double h = ar[NZ];
             const double rhs = -soft_w(r) - h;
             B[Ly.o_rhs + r] = rhs;
+            #pragma unroll
             for (int i = 0; i < NZ; ++i) {
                 f[i] -= ar[i] * (h + 0.5 * rhs);
+                #pragma unroll
                 for (int j = 0; j < NZ; ++j) Hu[i * NZ + j] += 0.5 * ar[i] * ar[j];
             }
         }
         for (int r = 0; r < Q; ++r) {
             const double* ar = rowp(B, RH + NS + r);
             const double h = ar[NZ];
+            #pragma unroll
             for (int i = 0; i < NZ; ++i) {
                 f[i] -= ar[i] * h;
+                #pragma unroll
                 for (int j = 0; j < NZ; ++j) Hu[i * NZ + j] += ar[i] * ar[j];
             }
         }
+        #pragma unroll
         for (int i = 0; i < NZ; ++i) Hu[i * NZ + i] += T.reg;
+        #pragma unroll
         for (int e = 0; e < NZ * NZ; ++e) B[Ly.o_H + e] = Hu[e];
+        #pragma unroll
         for (int i = 0; i < NZ; ++i) B[Ly.o_f + i] = f[i];
         if (t < K - 1)
+            #pragma unroll
             for (int i = 0; i < NXA; ++i) B[Ly.o_rp + i] = B[Ly.o_ct + i];
     }
     if (lane < NX) sMisc[lane] = -xinit[lane];
@@ -671,6 +721,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
         double* B = nb(t);
         const int nh = (int)B[Ly.o_nh];
         double z[NZ];
+        #pragma unroll
         for (int i = 0; i < NZ; ++i) { z[i] = B[Ly.o_dz + i]; B[Ly.o_z + i] = z[i]; }
         for (int r = 0; r < nh; ++r) {
             const double* ar = rowp(B, r);
@@ -699,6 +750,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
             mins = fmin(mins, Soc<QM>::mineig(sv, Q));
             minl = fmin(minl, Soc<QM>::mineig(lv, Q));
         }
+        #pragma unroll
         for (int i = 0; i < NXA; ++i) B[Ly.o_y + i] = 0.0;
     }
     {
@@ -715,6 +767,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
         }
     }
     double y0[NX];
+    #pragma unroll
     for (int i = 0; i < NX; ++i) y0[i] = 0.0;
     __syncthreads();
 
@@ -728,9 +781,12 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
             double* B = nb(t);
             const int nh = (int)B[Ly.o_nh];
             double z[NZ], rd[NZ];
+            #pragma unroll
             for (int i = 0; i < NZ; ++i) z[i] = B[Ly.o_z + i];
+            #pragma unroll
             for (int i = 0; i < NZ; ++i) {
                 double v = B[Ly.o_q + i];
+                #pragma unroll
                 for (int j = 0; j < NZ; ++j) v += B[Ly.o_P + i * NZ + j] * z[j];
                 pobjl += z[i] * (B[Ly.o_q + i] + 0.5 * (v - B[Ly.o_q + i]));
                 rd[i] = v;
@@ -738,6 +794,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
             for (int r = 0; r < nh; ++r) {
                 const double* ar = rowp(B, r);
                 const double l = B[Ly.o_lam + r], s = B[Ly.o_s + r];
+                #pragma unroll
                 for (int i = 0; i < NZ; ++i) rd[i] += ar[i] * l;
                 const double rc = dot(ar, z) + s - ar[NZ];
                 B[Ly.o_rc + r] = rc;
@@ -749,6 +806,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
                 const double l1 = B[Ly.o_lam + RH + 2 * r], l2 = B[Ly.o_lam + RH + 2 * r + 1];
                 const double s1 = B[Ly.o_s + RH + 2 * r], s2 = B[Ly.o_s + RH + 2 * r + 1];
                 const double sg = B[Ly.o_sig + r];
+                #pragma unroll
                 for (int i = 0; i < NZ; ++i) rd[i] += ar[i] * l1;
                 const double rs = soft_w(r) - l1 - l2;
                 B[Ly.o_rsig + r] = rs;
@@ -762,6 +820,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
             for (int r = 0; r < Q; ++r) {
                 const double* ar = rowp(B, RH + NS + r);
                 const double l = B[Ly.o_lam + NLP + r], s = B[Ly.o_s + NLP + r];
+                #pragma unroll
                 for (int i = 0; i < NZ; ++i) rd[i] += ar[i] * l;
                 const double rc = dot(ar, z) + s - ar[NZ];
                 B[Ly.o_rc + NLP + r] = rc;
@@ -769,15 +828,22 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
                 gapl += s * l;
             }
             // rd0 (no multipliers) -> o_rd; the full residual adds the dynamics multipliers
+            #pragma unroll
             for (int i = 0; i < NZ; ++i) B[Ly.o_rd + i] = pinned(t, i) ? 0.0 : rd[i];
             if (t < K - 1) {
                 double y[NXA];
+                #pragma unroll
                 for (int i = 0; i < NXA; ++i) y[i] = B[Ly.o_y + i];
+                #pragma unroll
                 for (int j = 0; j < NXA; ++j)
+                    #pragma unroll
                     for (int i = 0; i < NXA; ++i) rd[j] += B[Ly.o_At + i * NXA + j] * y[i];
+                #pragma unroll
                 for (int j = 0; j < NUA; ++j)
+                    #pragma unroll
                     for (int i = 0; i < NXA; ++i) rd[NXA + j] += B[Ly.o_Bt + i * NUA + j] * y[i];
                 const double* Bn = nb(t + 1);
+                #pragma unroll
                 for (int i = 0; i < NXA; ++i) {
                     double v = B[Ly.o_ct + i] - Bn[Ly.o_z + i];
                     for (int k = 0; k < NXA; ++k) v += B[Ly.o_At + i * NXA + k] * z[k];
@@ -788,14 +854,17 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
             }
             if (t > 0) {
                 const double* Bp = nb(t - 1);
+                #pragma unroll
                 for (int i = 0; i < NXA; ++i) rd[i] -= Bp[Ly.o_y + i];
             } else {
+                #pragma unroll
                 for (int i = 0; i < NX; ++i) {
                     rd[i] -= y0[i];
                     const double ri = z[i] - xinit[i];
                     presl = fmax(presl, fabs(ri));
                 }
             }
+            #pragma unroll
             for (int i = 0; i < NZ; ++i)
                 if (!pinned(t, i)) dresl = fmax(dresl, fabs(rd[i]));
         }
@@ -813,6 +882,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
             double* B = nb(t);
             const int nh = (int)B[Ly.o_nh];
             double Hu[NZ * NZ];
+            #pragma unroll
             for (int e = 0; e < NZ * NZ; ++e) Hu[e] = B[Ly.o_P + e];
             for (int r = 0; r < NLP; ++r) {
                 if (r >= nh && r < RH) continue;
@@ -824,8 +894,10 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
             for (int r = 0; r < nh; ++r) {
                 const double* ar = rowp(B, r);
                 const double d = B[Ly.o_lam + r] / B[Ly.o_s + r];
+                #pragma unroll
                 for (int i = 0; i < NZ; ++i) {
                     const double di = d * ar[i];
+                    #pragma unroll
                     for (int j = 0; j < NZ; ++j) Hu[i * NZ + j] += di * ar[j];
                 }
             }
@@ -834,8 +906,10 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
                 const double d1 = B[Ly.o_lam + RH + 2 * r] / B[Ly.o_s + RH + 2 * r];
                 const double d2 = B[Ly.o_lam + RH + 2 * r + 1] / B[Ly.o_s + RH + 2 * r + 1];
                 const double d = d1 * d2 / (d1 + d2);
+                #pragma unroll
                 for (int i = 0; i < NZ; ++i) {
                     const double di = d * ar[i];
+                    #pragma unroll
                     for (int j = 0; j < NZ; ++j) Hu[i * NZ + j] += di * ar[j];
                 }
             }
@@ -863,14 +937,18 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
                         const double* a2 = rowp(B, RH + NS + r2);
                         const double mm = M[r1 * QM + r2];
                         if (mm == 0.0) continue;
+                        #pragma unroll
                         for (int i = 0; i < NZ; ++i) {
                             const double di = mm * a1[i];
+                            #pragma unroll
                             for (int j = 0; j < NZ; ++j) Hu[i * NZ + j] += di * a2[j];
                         }
                     }
                 }
             }
+            #pragma unroll
             for (int i = 0; i < NZ; ++i) Hu[i * NZ + i] += T.reg;
+            #pragma unroll
             for (int e = 0; e < NZ * NZ; ++e) B[Ly.o_H + e] = Hu[e];
         }
         __syncthreads();
@@ -882,6 +960,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
                 double* B = nb(t);
                 const int nh = (int)B[Ly.o_nh];
                 double f[NZ];
+                #pragma unroll
                 for (int i = 0; i < NZ; ++i) f[i] = B[Ly.o_rd + i];
                 // LP rows: lt = sqrt(s l), wl = sqrt(s/l); rcomp = -lt^2 [- (ds_a/wl)(wl dl_a) + sg mu]
                 for (int r = 0; r < NLP; ++r) {
@@ -895,6 +974,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
                     B[Ly.o_t + r] = tv;
                     if (r < nh) {
                         const double* ar = rowp(B, r);
+                        #pragma unroll
                         for (int i = 0; i < NZ; ++i) f[i] += ar[i] * tv;
                     }
                 }
@@ -906,6 +986,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
                     const double rhs = -B[Ly.o_rsig + r] + t1 + t2;
                     B[Ly.o_rhs + r] = rhs;
                     const double c = t1 - d1 * rhs / (d1 + d2);
+                    #pragma unroll
                     for (int i = 0; i < NZ; ++i) f[i] += ar[i] * c;
                 }
                 if (Q > 0) {
@@ -934,9 +1015,11 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
                         B[Ly.o_rho + NLP + r] = rho[r];
                         B[Ly.o_t + NLP + r] = tv[r];
                         const double* ar = rowp(B, RH + NS + r);
+                        #pragma unroll
                         for (int i = 0; i < NZ; ++i) f[i] += ar[i] * tv[r];
                     }
                 }
+                #pragma unroll
                 for (int i = 0; i < NZ; ++i) B[Ly.o_f + i] = pinned(t, i) ? 0.0 : f[i];
             }
             __syncthreads();
@@ -947,6 +1030,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
                 double* B = nb(t);
                 const int nh = (int)B[Ly.o_nh];
                 double dz[NZ];
+                #pragma unroll
                 for (int i = 0; i < NZ; ++i) dz[i] = B[Ly.o_dz + i];
                 auto lpstep = [&](int r, double gdz) {
                     const double wl = B[Ly.o_wl + r];
@@ -1022,6 +1106,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
             const double* B = nb(t);
             const int nh = (int)B[Ly.o_nh];
             double acc = 0.0;
+            #pragma unroll
             for (int i = 0; i < NZ; ++i) acc += B[Ly.o_dz + i];
             for (int r = 0; r < NS; ++r) acc += B[Ly.o_dsig + r];
             for (int r = 0; r < RL; ++r) {
@@ -1029,9 +1114,11 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
                 acc += B[Ly.o_ds + r] + B[Ly.o_dl + r];
             }
             if (t < K - 1)
+                #pragma unroll
                 for (int i = 0; i < NXA; ++i) acc += B[Ly.o_yp + i];
             if (!(fabs(acc) < INFINITY)) badl = 1.0;
         }
+        #pragma unroll
         for (int i = 0; i < NX; ++i)
             if (!(fabs(sMisc[8 + i]) < INFINITY)) badl = 1.0;
         if (wave_max(badl) > 0.0) { status = near_ok ? 1 : 2; break; }
@@ -1039,6 +1126,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
         for (int t = lane; t < K; t += WAVE) {
             double* B = nb(t);
             const int nh = (int)B[Ly.o_nh];
+            #pragma unroll
             for (int i = 0; i < NZ; ++i) B[Ly.o_z + i] += al * B[Ly.o_dz + i];
             for (int r = 0; r < NS; ++r) B[Ly.o_sig + r] += al * B[Ly.o_dsig + r];
             for (int r = 0; r < RL; ++r) {
@@ -1047,8 +1135,10 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
                 B[Ly.o_lam + r] += al * B[Ly.o_dl + r];
             }
             if (t < K - 1)
+                #pragma unroll
                 for (int i = 0; i < NXA; ++i) B[Ly.o_y + i] += al * (B[Ly.o_yp + i] - B[Ly.o_y + i]);
         }
+        #pragma unroll
         for (int i = 0; i < NX; ++i) y0[i] += al * (sMisc[8 + i] - y0[i]);
         __syncthreads();
     }
@@ -1060,13 +1150,17 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
     for (int t = lane; t < K; t += WAVE) {
         double* B = nb(t);
         double u[NU], x[NX];
+        #pragma unroll
         for (int j = 0; j < NU; ++j) u[j] = B[Ly.o_z + ZU + j];
+        #pragma unroll
         for (int i = 0; i < NX; ++i) {
             double v = B[Ly.o_z + i];
+            #pragma unroll
             for (int j = 0; j < NU; ++j) v += Cprev(t, i, j) * u[j];
             x[i] = v;
             a.X[(agent * K + t) * NX + i] = v;
         }
+        #pragma unroll
         for (int j = 0; j < NU; ++j) a.U[(agent * K + t) * NU + j] = u[j];
         for (int o = 0; o < T.n_obs; ++o) {
             const double sg = B[Ly.o_sig + o];
@@ -1085,6 +1179,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
         }
         if (t < K - 1 && !(fin && t == K - 2)) {
             double s1 = 0.0;
+            #pragma unroll
             for (int i = 0; i < NX; ++i) {
                 const double v = B[Ly.o_z + ZN + i];
                 a.nu[(agent * (K - 1) + t) * NX + i] = v;
@@ -1102,9 +1197,11 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
         const double* uk = a.U + (agent * K + t) * NU;
         const double* uk1 = a.U + (agent * K + t + 1) * NU;
         double s1 = 0.0;
+        #pragma unroll
         for (int i = 0; i < NX; ++i) {
             double v = xfin[i] - dk[NX * NX + 2 * NX * NU + i] * sigv - dk[NX * NX + 2 * NX * NU + NX + i];
             for (int l = 0; l < NX; ++l) v -= dk[l * NX + i] * xk[l];
+            #pragma unroll
             for (int j = 0; j < NU; ++j) v -= dk[NX * NX + j * NX + i] * uk[j] + dk[NX * NX + NX * NU + j * NX + i] * uk1[j];
             a.nu[(agent * (K - 1) + t) * NX + i] = v;
             s1 += fabs(v);
