@@ -873,8 +873,8 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
         if (pres < T.tol * pscale && dres < T.tol * dscale && gap < T.tol * fmax(1.0, fabs(pobj))) { status = 0; break; }
         // ECOS-style reduced tolerances: an iterate meeting them is reported "optimal_inaccurate"
         // if the iteration cap or a numerical breakdown ends the solve before full accuracy
-        const double tol_i = fmax(1e-6, 1e3 * T.tol);
-        near_ok = pres < tol_i * pscale && dres < tol_i * dscale && gap < tol_i * fmax(1.0, fabs(pobj));
+        near_ok = pres < fmax(1e-4, T.tol) * pscale && dres < fmax(1e-4, T.tol) * dscale &&
+                  gap < fmax(5e-5, T.tol) * fmax(1.0, fabs(pobj));  // ECOS reduced tolerances
         const double mu = gap / deg;
         if (lane < NX) sMisc[lane] = nb(0)[Ly.o_z + lane] - xinit[lane];  // r_init
         // ---- scaling and node Hessians

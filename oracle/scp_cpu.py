@@ -335,8 +335,8 @@ class SCPSolver:
                 status = "optimal"
                 break
             # reduced (ECOS-style "inaccurate") tolerances, used if the solve ends early (kernel: near_ok)
-            tol_i = max(1e-6, 1e3 * self.tol)
-            near_ok = pres < tol_i * pscale and dres < tol_i * dscale and gap < tol_i * max(1.0, abs(pobj))
+            near_ok = (pres < max(1e-4, self.tol) * pscale and dres < max(1e-4, self.tol) * dscale
+                       and gap < max(5e-5, self.tol) * max(1.0, abs(pobj)))   # ECOS reduced tolerances
             # scaling
             Wn = [self._nt(nd, s[k], lam[k]) for k, nd in enumerate(nodes)]
             lt = [self._Wmul(nd, Wn[k], lam[k], 0) for k, nd in enumerate(nodes)]   # lambda~ = W lam
