@@ -141,7 +141,7 @@ __device__ __forceinline__ void ldl_solve(const double (&Lm)[D * D], int nn, dou
 template <int QM>
 struct Soc {
     // W v and W^-1 v from (w, eta)
-    __device__ static void wmul(const double* w, double eta, const double* vin, double* out, int Q, bool inv) {
+    __device__ __forceinline__ static void wmul(const double* w, double eta, const double* vin, double* out, int Q, bool inv) {
         double v[QM];
         for (int i = 0; i < Q; ++i) v[i] = vin[i];
         double w1v1 = 0.0;
@@ -152,7 +152,7 @@ struct Soc {
         const double c = sgn * v[0] + w1v1 / (1.0 + w[0]);
         for (int i = 1; i < Q; ++i) out[i] = sc * (v[i] + c * w[i]);
     }
-    __device__ static void nt(const double* s, const double* z, double* w, double& eta, int Q) {
+    __device__ __forceinline__ static void nt(const double* s, const double* z, double* w, double& eta, int Q) {
         double js = s[0] * s[0], jz = z[0] * z[0];
         for (int i = 1; i < Q; ++i) { js -= s[i] * s[i]; jz -= z[i] * z[i]; }
         const double rs = 1.0 / sqrt(js), rz = 1.0 / sqrt(jz);
@@ -164,21 +164,21 @@ struct Soc {
         for (int i = 1; i < Q; ++i) w[i] = (s[i] * rs - z[i] * rz) * ig;
         eta = sqrt(sqrt(js / jz));
     }
-    __device__ static void jprod(const double* a, const double* b, double* out, int Q) {
+    __device__ __forceinline__ static void jprod(const double* a, const double* b, double* out, int Q) {
         double d = 0.0;
         for (int i = 0; i < Q; ++i) d += a[i] * b[i];
         const double a0 = a[0], b0 = b[0];
         for (int i = 1; i < Q; ++i) out[i] = a0 * b[i] + b0 * a[i];
         out[0] = d;
     }
-    __device__ static void jdiv(const double* x, const double* r, double* out, int Q) {
+    __device__ __forceinline__ static void jdiv(const double* x, const double* r, double* out, int Q) {
         double d = x[0] * x[0], xr = x[0] * r[0];
         for (int i = 1; i < Q; ++i) { d -= x[i] * x[i]; xr -= x[i] * r[i]; }
         const double r0 = xr / d;
         for (int i = 1; i < Q; ++i) out[i] = (r[i] - r0 * x[i]) / x[0];
         out[0] = r0;
     }
-    __device__ static double step(const double* x, const double* dx, int Q) {
+    __device__ __forceinline__ static double step(const double* x, const double* dx, int Q) {
         double qa = dx[0] * dx[0], qb = x[0] * dx[0], qc = x[0] * x[0];
         for (int i = 1; i < Q; ++i) { qa -= dx[i] * dx[i]; qb -= x[i] * dx[i]; qc -= x[i] * x[i]; }
         qb *= 2.0;
@@ -197,7 +197,7 @@ struct Soc {
         if (dx[0] < 0.0) a = fmin(a, -x[0] / dx[0]);
         return a;
     }
-    __device__ static double mineig(const double* x, int Q) {
+    __device__ __forceinline__ static double mineig(const double* x, int Q) {
         double nr = 0.0;
         for (int i = 1; i < Q; ++i) nr += x[i] * x[i];
         return x[0] - sqrt(nr);
@@ -205,7 +205,10 @@ struct Soc {
 };
 
 template <int NX, int NU>
-__global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
+__global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restrict__ ws_all, const double* __restrict__ disc_all) {
+    // workspace and disc come in as kernel pointer arguments (known global address space): read out
+    // of the by-value struct they would be FLAT accesses, which also count against lgkmcnt, so every
+    // LDS wait would drain the outstanding global loads
     constexpr int NXA = NX + SCP_NG, NUA = NU + NX, NZ = NXA + NUA, RS = NZ + 1;
     constexpr int SIG = NX, TX = NX + 1, TU = NX + 2, TN = NX + 3, ZU = NX + SCP_NG, ZN = ZU + NU;
     constexpr int QM = NU + 1;
@@ -214,16 +217,16 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
     const long long agent = blockIdx.x;
     const SCPLay Ly = scp_layout(T);
     const int RH = Ly.RH, NS = Ly.NS, Q = Ly.Q, RL = Ly.RL, NLP = RH + 2 * NS;
-    double* ws = a.ws + agent * a.ws_agent;
+    double* ws = ws_all + agent * a.ws_agent;
     auto nb = [&](int t) -> double* { return ws + (long long)t * Ly.stride; };
-    const double* disc = a.disc + agent * (long long)(K - 1) * (NX * (NX + 2 * NU + 2));
+    const double* disc = disc_all + agent * (long long)(K - 1) * (NX * (NX + 2 * NU + 2));
     constexpr int DSTR = NX * (NX + 2 * NU + 2);
     const double trv = a.tr[agent], sref = a.sigma_ref[agent];
     const double* xinit = a.x_init + agent * NX;
     const double* xfin = a.x_final + agent * NX;
     const bool fin = T.has_final != 0;
 
-    __shared__ double sP[NXA * NXA], sPv[NXA], sH[NZ * NZ], sAt[NXA * NXA], sBt[NXA * NUA], sPA[NXA * NXA],
+    __shared__ double sP[NXA * NXA], sPv[NXA], sPA[NXA * NXA],
         sPB[NXA * NUA], sQxx[NXA * NXA], sQux[NUA * NXA], sQuu[NUA * NUA], sK[NUA * NXA], sV[NXA], sQ[NZ],
         sXi[2][NXA], sU[NUA], sMisc[32];
     // sMisc: 0..NX-1 r_init, 8..8+NX-1 y0+, 16.. scalars
@@ -458,19 +461,60 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
 
     auto soft_w = [&](int r) -> double { return r < T.n_obs ? w_obs : w_col; };
 
-    // ------------------------------------------------------------------ Riccati factor (uses o_H)
-    auto factor = [&]() {
-        for (int e = lane; e < NXA * NXA; e += WAVE) sP[e] = 0.0;
-        __syncthreads();
-        for (int t = K - 1; t >= 0; --t) {
-            const double* B = nb(t);
-            for (int e = lane; e < NZ * NZ; e += WAVE) sH[e] = B[Ly.o_H + e];
-            const bool dyn = t < K - 1;
-            if (dyn) {
-                for (int e = lane; e < NXA * NXA; e += WAVE) sAt[e] = B[Ly.o_At + e];
-                for (int e = lane; e < NXA * NUA; e += WAVE) sBt[e] = B[Ly.o_Bt + e];
+    // ------------------------------------------------------------------ stage packets
+    // The Riccati sweeps are sequential over nodes, so every global load inside a stage is exposed
+    // latency.  Each sweep instead gathers the next stage's operands (a packet of segments of the node
+    // blocks) into registers at the top of the current stage and parks them in an LDS ring slot at its
+    // end; the stage itself reads only LDS.  Loads are unconditional (node clamped to [0, K-1], lanes
+    // past the packet re-read its first element into the slot tail) and the sweeps use LDS-only wave
+    // barriers, so nothing drains the prefetch.
+    constexpr int PK_F = NZ * NZ + NXA * NXA + NXA * NUA;                                   // factor
+    constexpr int PK_B = NXA * NXA + NXA + NZ + NXA * NXA + NXA * NUA + NUA * NUA + NUA * NXA;  // LQ backward
+    constexpr int PK_W = NUA + NUA * NXA + NXA + NXA * NXA + NXA * NUA + NXA + NXA * NXA;   // LQ forward
+    constexpr int PK_MAX = PK_F > PK_B ? (PK_F > PK_W ? PK_F : PK_W) : (PK_B > PK_W ? PK_B : PK_W);
+    constexpr int PF = (PK_MAX + WAVE - 1) / WAVE;
+    __shared__ double sRing[2][PF * WAVE];
+    double pf[PF];
+    // segments: {node offset (0 or +1), node-block offset, length}
+    auto gather = [&](int t, const int (&dn)[7], const int (&off)[7], const int (&len)[7], int nseg) {
+        #pragma unroll
+        for (int c = 0; c < PF; ++c) {
+            const int e = lane + c * WAVE;
+            long long addr = 0;
+            int acc = 0;
+            #pragma unroll
+            for (int sg = 0; sg < 7; ++sg) {
+                if (sg < nseg && e >= acc && e < acc + len[sg]) {
+                    int tn = t + dn[sg];
+                    tn = tn < 0 ? 0 : (tn > K - 1 ? K - 1 : tn);
+                    addr = (long long)tn * Ly.stride + off[sg] + (e - acc);
+                }
+                if (sg < nseg) acc += len[sg];
             }
-            __syncthreads();
+            pf[c] = ws[addr];
+        }
+    };
+    auto park = [&](int slot) {
+        #pragma unroll
+        for (int c = 0; c < PF; ++c) sRing[slot][lane + c * WAVE] = pf[c];
+    };
+
+    // ------------------------------------------------------------------ Riccati factor (uses o_H)
+    auto factor = [&]() __attribute__((always_inline)) {
+        const int dn[7] = {0, 0, 0, 0, 0, 0, 0};
+        const int off[7] = {Ly.o_H, Ly.o_At, Ly.o_Bt, 0, 0, 0, 0};
+        const int len[7] = {NZ * NZ, NXA * NXA, NXA * NUA, 0, 0, 0, 0};
+        for (int e = lane; e < NXA * NXA; e += WAVE) sP[e] = 0.0;
+        gather(K - 1, dn, off, len, 3);
+        park(0);
+        wsync();
+        for (int t = K - 1; t >= 0; --t) {
+            const int slot = (K - 1 - t) & 1;
+            gather(t - 1, dn, off, len, 3);
+            const double* sH = sRing[slot];
+            const double* sAt = sH + NZ * NZ;
+            const double* sBt = sAt + NXA * NXA;
+            const bool dyn = t < K - 1;
             if (dyn) {
                 for (int e = lane; e < NXA * (NXA + NUA); e += WAVE) {
                     const int i = e / (NXA + NUA), j = e % (NXA + NUA);
@@ -483,7 +527,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
                         sPB[i * NUA + j - NXA] = v;
                     }
                 }
-                __syncthreads();
+                wsync();
             }
             for (int e = lane; e < NXA * NXA + NUA * NXA + NUA * NUA; e += WAVE) {
                 if (e < NXA * NXA) {
@@ -507,7 +551,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
                     sQuu[o] = v;
                 }
             }
-            __syncthreads();
+            wsync();
             double Lm[NUA * NUA];
             #pragma unroll
             for (int e = 0; e < NUA * NUA; ++e) Lm[e] = sQuu[e];
@@ -526,7 +570,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
             if (lane == 0)
                 #pragma unroll
                 for (int e = 0; e < NUA * NUA; ++e) nb(t)[Ly.o_LD + e] = Lm[e];
-            __syncthreads();
+            wsync();
             for (int e = lane; e < NXA * NXA; e += WAVE) {
                 const int i = e / NXA, j = e % NXA, p = i < j ? i : j, q = i < j ? j : i;
                 double v = sQxx[p * NXA + q];
@@ -534,65 +578,80 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
                 sP[e] = v;
                 nb(t)[Ly.o_Pr + e] = v;
             }
-            __syncthreads();
+            park(slot ^ 1);
+            wsync();
         }
+        __syncthreads();
     };
 
     // ------------------------------------------------------------------ LQ solve
     // In: o_f (per node), o_rp (t < K-1), sMisc[0..NX) = r_init.  Out: o_dz, o_yp (costates y+),
     // sMisc[8..8+NX) = y0+.
-    auto lqsolve = [&]() {
+    auto lqsolve = [&]() __attribute__((always_inline)) {
         // backward: v = P_{t+1} rp_t + p_{t+1}; qx = fx + At'v; qu = fu + Bt'v; k = -Quu^-1 qu; p = qx + K'qu
-        for (int t = K - 1; t >= 0; --t) {
-            const double* B = nb(t);
-            const bool dyn = t < K - 1;
-            if (lane < NXA) {
-                double v = 0.0;
-                if (dyn) {
-                    const double* Bn = nb(t + 1);
-                    v = sPv[lane];
-                    for (int k = 0; k < NXA; ++k) v += Bn[Ly.o_Pr + lane * NXA + k] * B[Ly.o_rp + k];
+        constexpr int B_PR = 0, B_RP = B_PR + NXA * NXA, B_F = B_RP + NXA, B_AT = B_F + NZ, B_BT = B_AT + NXA * NXA,
+                      B_LD = B_BT + NXA * NUA, B_K = B_LD + NUA * NUA;
+        {
+            const int dn[7] = {1, 0, 0, 0, 0, 0, 0};
+            const int off[7] = {Ly.o_Pr, Ly.o_rp, Ly.o_f, Ly.o_At, Ly.o_Bt, Ly.o_LD, Ly.o_K};
+            const int len[7] = {NXA * NXA, NXA, NZ, NXA * NXA, NXA * NUA, NUA * NUA, NUA * NXA};
+            gather(K - 1, dn, off, len, 7);
+            park(0);
+            wsync();
+            for (int t = K - 1; t >= 0; --t) {
+                const int slot = (K - 1 - t) & 1;
+                gather(t - 1, dn, off, len, 7);
+                const double* pk = sRing[slot];
+                const bool dyn = t < K - 1;
+                if (lane < NXA) {
+                    double v = 0.0;
+                    if (dyn) {
+                        v = sPv[lane];
+                        for (int k = 0; k < NXA; ++k) v += pk[B_PR + lane * NXA + k] * pk[B_RP + k];
+                    }
+                    sV[lane] = v;
                 }
-                sV[lane] = v;
-            }
-            __syncthreads();
-            if (lane < NZ) {
-                double v = B[Ly.o_f + lane];
-                if (dyn) {
-                    if (lane < NXA)
-                        for (int k = 0; k < NXA; ++k) v += B[Ly.o_At + k * NXA + lane] * sV[k];
-                    else
-                        for (int k = 0; k < NXA; ++k) v += B[Ly.o_Bt + k * NUA + lane - NXA] * sV[k];
+                wsync();
+                if (lane < NZ) {
+                    double v = pk[B_F + lane];
+                    if (dyn) {
+                        if (lane < NXA)
+                            for (int k = 0; k < NXA; ++k) v += pk[B_AT + k * NXA + lane] * sV[k];
+                        else
+                            for (int k = 0; k < NXA; ++k) v += pk[B_BT + k * NUA + lane - NXA] * sV[k];
+                    }
+                    if (pinned(t, lane)) v = 0.0;
+                    sQ[lane] = v;
                 }
-                if (pinned(t, lane)) v = 0.0;
-                sQ[lane] = v;
-            }
-            __syncthreads();
-            {
-                double Lm[NUA * NUA], x[NUA];
-                #pragma unroll
-                for (int e = 0; e < NUA * NUA; ++e) Lm[e] = B[Ly.o_LD + e];
-                #pragma unroll
-                for (int i = 0; i < NUA; ++i) x[i] = -sQ[NXA + i];
-                ldl_solve<NUA>(Lm, NUA, x);
-                if (lane < NUA) {
-                    // (select x[lane] without dynamic register indexing)
-                    double xv = 0.0;
+                wsync();
+                {
+                    double Lm[NUA * NUA], x[NUA];
                     #pragma unroll
-                    for (int i = 0; i < NUA; ++i) xv = (i == lane) ? x[i] : xv;
-                    nb(t)[Ly.o_kv + lane] = xv;
+                    for (int e = 0; e < NUA * NUA; ++e) Lm[e] = pk[B_LD + e];
+                    #pragma unroll
+                    for (int i = 0; i < NUA; ++i) x[i] = -sQ[NXA + i];
+                    ldl_solve<NUA>(Lm, NUA, x);
+                    if (lane < NUA) {
+                        // (select x[lane] without dynamic register indexing)
+                        double xv = 0.0;
+                        #pragma unroll
+                        for (int i = 0; i < NUA; ++i) xv = (i == lane) ? x[i] : xv;
+                        nb(t)[Ly.o_kv + lane] = xv;
+                    }
                 }
+                double pn = 0.0;
+                if (lane < NXA) {
+                    pn = sQ[lane];
+                    for (int k = 0; k < NUA; ++k) pn += pk[B_K + k * NXA + lane] * sQ[NXA + k];
+                    nb(t)[Ly.o_pv + lane] = pn;
+                }
+                wsync();
+                if (lane < NXA) sPv[lane] = pn;
+                park(slot ^ 1);
+                wsync();
             }
-            double pn = 0.0;
-            if (lane < NXA) {
-                pn = sQ[lane];
-                for (int k = 0; k < NUA; ++k) pn += B[Ly.o_K + k * NXA + lane] * sQ[NXA + k];
-                nb(t)[Ly.o_pv + lane] = pn;
-            }
-            __syncthreads();
-            if (lane < NXA) sPv[lane] = pn;
-            __syncthreads();
         }
+        __syncthreads();
         // stage 0: x part fixed (-r_init), g part free: P_gg dg = -(p_g + P_gx dx)
         {
             const double* B0 = nb(0);
@@ -621,32 +680,47 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
             }
         }
         __syncthreads();
-        int cur = 0;
-        for (int t = 0; t < K; ++t) {
-            double* B = nb(t);
-            if (lane < NUA) {
-                double v = B[Ly.o_kv + lane];
-                for (int k = 0; k < NXA; ++k) v += B[Ly.o_K + lane * NXA + k] * sXi[cur][k];
-                sU[lane] = v;
-                B[Ly.o_dz + NXA + lane] = v;
-            }
-            if (lane < NXA) B[Ly.o_dz + lane] = sXi[cur][lane];
-            __syncthreads();
-            if (t < K - 1) {
-                if (lane < NXA) {
-                    double v = B[Ly.o_rp + lane];
-                    for (int k = 0; k < NXA; ++k) v += B[Ly.o_At + lane * NXA + k] * sXi[cur][k];
-                    for (int k = 0; k < NUA; ++k) v += B[Ly.o_Bt + lane * NUA + k] * sU[k];
-                    sXi[cur ^ 1][lane] = v;
+        // forward: u = kv + K xi; xi+ = rp + At xi + Bt u; y+ = p_{t+1} + P_{t+1} xi+
+        {
+            constexpr int W_KV = 0, W_K = W_KV + NUA, W_RP = W_K + NUA * NXA, W_AT = W_RP + NXA,
+                          W_BT = W_AT + NXA * NXA, W_PV1 = W_BT + NXA * NUA, W_PR1 = W_PV1 + NXA;
+            const int dn[7] = {0, 0, 0, 0, 0, 1, 1};
+            const int off[7] = {Ly.o_kv, Ly.o_K, Ly.o_rp, Ly.o_At, Ly.o_Bt, Ly.o_pv, Ly.o_Pr};
+            const int len[7] = {NUA, NUA * NXA, NXA, NXA * NXA, NXA * NUA, NXA, NXA * NXA};
+            gather(0, dn, off, len, 7);
+            park(0);
+            wsync();
+            int cur = 0;
+            for (int t = 0; t < K; ++t) {
+                const int slot = t & 1;
+                gather(t + 1, dn, off, len, 7);
+                const double* pk = sRing[slot];
+                double* B = nb(t);
+                if (lane < NUA) {
+                    double v = pk[W_KV + lane];
+                    for (int k = 0; k < NXA; ++k) v += pk[W_K + lane * NXA + k] * sXi[cur][k];
+                    sU[lane] = v;
+                    B[Ly.o_dz + NXA + lane] = v;
                 }
-                __syncthreads();
-                cur ^= 1;
-                if (lane < NXA) {
-                    const double* Bn = nb(t + 1);
-                    double v = Bn[Ly.o_pv + lane];
-                    for (int k = 0; k < NXA; ++k) v += Bn[Ly.o_Pr + lane * NXA + k] * sXi[cur][k];
-                    B[Ly.o_yp + lane] = v;
+                if (lane < NXA) B[Ly.o_dz + lane] = sXi[cur][lane];
+                wsync();
+                if (t < K - 1) {
+                    if (lane < NXA) {
+                        double v = pk[W_RP + lane];
+                        for (int k = 0; k < NXA; ++k) v += pk[W_AT + lane * NXA + k] * sXi[cur][k];
+                        for (int k = 0; k < NUA; ++k) v += pk[W_BT + lane * NUA + k] * sU[k];
+                        sXi[cur ^ 1][lane] = v;
+                    }
+                    wsync();
+                    cur ^= 1;
+                    if (lane < NXA) {
+                        double v = pk[W_PV1 + lane];
+                        for (int k = 0; k < NXA; ++k) v += pk[W_PR1 + lane * NXA + k] * sXi[cur][k];
+                        B[Ly.o_yp + lane] = v;
+                    }
                 }
+                park(slot ^ 1);
+                wsync();
             }
         }
         __syncthreads();
@@ -774,6 +848,13 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
     // ------------------------------------------------------------------ IPM iterations
     int status = 1, it = 0;
     bool near_ok = false;
+#ifdef SCP_TRACE
+    long long tr_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    long long tr_last = __builtin_amdgcn_s_memtime();
+#define SCP_TR(i) { const long long now_ = __builtin_amdgcn_s_memtime(); tr_acc[i] += now_ - tr_last; tr_last = now_; }
+#else
+#define SCP_TR(i)
+#endif
     for (it = 0; it < T.max_iter; ++it) {
         // ---- residuals (node-parallel); rp needs xi~_{t+1}
         double gapl = 0.0, pobjl = 0.0, presl = 0.0, dresl = 0.0;
@@ -868,6 +949,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
             for (int i = 0; i < NZ; ++i)
                 if (!pinned(t, i)) dresl = fmax(dresl, fabs(rd[i]));
         }
+        SCP_TR(0)
         const double gap = wave_sum(gapl), pobj = wave_sum(pobjl), pres = wave_max(presl), dres = wave_max(dresl);
         if (!(gap == gap) || !(pres == pres) || !(dres == dres)) { status = 2; break; }
         if (pres < T.tol * pscale && dres < T.tol * dscale && gap < T.tol * fmax(1.0, fabs(pobj))) { status = 0; break; }
@@ -952,10 +1034,12 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
             for (int e = 0; e < NZ * NZ; ++e) B[Ly.o_H + e] = Hu[e];
         }
         __syncthreads();
+        SCP_TR(1)
         factor();
+        SCP_TR(2)
 
         // ---- one Newton direction: corrector = false -> affine (predictor)
-        auto direction = [&](bool corr, double sgmu) -> double {
+        auto direction = [&](bool corr, double sgmu) __attribute__((always_inline)) -> double {
             for (int t = lane; t < K; t += WAVE) {
                 double* B = nb(t);
                 const int nh = (int)B[Ly.o_nh];
@@ -1023,7 +1107,9 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
                 for (int i = 0; i < NZ; ++i) B[Ly.o_f + i] = pinned(t, i) ? 0.0 : f[i];
             }
             __syncthreads();
+            SCP_TR(3)
             lqsolve();
+            SCP_TR(4)
             // recover slack steps, step length
             double amax = INFINITY;
             for (int t = lane; t < K; t += WAVE) {
@@ -1075,7 +1161,9 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
                     amax = fmin(amax, fmin(Soc<QM>::step(sv, ds, Q), Soc<QM>::step(lv, dl, Q)));
                 }
             }
-            return wave_min(amax);
+            const double am = wave_min(amax);
+            SCP_TR(5)
+            return am;
         };
 
         const double aa = fmin(1.0, direction(false, 0.0));
@@ -1141,7 +1229,13 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a) {
         #pragma unroll
         for (int i = 0; i < NX; ++i) y0[i] += al * (sMisc[8 + i] - y0[i]);
         __syncthreads();
+        SCP_TR(6)
     }
+#ifdef SCP_TRACE
+    if (agent == 0 && lane == 0)
+        printf("SCP_TRACE it=%d res=%lld hess=%lld factor=%lld dirnode=%lld lqsolve=%lld step=%lld upd=%lld\n", it,
+               tr_acc[0], tr_acc[1], tr_acc[2], tr_acc[3], tr_acc[4], tr_acc[5], tr_acc[6]);
+#endif
 
     if (status == 1 && it == T.max_iter && !near_ok) status = 2;   // cap reached far from optimal
     // ------------------------------------------------------------------ outputs
@@ -1264,9 +1358,9 @@ extern "C" int scvx_scp_solve_batched(const scvx_scp_template* T, int N, const d
     hipStream_t st = (hipStream_t)stream;
     if (T->model_id == SCVX_MODEL_UNICYCLE && T->n_x == 3 && T->n_u == 2) {
         if (T->has_soc) return set_error(SCVX_EUNSUPPORTED, "scp: SOC rows need n_u + 1 <= 4");
-        hipLaunchKernelGGL((scp_ipm_kernel<3, 2>), dim3(N), dim3(WAVE), 0, st, a);
+        hipLaunchKernelGGL((scp_ipm_kernel<3, 2>), dim3(N), dim3(WAVE), 0, st, a, a.ws, a.disc);
     } else if (T->model_id == SCVX_MODEL_SINGLE_INTEGRATOR && T->n_x == 3 && T->n_u == 3) {
-        hipLaunchKernelGGL((scp_ipm_kernel<3, 3>), dim3(N), dim3(WAVE), 0, st, a);
+        hipLaunchKernelGGL((scp_ipm_kernel<3, 3>), dim3(N), dim3(WAVE), 0, st, a, a.ws, a.disc);
     } else {
         return set_error(SCVX_EUNSUPPORTED, "scp: model (unicycle n=3 m=2, single integrator n=3 m=3)");
     }
