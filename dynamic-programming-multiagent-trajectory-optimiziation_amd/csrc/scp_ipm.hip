@@ -751,7 +751,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             for (int i = 0; i < NZ; ++i) {
                 f[i] -= ar[i] * h;
                 #pragma unroll
-                for (int j = 0; j < NZ; ++j) Hu[i * NZ + j] += ar[i] * ar[j];
+                for (int j = i; j < NZ; ++j) Hu[i * NZ + j] += ar[i] * ar[j];
             }
         }
         for (int r = 0; r < NS; ++r) {
@@ -763,7 +763,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             for (int i = 0; i < NZ; ++i) {
                 f[i] -= ar[i] * (h + 0.5 * rhs);
                 #pragma unroll
-                for (int j = 0; j < NZ; ++j) Hu[i * NZ + j] += 0.5 * ar[i] * ar[j];
+                for (int j = i; j < NZ; ++j) Hu[i * NZ + j] += 0.5 * ar[i] * ar[j];
             }
         }
         for (int r = 0; r < Q; ++r) {
@@ -773,13 +773,13 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             for (int i = 0; i < NZ; ++i) {
                 f[i] -= ar[i] * h;
                 #pragma unroll
-                for (int j = 0; j < NZ; ++j) Hu[i * NZ + j] += ar[i] * ar[j];
+                for (int j = i; j < NZ; ++j) Hu[i * NZ + j] += ar[i] * ar[j];
             }
         }
         #pragma unroll
         for (int i = 0; i < NZ; ++i) Hu[i * NZ + i] += T.reg;
         #pragma unroll
-        for (int e = 0; e < NZ * NZ; ++e) B[Ly.o_H + e] = Hu[e];
+        for (int e = 0; e < NZ * NZ; ++e) B[Ly.o_H + e] = Hu[e / NZ <= e % NZ ? e : (e % NZ) * NZ + e / NZ];  // upper triangle, mirrored
         #pragma unroll
         for (int i = 0; i < NZ; ++i) B[Ly.o_f + i] = f[i];
         if (t < K - 1)
@@ -980,7 +980,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
                 for (int i = 0; i < NZ; ++i) {
                     const double di = d * ar[i];
                     #pragma unroll
-                    for (int j = 0; j < NZ; ++j) Hu[i * NZ + j] += di * ar[j];
+                    for (int j = i; j < NZ; ++j) Hu[i * NZ + j] += di * ar[j];
                 }
             }
             for (int r = 0; r < NS; ++r) {
@@ -992,7 +992,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
                 for (int i = 0; i < NZ; ++i) {
                     const double di = d * ar[i];
                     #pragma unroll
-                    for (int j = 0; j < NZ; ++j) Hu[i * NZ + j] += di * ar[j];
+                    for (int j = i; j < NZ; ++j) Hu[i * NZ + j] += di * ar[j];
                 }
             }
             if (Q > 0) {
@@ -1023,7 +1023,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
                         for (int i = 0; i < NZ; ++i) {
                             const double di = mm * a1[i];
                             #pragma unroll
-                            for (int j = 0; j < NZ; ++j) Hu[i * NZ + j] += di * a2[j];
+                            for (int j = i; j < NZ; ++j) Hu[i * NZ + j] += di * a2[j];
                         }
                     }
                 }
@@ -1031,7 +1031,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             #pragma unroll
             for (int i = 0; i < NZ; ++i) Hu[i * NZ + i] += T.reg;
             #pragma unroll
-            for (int e = 0; e < NZ * NZ; ++e) B[Ly.o_H + e] = Hu[e];
+            for (int e = 0; e < NZ * NZ; ++e) B[Ly.o_H + e] = Hu[e / NZ <= e % NZ ? e : (e % NZ) * NZ + e / NZ];  // upper triangle, mirrored
         }
         __syncthreads();
         SCP_TR(1)
