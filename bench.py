@@ -48,13 +48,46 @@ FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) dense peak, spec
 HBM_PEAK_GBS = 8000.0
 
 
+def foh_bytes_per_agent(n, m, K):
+    """Algorithmic HBM bytes of the FOH stage per agent (SURVEY §8(d)): read X (K,n), U (K,m), sigma;
+    write disc (K-1, n(n+2m+2)).  DI, K=50: 36,536 B."""
+    return 8 * (K * n + K * m + 1) + 8 * (K - 1) * n * (n + 2 * m + 2)
+
+
+def foh_flops_per_agent(n, m, K, nsub=1, f_flops=None):
+    """Algorithmic FLOPs of the FOH stage per agent: per RK4 step 4 RHS evaluations of
+    F + 2n^3 + 4n^2 m + 7n^2 + 7nm + 4n + 3m (F = model f/A/B, dense mat-vecs 2(n^2 + nm): DI 108) plus
+    11 L for the RK4 combination, L = n + n^2 + 2nm + 2n.  DI, K=50: 6,522 per interval-substep."""
+    F = f_flops if f_flops is not None else 2 * (n * n + n * m)
+    L = n + n * n + 2 * n * m + 2 * n
+    rhs = F + 2 * n ** 3 + 4 * n * n * m + 7 * n * n + 7 * n * m + 4 * n + 3 * m
+    return (K - 1) * nsub * (4 * rhs + 11 * L)
+
+
+def qp_bytes_per_agent(n, m, K, j_max=0, pos_dim=3):
+    """Algorithmic (interface) HBM bytes of one QP solve per agent: in disc, Xref, Uref, x_init, x_final,
+    tr, sigma (+ collision rows and counts); out X, U, shared slack, obj, status, iters.  DI, K=50, no
+    coupling: 36,640 + 4,016 = 40,656 B (~42.7 KB incl. the SCP-form outputs)."""
+    b_in = 8 * ((K - 1) * n * (n + 2 * m + 2) + K * n + K * m + 2 * n + 2)
+    b_in += (8 * K * j_max * (pos_dim + 1) + 4 * K) if j_max else 0
+    b_out = 8 * (K * n + K * m + K + 1) + 8
+    return b_in + b_out
+
+
 def qp_flops_per_ipm_iter(n, m, K, rows):
-    """Algorithmic FP64 FLOPs of one IPM iteration of one agent:
-    Riccati factor (with terminal sensitivities) + 2 solves + node-local work."""
-    factor = 2 * (3 * n ** 3 + 5 * n * n * m + 3 * n * m * m + m ** 3 / 3)
-    solve = 2 * (6 * n * n + 7 * n * m + 2 * m * m)
-    node = 2 * (8 * 12 * rows + n * n * m + n * m * m)
-    return K * (factor + 2 * solve + node)
+    """Algorithmic FP64 FLOPs of one IPM iteration of one agent, SURVEY §8(d)'s count: the block-banded
+    KKT factorization with block size b = n+m, (b^3/3 + 2 b^3) K, plus the residual / assembly work over
+    the inequality rows, 2 (n+m) FLOPs per row per node.  DI (b=9), K=50, 32 rows: 85,050 + 28,800 =
+    113,850 (~0.12 MFLOP).  The two Riccati solves per iteration are not counted: a lower bound."""
+    b = n + m
+    return K * (b ** 3 / 3 + 2 * b ** 3) + K * rows * 2 * (n + m)
+
+
+def qp_rows(n, m, n_box, n_obs, j_max, soc):
+    """Inequality rows per node of the QP template: 2^m trust-region facets, 2 per box constraint, an
+    obstacle row and its slack sign row per obstacle, j_max collision rows + 1 shared-slack row, and the
+    (m+1)-dimensional SOC counted as m+1 rows."""
+    return (1 << m) + 2 * n_box + 2 * n_obs + (j_max + 1 if j_max else 0) + ((m + 1) if soc else 0)
 
 
 def committed_traffic(kernel_prefix="scvx::qp_ipm_kernel<scvx::QPCfg<6, 3, 2, 8, 0>"):
@@ -99,10 +132,29 @@ def make_coupled(config, world, rank, device):
     return sc, t, dict(model=model, R=R, obs=obs, box=box, j_max=j_max, N_total=N_total, n_loc=n_loc)
 
 
-def cpu_baseline(sc, n_sample, threads, min_seconds=10.0, tol=1e-9):
+def host_info():
+    """What the CPU baseline ran on: nproc (CPUs this process may use), the machine's CPU count, the
+    cgroup CPU quota if one is set, and the CPU model."""
+    info = {"nproc": len(os.sched_getaffinity(0)), "cpu_count": os.cpu_count()}
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        info["cgroup_cpu_quota"] = None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        info["cgroup_cpu_quota"] = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                info["cpu_model"] = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return info
+
+
+def cpu_baseline(sc, n_sample, threads, min_seconds=8.0, tol=1e-9):
     """Time the CPU restatement (oracle) on n_sample agents: FOH + QP for one SCvx iteration,
-    repeated until about min_seconds of wall time (a bounded sample of the same workload)."""
-    import numpy as np
+    repeated until about min_seconds of wall time (a bounded sample of the same workload).
+    Returns SCvx iterations/s scaled to the N=1024-agent workload."""
     from oracle import foh_oracle, qp_cpu
     tpl = qp_cpu.make_template(6, 3, K, box=BOX, obs=sc["obs"], w_obs=1e6, u_max=U_MAX, tol=tol, max_iter=60)
     reps = 0
@@ -119,10 +171,22 @@ def cpu_baseline(sc, n_sample, threads, min_seconds=10.0, tol=1e-9):
         el = time.perf_counter() - t0
         if el >= min_seconds:
             break
-    return dict(value=reps * (n_sample / N_AGENTS) / el, unit="SCvx-iterations/s (N=1024-agent equivalent)",
-                cores=threads, kind="port",
-                sample=f"{reps} x one SCvx iteration of {n_sample} of the {N_AGENTS} agents (FOH C + structured "
-                       f"IPM C++), {el:.1f} s wall, -O3 x86-64-v3, OpenMP over agents")
+    return reps * (n_sample / N_AGENTS) / el, reps, el
+
+
+def cpu_baselines(sc, n_sample, tol):
+    """All-core (nproc threads, OpenMP over agents) and single-core CPU figures of the restatement."""
+    info = host_info()
+    threads = info["nproc"]
+    v_all, reps, el = cpu_baseline(sc, n_sample, threads, tol=tol)
+    n1 = min(n_sample, 64)
+    v_one, reps1, el1 = cpu_baseline(sc, n1, 1, tol=tol)
+    return dict(value=v_all, unit="SCvx-iterations/s (N=1024-agent equivalent)", cores=threads, kind="port",
+                sample=f"{reps} x one SCvx iteration of {n_sample} of the {N_AGENTS} agents (FOH C + structured IPM "
+                       f"C++, -O3 x86-64-v3, OpenMP over agents on {threads} threads), {el:.1f} s wall",
+                single_core={"value": v_one, "cores": 1,
+                             "sample": f"{reps1} x one SCvx iteration of {n1} agents on 1 thread, {el1:.1f} s wall"},
+                host=info)
 
 
 def is_flops_per_rollout(n, m, nsub):
@@ -187,7 +251,7 @@ def bench_intersample(args, world, rank, device):
         "vs_baseline": None, "dtype": "f64", "data": "synthetic (C3 starts/goals and spheres, SI velocities + noise)",
         "config": {"workload": "intersample: N=1024 SI agents, K=50, 8 spheres, T=I, dt=1, 100 samples, eps 1e-4",
                    "agents_per_gpu": N, "K": K, "parallelism": f"agents sharded x{world}"},
-        "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+        "roofline": {"bound": "fp64_valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None, "kernel": "intersample_kernel",
                      "kernel_ms": kms, "note": "FP64 VALU; algorithmic FLOPs = grid central differences only "
                                                "(lower bound: bisection / linearisation roll-outs not counted)"},
@@ -244,26 +308,86 @@ def bench_scproblem(args, world, rank, device):
         "cpu_baseline": cpu}), flush=True)
 
 
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(args):
+    """--gpus N > 1 without a torch.distributed environment: start the N ranks as a child process
+    (python -m torch.distributed.run, one rank per GPU, rendezvous on 127.0.0.1) before this process
+    touches the GPU, and exit with its return code."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def stage_times(marks_per_step):
+    """Per-stage milliseconds (median over steps) from the (name, event) marks of JacobiSCvx.step, and
+    the per-step GPU-timeline durations (consecutive 'start' marks, the last step to its last mark)."""
+    stages, steps = {}, []
+    for marks in marks_per_step:
+        for (n0, e0), (n1, e1) in zip(marks[:-1], marks[1:]):
+            stages.setdefault(n1, []).append(e0.elapsed_time(e1))
+        steps.append(marks[0][1].elapsed_time(marks[-1][1]))
+    return {k: float(np.median(v)) for k, v in stages.items()}, steps
+
+
+def dry_run(args, world, rank):
+    """--dry-run: the launcher / rendezvous / barrier / max-over-ranks timing path on CPU (gloo), with
+    no GPU work -- used by tests/test_bench_cpu.py to check that --gpus N really runs N ranks."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.001)
+    el_t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.barrier()
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run", "value": None, "n_gpus": world, "steps": args.steps,
+                          "ms_per_step": 1e3 * el_t.item() / args.steps, "dry_run": True}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", choices=("c3", "c4", "c5", "is", "scp"), default="c3")
     ap.add_argument("--agents", type=int, default=N_AGENTS, help="c3: agents per GPU")
     ap.add_argument("--cpu-sample", type=int, default=1024)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--tol", type=float, default=1e-9, help="IPM stopping tolerance (Clarabel's default is 1e-8)")
+    ap.add_argument("--tol", type=float, default=1e-8,
+                    help="IPM relative stopping tolerance; default = Clarabel's defaults (tol_feas = tol_gap_rel = "
+                         "1e-8), the solver of the reference's dist_scvx_3d.py:110")
+    ap.add_argument("--dry-run", action="store_true", help="launcher/rendezvous check on CPU, no GPU work")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        return dry_run(args, world, rank)
 
     import torch
     import torch.distributed as dist
     import scvx_hip
     from scvx_hip.scvx import CouplingSpec, JacobiSCvx
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -291,8 +415,8 @@ def main():
                          tr_rule="global")
     X, U = w["X"].clone(), w["U"].clone()
 
-    def step(X, U, ev=None):
-        Xn, Un, out = drv.step(X, U, qp_events=ev)
+    def step(X, U, marks=None):
+        Xn, Un, out = drv.step(X, U, marks=marks)
         X.copy_(Xn)
         U.copy_(Un)
         return out
@@ -303,14 +427,17 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    # timed region: exactly K steps (the same code path as the warmup); the QP kernel is bracketed
-    # by HIP events on its launch stream
-    qp_ms = []
-    iters = []
+    # timed region: exactly `steps` steps (the same code path as the warmup); every stage is bracketed
+    # by HIP events on the launch stream (the QP kernel's mark pair gives its launch duration)
+    marks, iters, checks = [], [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out = step(X, U, qp_ms)
+        mk = []
+        out = step(X, U, mk)
+        marks.append(mk)
         iters.append(out["iters"].sum())
+        if drv.last_check is not None:
+            checks.append(dict(drv.last_check))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -320,17 +447,34 @@ def main():
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     el = el_t.item()
-    qp_avg_ms = sum(a.elapsed_time(b) for a, b in qp_ms) / len(qp_ms)
+    st_ms, step_ms = stage_times(marks)
+    if world > 1:   # every rank's stage medians (the all-gather time per rank for c4/c5)
+        mine = torch.tensor([st_ms.get(k, 0.0) for k in ("foh", "gather", "rows", "qp", "check", "update")],
+                            dtype=torch.float64, device=device)
+        allr = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = [r.tolist() for r in allr]
+    else:
+        per_rank = None
+    qp_ms = st_ms["qp"]
     ipm_iters = float(torch.stack(iters).sum().item())
+    it_agent = ipm_iters / (args.steps * N)
     status = out["status"].cpu()
-    rows = (1 << m) + 2 * len(box) + 2 * n_obs + 2 * j_max
-    flops = qp_flops_per_ipm_iter(n, m, K, rows) * ipm_iters / args.steps
-    achieved = flops / (qp_avg_ms * 1e-3) / 1e12
+    rows = qp_rows(n, m, len(box), n_obs, j_max, args.config == "c3")
+    qp_flops = qp_flops_per_ipm_iter(n, m, K, rows) * ipm_iters / args.steps          # per launch
+    qp_bytes = qp_bytes_per_agent(n, m, K, j_max) * N
+    foh_bytes = foh_bytes_per_agent(n, m, K) * N
+    foh_flops = foh_flops_per_agent(n, m, K, nsub=scvx_hip.DEFAULT_NSUB[model]) * N
+    achieved = qp_flops / (qp_ms * 1e-3) / 1e12
+    qp_gbs = qp_bytes / (qp_ms * 1e-3) / 1e9
+    t_step = el / args.steps
+    t_min = (max(foh_bytes / (HBM_PEAK_GBS * 1e9), foh_flops / (FP64_PEAK_TFLOPS * 1e12))
+             + max(qp_bytes / (HBM_PEAK_GBS * 1e9), qp_flops / (FP64_PEAK_TFLOPS * 1e12)))
     traffic, traffic_src = committed_traffic() if args.config == "c3" else (None, None)
     if rank == 0:
         cpu = None
         if not args.no_cpu and args.config == "c3":
-            cpu = cpu_baseline(sc, min(args.cpu_sample, N), threads=min(16, os.cpu_count() or 1), tol=args.tol)
+            cpu = cpu_baselines(sc, min(args.cpu_sample, N), tol=args.tol)
         if args.config == "c3":
             value, scaling = world * args.steps / el, "weak"
             metric = "SCvx-iterations/sec, N agents x K=50 nodes (N=1024 per GPU)"
@@ -344,8 +488,9 @@ def main():
                     if args.config == "c4" else
                     "synthetic (C5 construction: quadrotors from hover, seeded starts/goals, 8 spheres)")
             workload = (f"{args.config.upper()}: N={cfg['N_total']} agents ({N}/GPU), model {model} n={n} m={m}, "
-                        f"K=50, pairwise coupling R={cfg['R']} (j_max={j_max} nearest per node, one shared slack), "
-                        f"{n_obs} obstacles, box |x|,|y|<={box[0][2]:g}, global trust-region rule, RCCL all_gather of states")
+                        f"K=50, pairwise coupling R={cfg['R']} (j_max={j_max} nearest rows per node in the solve, "
+                        f"every other row checked at the solution and violators re-solved with 32), {n_obs} "
+                        f"obstacles, box |x|,|y|<={box[0][2]:g}, global trust-region rule, RCCL all_gather of states")
         line = {
             "metric": metric,
             "value": value,
@@ -353,24 +498,36 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": 1e3 * el / args.steps,
+            "ms_per_step": 1e3 * t_step,
+            "ms_per_step_median": float(np.median(step_ms)),
             "higher_is_better": True,
             "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": data,
             "config": {"workload": workload, "agents_per_gpu": N, "K": K, "parallelism": f"agents sharded x{world}"},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "roofline": {"bound": "fp64_valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                          "traffic_unit": "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE)", "traffic_source": traffic_src,
-                         "kernel": "qp_ipm_kernel", "kernel_ms": qp_avg_ms,
-                         "note": "FP64 VALU-bound small dense linear algebra; peak = FP64 dense peak; "
-                                 "algorithmic FLOPs per DESIGN.md §4 x executed IPM iterations"},
-            "ipm_iters_per_agent": ipm_iters / (args.steps * N),
+                         "kernel": "qp_ipm_kernel", "kernel_ms": qp_ms,
+                         "algorithmic_flops_per_launch": qp_flops, "algorithmic_bytes_per_launch": qp_bytes,
+                         "hbm_achieved_gbs": qp_gbs, "hbm_frac": qp_gbs / HBM_PEAK_GBS,
+                         "note": "FP64-VALU small dense linear algebra (no MFMA: 6x6 / 6x3 f64 blocks); peak = FP64 "
+                                 "dense peak; FLOPs = SURVEY §8(d) count (bench.qp_flops_per_ipm_iter) x executed IPM "
+                                 "iterations; bytes = interface bytes (bench.qp_bytes_per_agent)"},
+            "step_roofline": {"hbm_frac": (foh_bytes + qp_bytes) / (t_step * HBM_PEAK_GBS * 1e9),
+                              "fp64_frac": (foh_flops + qp_flops) / (t_step * FP64_PEAK_TFLOPS * 1e12),
+                              "t_min_ms": 1e3 * t_min, "t_min_over_t": t_min / t_step,
+                              "algorithmic_bytes_per_step": foh_bytes + qp_bytes,
+                              "algorithmic_flops_per_step": foh_flops + qp_flops},
+            "stage_ms_median": st_ms,
+            "stage_ms_per_rank": per_rank,
+            "ipm_iters_per_agent": it_agent,
             "ipm_iters_max_last": int(out["iters"].max().item()),
             "ipm_iters_hist_last": {str(int(v)): int(c) for v, c in zip(*np.unique(out["iters"].cpu().numpy(),
                                                                                   return_counts=True))},
             "status_counts": {str(k): int((status == k).sum()) for k in (0, 1, 2)},
+            "coupling_check": checks or None,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -49,7 +49,7 @@ def x_traj_opt(X_traj, trust_region):
     if jmax > 0:
         rows, count = scvx_hip.collision_rows(Xd, 0, N, R, jmax, pos_dim=3, cull_radius=0.0)
     spec = scvx_hip.QPSpec(model="di", K=T, pos_dim=3, has_final=True, fix_last_input=True,
-                           box=[(0, -1.0, 22.0), (1, -1.0, 20.0)], j_max=jmax, w_coll=10000.0, tol=1e-9,
+                           box=[(0, -1.0, 22.0), (1, -1.0, 20.0)], j_max=jmax, w_coll=10000.0, tol=1e-8,
                            max_iter=80)
     out = scvx_hip.qp_solve_batched(spec, t_(np.broadcast_to(disc, (N,) + disc.shape)), t_(np.zeros(N)), Xd,
                                     t_(Ur), t_(Xr[:, 0]), t_(np.stack([x_des[nm][0:n] for nm in names])),

@@ -39,7 +39,10 @@ class _Leaf:
             self._value = None
             return
         a = np.asarray(v, dtype=float)
-        if a.shape != self.shape and a.size == int(np.prod(self.shape)):
+        # only singleton axes may differ ((K,) vs (K, 1), a 1-element array for a scalar): any other
+        # mismatch -- a transposed (K, n) trajectory for an (n, K) parameter -- is a caller bug that
+        # cvxpy rejects, and reshaping it would scramble the data silently
+        if a.shape != self.shape and tuple(d for d in a.shape if d != 1) == tuple(d for d in self.shape if d != 1):
             a = a.reshape(self.shape)
         if a.shape != self.shape:
             raise ValueError(f"Invalid dimensions {a.shape} for {type(self).__name__} value of shape {self.shape}.")

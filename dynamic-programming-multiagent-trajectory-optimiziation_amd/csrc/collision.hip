@@ -9,8 +9,11 @@
 //
 // Exact mode (cull_radius <= 0 and j_max >= N_total-1) reproduces the reference's full neighbour
 // set.  With culling only neighbours closer than cull_radius are kept, and at most j_max of them
-// per node (the closest ones, i.e. the rows with the largest violation S); the QP is then exact
-// whenever the culled rows stay inactive, which the host layer verifies after the solve.
+// per node (the closest ones, i.e. the rows with the largest violation S).  The culled QP is a
+// relaxation of the reference's (it drops rows), so its solution is the reference's solution
+// whenever it also satisfies every dropped row: collision_check_kernel below evaluates ALL
+// N_total-1 rows of every node at the solution, and the host (scvx_hip/scvx.py JacobiSCvx)
+// re-solves the agents with a violated row at a larger j_max, flagging any that still violate.
 //
 // Mapping: one workgroup per (node t, block of 64 local agents), lane = local agent.  All lanes scan
 // the same neighbour sequence j = 0..N_total-1, so node t's positions of a tile of TJ neighbours are
@@ -115,7 +118,81 @@ __global__ __launch_bounds__(64) void collision_rows_kernel(int K, int pd, int n
     count[a * K + t] = n;
 }
 
+// A-posteriori check of the full reference row set at a solution (dist_scvx_3d.py:93-107):
+//     (2R - ||pbar_i - pbar_j||) - g_ij' (p_t - pbar_i) <= S_t     for every j != i, t < K-1
+// with pbar the linearisation point (X_all, the previous iterate of every agent), p_t the solved
+// position of local agent i and S_t its solved shared slack.  Same mapping as collision_rows_kernel
+// (workgroup = (node t, 64 local agents), neighbour positions staged in LDS).  Per (agent, node):
+// the number of rows violated by more than tol and the largest violation.
+__global__ __launch_bounds__(64) void collision_check_kernel(int K, int pd, int nx, int N_total, int N_local,
+                                                             const double* __restrict__ X_all, int i0, double R,
+                                                             const double* __restrict__ X_new,
+                                                             const double* __restrict__ slack, double tol,
+                                                             int32_t* __restrict__ viol, double* __restrict__ vmax) {
+    __shared__ double tile[COLL_TJ * 3];
+    const int lane = threadIdx.x;
+    const int t = blockIdx.y;
+    const long long a = (long long)blockIdx.x * 64 + lane;
+    const bool live = a < N_local;
+    const long long gi = i0 + a;
+    if (t >= K - 1) {
+        if (live) { viol[a * K + t] = 0; vmax[a * K + t] = 0.0; }
+        return;
+    }
+    double pi[3] = {0, 0, 0}, dp[3] = {0, 0, 0}, S = 0.0;
+    if (live) {
+        for (int d = 0; d < pd; ++d) {
+            pi[d] = X_all[(gi * K + t) * nx + d];
+            dp[d] = X_new[(a * K + t) * nx + d] - pi[d];
+        }
+        S = slack[a * K + t];
+    }
+    int nv = 0;
+    double worst = -1e300;
+    const double rr = 2.0 * R;
+    for (int j0 = 0; j0 < N_total; j0 += COLL_TJ) {
+        const int nt = min(COLL_TJ, N_total - j0);
+        __syncthreads();
+        for (int e = lane; e < nt * pd; e += 64) {
+            const int jj = e / pd, d = e - jj * pd;
+            tile[jj * 3 + d] = X_all[((long long)(j0 + jj) * K + t) * nx + d];
+        }
+        __syncthreads();
+        if (!live) continue;
+#pragma unroll 4
+        for (int jj = 0; jj < nt; ++jj) {
+            if (j0 + jj == gi) continue;
+            double d2 = 0.0, gd = 0.0;
+            for (int d = 0; d < pd; ++d) {
+                const double df = pi[d] - tile[jj * 3 + d];
+                d2 += df * df;
+                gd += df * dp[d];
+            }
+            const double nr = sqrt(d2);
+            const double v = (rr - nr) - gd / nr - S;  // NaN for coincident agents, as the reference's 0/0
+            worst = (v > worst || v != v) ? v : worst;
+            nv += (v > tol || v != v) ? 1 : 0;
+        }
+    }
+    if (!live) return;
+    viol[a * K + t] = nv;
+    vmax[a * K + t] = worst;
+}
+
 }  // namespace scvx
+
+extern "C" int scvx_collision_check_batched(int K, int pos_dim, int n_x, int N_total, const double* X_all, int i0,
+                                            int N_local, double R, const double* X_new, const double* slack,
+                                            double tol, int32_t* viol, double* vmax, void* stream) {
+    if (K < 2 || K > 64 || pos_dim < 1 || pos_dim > 3 || pos_dim > n_x || N_total < 0 || N_local < 0 || i0 < 0 ||
+        i0 + N_local > N_total || !X_all || !X_new || !slack || !viol || !vmax)
+        return scvx::set_error(SCVX_EINVAL, "collision_check: bad args");
+    if (N_local == 0) return SCVX_OK;
+    const dim3 grid((unsigned)((N_local + 63) / 64), (unsigned)K);
+    hipLaunchKernelGGL(scvx::collision_check_kernel, grid, dim3(64), 0, (hipStream_t)stream, K, pos_dim, n_x, N_total,
+                       N_local, X_all, i0, R, X_new, slack, tol, viol, vmax);
+    return scvx::check_launch("collision_check_kernel");
+}
 
 extern "C" int scvx_collision_rows_batched(int K, int pos_dim, int n_x, int N_total, const double* X_all, int i0,
                                            int N_local, double R, double cull_radius, int j_max, double* rows,

@@ -74,6 +74,9 @@ size_t ws_bytes(const ModelTable& mt, int cls, int N) {
 // Diagnostics hook (not part of the solve contract): subsequent scvx_qp_solve_batched launches write
 // 8 doubles per IPM iteration of agent `agent` into the device buffer (pres, dres, gap, pobj,
 // alpha_aff, alpha, sigma, mu), then 4 doubles (factor cycles, solve cycles, total cycles, fail code).
+// agent < 0: one double per agent instead, its exit code (0 converged, 1 start-point factorization,
+// 2 terminal Schur complement, 3 non-finite residual, 4 non-finite direction, 5 iteration cap,
+// 6 stall at reduced accuracy).
 extern "C" int scvx_qp_set_trace(double* buf, int agent, int cap) {
     g_trace = buf; g_trace_agent = agent; g_trace_cap = buf ? cap : 0;
     return SCVX_OK;

@@ -226,9 +226,7 @@ __device__ __forceinline__ void qp_phase(double* lds, const int (&d)[NREP][4], i
         const double old = lds[oo];
         lds[oo] = (on && ((O >> 15) & 1)) ? old + val[r] : val[r];
         const int g = on ? (O >> 17) - 1 : -1;
-#ifndef QPX_NOGST
         wb.st(g >= 0 ? g * 8 : vsink, fbo, val[r]);
-#endif
     }
 }
 
@@ -244,11 +242,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     const bool act = t < K;
     const bool ineq = act && ((t < K - 1) || T.ineq_last);
     const bool fin = T.has_final != 0;
-#ifdef QPX_NOSOC
-    const bool soc = false;
-#else
     const bool soc = ineq && T.has_soc;
-#endif
     const bool has_coll = NC > 0 && T.j_max > 0;
     const int nobs = T.n_obs, nbox = T.n_box;
     const int ccount = (ineq && has_coll) ? min((int)a.coll_count[agent * K + t], min(T.j_max, NC)) : 0;
@@ -408,9 +402,6 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     // LDS.  false on a breakdown.
     constexpr int PFN = (PKT + WAVE - 1) / WAVE;
     auto factor = [&]() __attribute__((always_inline)) -> bool {
-#ifdef QPX_NOFACTOR
-        return true;
-#endif
         // phase descriptors (rebuilt per call: nothing of them stays live outside the sweep)
         constexpr int E1 = 2 * NX * NX + 2 * NX * NU + 2 * NX, E2 = NX * NX + NU * NX + NU * NU, E4 = 4 * NX * NX;
         constexpr int R1 = (E1 + WAVE - 1) / WAVE, R2 = (E2 + WAVE - 1) / WAVE, R4 = (E4 + WAVE - 1) / WAVE;
@@ -591,9 +582,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                     for (int i = 0; i < NU; ++i) {
                         const double v = fx ? 0.0 : -x[i];
                         lds[kl ? C::F_KK + c * NU + i : C::F_SINK] = v;
-#ifndef QPX_NOGST
                         wb.st(kl ? (g + i * NX) * 8 : SKB - fbo + lane * 8, fbo, v);
-#endif
                     }
                 }
                 {
@@ -603,9 +592,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                         const int ei = e / NU, ej = e % NU;
                         v = fma(qp_mask(e, lane), (ei > ej) ? Lm[e] : (ei == ej ? dinv[ei] : 0.0), v);
                     }
-#ifndef QPX_NOGST
                     wb.st(lane < NU * NU ? (C::B_LD + lane) * 8 : SKB - fbo + lane * 8, fbo, v);
-#endif
                 }
             }
             wsync();
@@ -679,11 +666,6 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     // Out: dzo (NZ) = (dx_t, du_t), dyo (NX) = dy_t of this lane; V_DYI / V_DYF (LDS) the
     // initial / terminal multiplier directions.  Assumes a __syncthreads() since the factor.
     auto solve = [&](const double* q, const double* r, double* dzo, double* dyo) __attribute__((always_inline)) {
-#ifdef QPX_NOSOLVE
-        for (int i = 0; i < NZ; ++i) dzo[i] = q[i % NX] * r[0];
-        for (int i = 0; i < NX; ++i) dyo[i] = q[i];
-        return;
-#endif
         // ---- backward pre-pass: g = q + K'r + Acl'(P_{t+1} e)
         fresh();
         if (act) {
@@ -1321,7 +1303,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         double q[NX], rr[NU];
         reduce_rhs(r1, r1a, q, rr);
         set_boundary(z);
-        if (!factor()) status = SCVX_STATUS_NUMERICAL;
+        if (!factor()) { status = SCVX_STATUS_NUMERICAL; fail_code = 1.0; }
         __syncthreads();  // factor columns (global) -> lane-parallel solve passes
         double dz[NZ], dy[NX], da[NGA];
         solve(q, rr, dz, dy);
@@ -1373,7 +1355,10 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     // ------------------------------------------------------------------ IPM iterations
     const long long cyc_all0 = __builtin_amdgcn_s_memtime();
     stamp(-1);
-    for (it = 0; it < T.max_iter && status != SCVX_STATUS_NUMERICAL; ++it) {
+    // the residuals are evaluated once more after the last step: an iterate that reaches the
+    // iteration cap is reported `optimal_inaccurate` only if it meets the reduced tolerances below,
+    // otherwise `solver_error` (ECOS / Clarabel report a cap far from optimal as a failure too)
+    for (it = 0; status != SCVX_STATUS_NUMERICAL; ++it) {
         fresh();
         double dt[C::DSTR], Cpr[NX * NU];
         issue_state();
@@ -1483,6 +1468,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         // usable if it meets the reduced tolerances of the reference's solvers (Clarabel / ECOS:
         // feasibility 1e-4, gap 5e-5 relative)
         const bool near = pres <= 1e-4 * hsc && dres <= 1e-4 * qscl && gap <= 5e-5 * fmax(1.0, fabs(pobj));
+        if (it >= T.max_iter) {
+            status = near ? SCVX_STATUS_MAX_ITER : SCVX_STATUS_NUMERICAL;
+            fail_code = 5.0;
+            break;
+        }
         // SOC Nesterov-Todd scaling (hyperbolic-rotation form, W lam = W^-1 s)
         double Wi2uu[NU * NU];
 #pragma unroll
@@ -1726,6 +1716,14 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 fail_code = 4.0;
                 break;
             }
+            // stall at reduced accuracy: once the barrier Hessians span ~1e12 the Newton direction loses
+            // its dual accuracy and the step collapses; keep the current (reduced-tolerance) iterate
+            // rather than stepping along a direction that can break the next factorization
+            if (near && al < 1e-2) {
+                status = SCVX_STATUS_MAX_ITER;
+                fail_code = 6.0;
+                break;
+            }
         }
         if (a.trace && agent == a.trace_agent && lane == 0 && it < a.trace_cap) {
             double* tr_ = a.trace + 8 * it;
@@ -1784,6 +1782,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         a.obj[agent] = pobj;
         a.status[agent] = status;
         a.iters[agent] = it;
+        if (a.trace && a.trace_agent < 0) a.trace[agent] = fail_code;  // diagnostics: every agent's exit code
     }
 }
 

@@ -7,6 +7,7 @@ kernels run on torch's current HIP stream, nothing falls back to the CPU.
                            (SCvx/discretization/first_order_hold.py:52-87)
     integrate_nonlinear    FirstOrderHold.integrate_nonlinear_piecewise / _full (:127-155)
     collision_rows         linearized pairwise collision rows (Distributed_opt/dist_scvx_3d.py:93-107)
+    collision_check        every reference collision row evaluated at a (culled) solution
     qp_solve_batched       the per-agent trust-region subproblem (dist_scvx_3d.py:51-111)
     QPSpec                 problem template of qp_solve_batched
     SCPSpec / SCPSolver    the SCvx convex subproblem SCProblem (+ AgentSolver ADMM terms)
@@ -24,7 +25,7 @@ from ._lib import MODEL_DIMS, MODEL_IDS, STATUS, QPTemplate, SCPTemplate, ScvxEr
 DEFAULT_NSUB = {"di": 1, "si": 1, "unicycle": 16, "quad": 16}
 QUAD_PARAMS = (1.0, 9.81, 0.02, 0.02, 0.04)
 
-__all__ = ["foh_batched", "integrate_nonlinear", "collision_rows", "qp_solve_batched", "QPSpec", "SCPSpec", "SCPSolver",
+__all__ = ["foh_batched", "integrate_nonlinear", "collision_rows", "collision_check", "qp_solve_batched", "QPSpec", "SCPSpec", "SCPSolver",
            "intersample_batched",
            "disc_stride", "unpack_disc", "ScvxError", "MODEL_DIMS", "DEFAULT_NSUB"]
 
@@ -83,6 +84,9 @@ def foh_batched(model, X, U, sigma, nsub=None, params=None, out=None, stream=Non
     m = U.shape[2]
     if (n, m) != MODEL_DIMS[model]:
         raise ValueError(f"{model}: expected n,m={MODEL_DIMS[model]}, got {(n, m)}")
+    if tuple(U.shape[:2]) != (N, K) or tuple(sigma.shape) != (N,):
+        raise ValueError(f"foh_batched: U (N,K,m) and sigma (N,) must match X (N,K,n); got "
+                         f"{tuple(U.shape)}, {tuple(sigma.shape)}")
     if out is None:
         out = torch.empty((N, K - 1, disc_stride(model)), dtype=torch.float64, device=X.device)
     keep, pp = _params(model, params)
@@ -97,6 +101,12 @@ def integrate_nonlinear(model, X, U, sigma, piecewise, nsub=16, params=None, out
     """Batched FirstOrderHold.integrate_nonlinear_piecewise (piecewise=True) / _full (False)."""
     torch = _torch()
     N, K, n = X.shape
+    m = U.shape[2] if U.dim() == 3 else -1
+    if (n, m) != MODEL_DIMS[model]:
+        raise ValueError(f"{model}: expected n,m={MODEL_DIMS[model]}, got {(n, m)}")
+    if tuple(U.shape[:2]) != (N, K) or tuple(sigma.shape) != (N,):
+        raise ValueError(f"integrate_nonlinear: U (N,K,m) and sigma (N,) must match X (N,K,n); got "
+                         f"{tuple(U.shape)}, {tuple(sigma.shape)}")
     if out is None:
         out = torch.empty_like(X)
     keep, pp = _params(model, params)
@@ -122,6 +132,27 @@ def collision_rows(X_all, i0, n_local, R, j_max, pos_dim=3, cull_radius=0.0, row
     return rows, count
 
 
+def collision_check(X_all, i0, X_new, slack, R, pos_dim=3, tol=1e-7, viol=None, vmax=None, stream=None):
+    """Evaluate EVERY reference collision row (dist_scvx_3d.py:93-107) of local agents
+    [i0, i0+N_local) at a solution X_new (N_local,K,n) with shared slacks slack (N_local,K), linearised
+    at X_all (N_total,K,n).  Returns device tensors viol (N_local,K) int32 = rows violated by more
+    than tol, vmax (N_local,K) = largest row value (scvx_collision_check_batched)."""
+    torch = _torch()
+    N_total, K, n = X_all.shape
+    n_local = X_new.shape[0]
+    if tuple(X_new.shape) != (n_local, K, n) or tuple(slack.shape) != (n_local, K):
+        raise ValueError("collision_check: X_new (N_local,K,n) and slack (N_local,K) expected")
+    if viol is None:
+        viol = torch.empty((n_local, K), dtype=torch.int32, device=X_all.device)
+    if vmax is None:
+        vmax = torch.empty((n_local, K), dtype=torch.float64, device=X_all.device)
+    rc = lib().scvx_collision_check_batched(K, pos_dim, n, N_total, _dev(X_all, name="X_all"), int(i0), int(n_local),
+                                            float(R), _dev(X_new, name="X_new"), _dev(slack, name="slack"), float(tol),
+                                            _dev(viol, torch.int32, "viol"), _dev(vmax, name="vmax"), _stream(stream))
+    check(rc, "scvx_collision_check_batched")
+    return viol, vmax
+
+
 @dataclass
 class QPSpec:
     """Template of the batched trust-region subproblem (include/scvx_hip.h scvx_qp_template)."""
@@ -139,7 +170,9 @@ class QPSpec:
     w_coll: float = 1e4
     u_max: Optional[float] = None
     max_iter: int = 60
-    tol: float = 1e-9
+    # relative stopping tolerance (primal / dual residual and gap); 1e-8 is Clarabel's default
+    # (tol_feas = tol_gap_rel = tol_gap_abs = 1e-8), the solver dist_scvx_3d.py:110 calls
+    tol: float = 1e-8
 
     def to_c(self):
         n, m = MODEL_DIMS[self.model]
@@ -184,9 +217,33 @@ class QPSolver:
         self._dummy = torch.zeros(1, dtype=torch.float64, device=device)
         self._dummy_i = torch.zeros(1, dtype=torch.int32, device=device)
 
+    def _check_shapes(self, disc, sigma, Xref, Uref, x_init, x_final, tr, coll_rows, coll_count):
+        """Host-side shape checks: the kernel indexes every buffer with the template's compile-time
+        dimensions, so a mis-shaped tensor would be read out of bounds on the device."""
+        spec, N = self.spec, self.N
+        n, m = MODEL_DIMS[spec.model]
+        K = spec.K
+        want = {"disc": (disc, (N, K - 1, disc_stride(spec.model))), "sigma": (sigma, (N,)),
+                "Xref": (Xref, (N, K, n)), "Uref": (Uref, (N, K, m)), "x_init": (x_init, (N, n)),
+                "tr": (tr, (N,))}
+        if spec.has_final:
+            if x_final is None:
+                raise ValueError("QPSolver.solve: the template has a terminal condition; x_final is required")
+            want["x_final"] = (x_final, (N, n))
+        if spec.j_max > 0:
+            if coll_rows is None or coll_count is None:
+                raise ValueError(f"QPSolver.solve: spec.j_max={spec.j_max} needs coll_rows and coll_count "
+                                 "(scvx_hip.collision_rows)")
+            want["coll_rows"] = (coll_rows, (N, K, spec.j_max, spec.pos_dim + 1))
+            want["coll_count"] = (coll_count, (N, K))
+        for name, (t, shp) in want.items():
+            if tuple(t.shape) != shp:
+                raise ValueError(f"QPSolver.solve: {name} has shape {tuple(t.shape)}, expected {shp}")
+
     def solve(self, disc, sigma, Xref, Uref, x_init, x_final, tr, coll_rows=None, coll_count=None, stream=None):
         torch = _torch()
-        if coll_rows is None:
+        self._check_shapes(disc, sigma, Xref, Uref, x_init, x_final, tr, coll_rows, coll_count)
+        if self.spec.j_max == 0:
             coll_rows, coll_count = self._dummy, self._dummy_i
         xf = x_final if x_final is not None else self._dummy
         rc = lib().scvx_qp_solve_batched(

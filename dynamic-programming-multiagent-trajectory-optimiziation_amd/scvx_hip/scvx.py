@@ -11,10 +11,11 @@ update/bookkeeping.  Multi-GPU: agents are sharded contiguously over ranks; the 
 collective is one all_gather of the states per iteration (RCCL over xGMI), needed only when
 collision coupling is on, plus one scalar all_reduce for the global trust-region rule.
 """
+import dataclasses
 from dataclasses import dataclass
 from typing import Optional
 
-from . import (DEFAULT_NSUB, MODEL_DIMS, QPSolver, QPSpec, collision_rows, foh_batched)
+from . import (DEFAULT_NSUB, MODEL_DIMS, QPSolver, QPSpec, collision_check, collision_rows, foh_batched)
 
 
 class HipBackend:
@@ -26,14 +27,26 @@ class HipBackend:
     def collision_rows(self, X_all, i0, n_local, R, j_max, pos_dim, cull, rows, count):
         return collision_rows(X_all, i0, n_local, R, j_max, pos_dim, cull, rows, count)
 
+    def collision_check(self, X_all, i0, X_new, slack, R, pos_dim, tol):
+        return collision_check(X_all, i0, X_new, slack, R, pos_dim, tol)
+
     def qp_solver(self, spec, N, device):
         return QPSolver(spec, N, device=device)
 
 
 @dataclass
 class CouplingSpec:
+    """Collision coupling of dist_scvx_3d.py:93-107.  The QP keeps the spec.j_max nearest rows per
+    node; with check=True every dropped row is evaluated at the solution (collision_check) and the
+    agents that violate one are re-solved with the j_max_hi nearest rows.  The culled problem is a
+    relaxation of the reference's, so a solution that satisfies every row IS the reference's; agents
+    still violating after the re-solve (more binding neighbours than j_max_hi) are counted in
+    JacobiSCvx.last_check["overflow"]."""
     R: float = 2.3              # agent radius (dist_scvx_3d.py:211); rows use 2R
     cull_radius: float = 0.0    # <= 0: every neighbour (exact reference semantics)
+    check: bool = True          # evaluate every reference row at the solution
+    j_max_hi: int = 32          # nearest rows of the re-solve (the largest QP capacity class)
+    check_tol: float = 1e-7     # row violation threshold (metres)
 
 
 class JacobiSCvx:
@@ -62,6 +75,7 @@ class JacobiSCvx:
         self.prev_cost = torch.full((self.N,), float("inf"), dtype=torch.float64, device=self.device)
         self.prev_total = torch.full((1,), float("inf"), dtype=torch.float64, device=self.device)
         self.disc = None
+        self.last_check = None
         self.world = 1
         self.rank = 0
         if group is not None or (torch.distributed.is_available() and torch.distributed.is_initialized()):
@@ -76,6 +90,40 @@ class JacobiSCvx:
                                     device=self.device)
             self.count = torch.zeros((self.N, spec.K), dtype=torch.int32, device=self.device)
 
+    def _enforce_all_rows(self, X_all, X, U, out):
+        """Make the culled coupling exact: evaluate every reference row at the solution, re-solve the
+        violating agents with the j_max_hi nearest rows, count what still violates (overflow)."""
+        torch, spec, c = self.torch, self.spec, self.coupling
+        ok = out["status"] != 2
+
+        def violators():
+            viol, _ = self.backend.collision_check(X_all, self.i0, out["X"], out["slack_coll"], c.R, spec.pos_dim,
+                                                   c.check_tol)
+            return (viol.sum(dim=1) > 0) & ok
+
+        bad = violators()
+        n_bad = int(bad.sum().item())   # one host read per SCvx iteration
+        self.last_check = {"violated": n_bad, "resolved": 0, "overflow": n_bad}
+        if n_bad == 0 or spec.j_max >= c.j_max_hi:
+            return out
+        idx = bad.nonzero().flatten()
+        spec_hi = dataclasses.replace(spec, j_max=c.j_max_hi)
+        rows_hi = torch.zeros((self.N, spec.K, c.j_max_hi, spec.pos_dim + 1), dtype=torch.float64, device=self.device)
+        count_hi = torch.zeros((self.N, spec.K), dtype=torch.int32, device=self.device)
+        self.backend.collision_rows(X_all, self.i0, self.N, c.R, c.j_max_hi, spec.pos_dim, c.cull_radius, rows_hi,
+                                    count_hi)
+        g = lambda t: t.index_select(0, idx).contiguous()  # noqa: E731
+        sub = self.backend.qp_solver(spec_hi, n_bad, self.device)
+        o2 = sub.solve(g(self.disc), g(self.sigma), g(X), g(U), g(self.x_init), g(self.x_final), g(self.tr),
+                       g(rows_hi), g(count_hi))
+        out = {k: v.clone() for k, v in out.items()}
+        for k in ("X", "U", "slack_coll", "obj", "status", "iters"):
+            out[k].index_copy_(0, idx, o2[k])
+        ok = out["status"] != 2
+        still = int(violators().sum().item())
+        self.last_check.update(resolved=n_bad - still, overflow=still)
+        return out
+
     def gather_states(self, X):
         """All-gather the local states (N,K,n) into X_all (N_total,K,n) -- RCCL over xGMI."""
         if self.world == 1:
@@ -84,25 +132,36 @@ class JacobiSCvx:
             self.torch.distributed.all_gather_into_tensor(self.X_all, X.contiguous(), group=self.group)
         return self.X_all
 
-    def step(self, X, U, qp_events=None):
+    def _mark(self, marks, name):
+        """Record a timing event named `name` on the current (launch) stream (marks: list or None)."""
+        if marks is not None:
+            e = self.torch.cuda.Event(enable_timing=True)
+            e.record(self.torch.cuda.current_stream())
+            marks.append((name, e))
+
+    def step(self, X, U, marks=None):
         """One SCvx iteration; returns the new (X, U) and the raw solver outputs.
-        qp_events: optional list; a (start, end) pair of timing events recorded on the launch
-        stream around the QP kernel is appended to it."""
+        marks: optional list; (stage, event) pairs are appended on the launch stream -- "start", then
+        the end of "foh", "gather" (all-gather), "rows" (collision rows), "qp" (the QP kernel),
+        "check" (full-row check + re-solve) and "update" (bookkeeping); a stage's time is the
+        difference to the previous mark."""
         torch = self.torch
         spec = self.spec
+        self._mark(marks, "start")
         self.disc = self.backend.foh(spec.model, X, U, self.sigma, self.nsub, self.disc)
-        rows = count = None
+        self._mark(marks, "foh")
+        rows = count = X_all = None
         if self.coupling is not None:
             X_all = self.gather_states(X)
+            self._mark(marks, "gather")
             rows, count = self.backend.collision_rows(X_all, self.i0, self.N, self.coupling.R, spec.j_max,
                                                       spec.pos_dim, self.coupling.cull_radius, self.rows, self.count)
-        if qp_events is not None:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(torch.cuda.current_stream())
+            self._mark(marks, "rows")
         out = self.solver.solve(self.disc, self.sigma, X, U, self.x_init, self.x_final, self.tr, rows, count)
-        if qp_events is not None:
-            e1.record(torch.cuda.current_stream())
-            qp_events.append((e0, e1))
+        self._mark(marks, "qp")
+        if self.coupling is not None and self.coupling.check:
+            out = self._enforce_all_rows(X_all, X, U, out)
+            self._mark(marks, "check")
         # an agent whose subproblem failed numerically (status 2) rejects the step: it keeps its
         # iterate (its output may be non-finite and would otherwise reach every other agent through
         # the collision all-gather) and halves its own trust radius so the next subproblem differs.
@@ -124,4 +183,5 @@ class JacobiSCvx:
             self.tr.mul_(1.0 - 0.5 * shrink)
             self.prev_cost.copy_(cost)
         self.tr.mul_(1.0 - 0.5 * failed.to(torch.float64))
+        self._mark(marks, "update")
         return Xn, Un, out

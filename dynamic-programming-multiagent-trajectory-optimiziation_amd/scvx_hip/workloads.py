@@ -4,7 +4,8 @@
                        warm start (as x_initial, Distributed_opt/dist_scvx_3d.py:122-128), U = 0,
                        optional spheres (centres U[-8, 8]^3, radii U[0.5, 1.5]).
     synthetic_lattice  C4: starts on a cubic lattice whose spacing exceeds 2R (dist_scvx_3d.py:211),
-                       goals a random permutation of the lattice sites, so straight paths cross.
+                       goals a random permutation of the lattice sites inside 2x2x2 cells, so straight
+                       paths cross (and every goal is reachable under the trust region).
     synthetic_quad     C5: 12-state quadrotor (models.hpp Quadrotor) from hover: positions as C2,
                        attitude / rates 0, U = hover thrust (m g, 0, 0, 0).
 
@@ -39,12 +40,23 @@ def synthetic_di(N, K=50, seed=0, sigma=30.0, spread=10.0, obstacles=0, obs_seed
                 obs=_obstacles(obstacles, obs_seed))
 
 
-def synthetic_lattice(side=16, K=50, seed=2, sigma=30.0, spacing=6.0, obstacles=0, obs_seed=11):
-    """N = side^3 agents; lattice centred on the origin."""
+def synthetic_lattice(side=16, K=50, seed=2, sigma=30.0, spacing=6.0, obstacles=0, obs_seed=11, block=2):
+    """N = side^3 agents; lattice centred on the origin.  Goals are a random permutation of the lattice
+    sites composed of independent permutations inside every block x block x block cell of sites, so the
+    straight paths of a cell's agents cross at its centre.  (A permutation of the whole lattice sends
+    agents up to 90 m away, beyond what the trust region ||w_t||_1 <= 0.25 can reach in sigma = 30 s
+    (at most a sigma^2 / 4 ~ 56 m per axis): most subproblems are then infeasible, where the reference's
+    dist_scvx_3d.py:110-112 would get s_i.value = None from Clarabel and fail.)"""
     rng = np.random.default_rng(seed)
     g = (np.arange(side) - 0.5 * (side - 1)) * spacing
     sites = np.stack(np.meshgrid(g, g, g, indexing="ij"), -1).reshape(-1, 3)
-    goals = sites[rng.permutation(sites.shape[0])]
+    ijk = np.stack(np.meshgrid(*(np.arange(side),) * 3, indexing="ij"), -1).reshape(-1, 3)
+    cell = ((ijk // block) * np.array([side * side, side, 1])).sum(1)
+    perm = np.arange(sites.shape[0])
+    for c in np.unique(cell):
+        members = np.nonzero(cell == c)[0]
+        perm[members] = members[rng.permutation(members.size)]
+    goals = sites[perm]
     X = _straight(sites, goals, K, 6)
     N = sites.shape[0]
     return dict(X=X, U=np.zeros((N, K, 3)), x_init=X[:, 0, :].copy(), x_final=X[:, -1, :].copy(),

@@ -150,6 +150,19 @@ int scvx_collision_rows_batched(int K, int pos_dim, int n_x, int N_total, const 
                                 int N_local, double R, double cull_radius, int j_max, double* rows,
                                 int32_t* count, void* stream);
 
+/*
+ * A-posteriori check of the reference's FULL collision row set at a solution (replaces nothing in the
+ * reference, which always solves with every row: Distributed_opt/dist_scvx_3d.py:93-107).  For every
+ * local agent i, node t < K-1 and every j != i of X_all (the linearisation point):
+ *     v = (2R - |pbar_i - pbar_j|) - g_ij' (p_t - pbar_i) - S_t,   g_ij = (pbar_i - pbar_j)/|.|
+ * with p_t = X_new[i][t][0:pos_dim], S_t = slack[i][t].  Outputs viol [N_local][K] = #{j : v > tol}
+ * and vmax [N_local][K] = max_j v (0 at t = K-1).  A culled solve (j_max < N_total-1) is the
+ * reference's solution iff no row is violated: the culled problem is a relaxation of the full one.
+ */
+int scvx_collision_check_batched(int K, int pos_dim, int n_x, int N_total, const double* X_all, int i0,
+                                 int N_local, double R, const double* X_new, const double* slack, double tol,
+                                 int32_t* viol, double* vmax, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Batched SCvx convex subproblem: the reference's SCProblem (SCvx/optimization/sc_problem.py:15-83)
  * with the constraints of its models (unicycle_model.py:88-114, single_integrator_model.py:80-126)

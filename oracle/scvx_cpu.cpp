@@ -654,7 +654,7 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
     int it = 0;
     const double tol = T->tol > 0 ? T->tol : 1e-9;
     if (!init_point(ag)) { iters_out = 0; obj_out = 0.0; return SCVX_STATUS_NUMERICAL; }
-    for (it = 0; it < T->max_iter; ++it) {
+    for (it = 0;; ++it) {  // the residuals are evaluated once more after the last step (kernel: cap check)
         // ---- residuals
         double pres = 0.0, dres = 0.0, gap = 0.0, hscale = 1.0, qscale = 1.0;
         std::vector<Vec> rp(K - 1, Vec(n));
@@ -737,6 +737,7 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
         // reduced tolerances (kernel: `near`): a breakdown below ends with MAX_ITER ("inaccurate")
         const bool near = pres <= 1e-4 * hscale && dres <= 1e-4 * qscale && gap <= 5e-5 * std::max(1.0, std::fabs(pobj));
         const int fail_status = near ? SCVX_STATUS_MAX_ITER : SCVX_STATUS_NUMERICAL;
+        if (it >= T->max_iter) { status = fail_status; break; }
         // ---- scaling and node Hessians (aux eliminated)
         for (int t = 0; t < K; ++t) {
             Node& N = ag.nd[t];
@@ -955,6 +956,7 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
             }
             if (!newton(rco, rcq, dz, ds, dl, dsq, dlq, dy, dyi, dyf)) { status = fail_status; break; }
             double al = std::min(1.0, 0.99 * max_step(ds, dl, dsq, dlq));
+            if (near && al < 1e-2) { status = SCVX_STATUS_MAX_ITER; break; }  // stall at reduced accuracy (kernel)
             if (std::getenv("SCVX_DEBUG")) {
                 std::fprintf(stderr, "   alpha_aff %.3e sigma %.3e alpha %.3e\n", aa, sig, al);
                 for (int t = 0; t < K; ++t) { Node& N = ag.nd[t]; for (int r = 0; r < N.nr; ++r) {

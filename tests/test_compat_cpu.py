@@ -238,3 +238,25 @@ def test_workload_constructions():
     c3 = workloads.synthetic_di(7, K=10, obstacles=8)
     r = np.array([o[1] for o in c3["obs"]])
     assert c3["X"].shape == (7, 10, 6) and ((r >= 0.5) & (r <= 1.5)).all()
+
+
+# ---------------------------------------------------------------- Parameter / Variable value shapes
+def test_parameter_rejects_transposed_value():
+    """cvxpy raises 'Invalid dimensions' for a value of the wrong shape; a transposed (K, n)
+    trajectory for an (n, K) parameter must not be reshaped into a scrambled one."""
+    from SCvx.optimization.variables import Parameter
+    p = Parameter((3, 50))
+    with pytest.raises(ValueError, match="Invalid dimensions"):
+        p.value = np.zeros((50, 3))
+    p.value = np.arange(150.0).reshape(3, 50)
+    assert p.value.shape == (3, 50) and p.value[1, 0] == 50.0
+
+
+def test_parameter_accepts_singleton_axes():
+    from SCvx.optimization.variables import Parameter, Variable
+    v = Variable((50, 1))
+    v.value = np.ones(50)
+    assert v.value.shape == (50, 1)
+    s = Parameter(())
+    s.value = np.array([2.5])
+    assert s.value == 2.5

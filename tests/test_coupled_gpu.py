@@ -1,0 +1,191 @@
+"""GPU parity of the coupled configurations and of the exactness machinery of the
+culled coupling:
+
+  * C4: a 512-agent shard (rank 0 of 8) of the 4096-agent lattice construction
+    (scvx_hip.workloads.synthetic_lattice), j_max = 8 nearest rows per node, checked agent by agent
+    against the dense reference-formulation oracle (oracle/qp_dense.py: dist_scvx_3d.py:51-111 as
+    written) on the same rows, and against the full reference row set (all 4095 neighbours) through
+    the a-posteriori check;
+  * C5: 64 quadrotors (scvx_hip.workloads.synthetic_quad) with 8 spheres and coupling R = 0.5;
+  * culled + check == all rows: a dense 33-agent cluster where j_max = 32 keeps every neighbour;
+  * status honesty: an iterate that hits the iteration cap far from optimal is a failure (status 2).
+
+Tolerances (float64): objective 1e-7 relative, constraint violation 1e-7, trajectories 1e-8 (culled +
+check vs all rows: the same problem solved twice)."""
+import numpy as np
+import pytest
+
+import scvx_hip
+from oracle import problems as pb, qp_dense as qd
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(x, cuda, dtype=None):
+    import torch
+    return torch.tensor(np.ascontiguousarray(x), device=cuda, dtype=dtype or torch.float64)
+
+
+def _dense_prob(model, disc_a, sigma_a, Xref, Uref, x_final, tr, rows_a, cnt_a, box, obs, pd=3):
+    n, m = scvx_hip.MODEL_DIMS[model]
+    A, B, C, S, z = pb.unpack_disc(disc_a, n, m)
+    coll = None
+    if rows_a is not None:
+        coll = []
+        for t in range(Xref.shape[0] - 1):
+            r = rows_a[t, :cnt_a[t]]
+            c = r[:, pd] - r[:, :pd] @ Xref[t, :pd]
+            coll.append(np.hstack([r[:, :pd], c[:, None]]))
+    return dict(A=A, B=B, C=C, c=S * sigma_a + z, Xref=Xref, Uref=Uref, x_final=x_final, tr=tr, box=box, obs=obs,
+                w_obs=1e6, coll=coll, w_coll=1e4, umax=None, fix_last_input=True, pos_dim=pd)
+
+
+def _check_against_dense(model, agents, out, dn, sig, X, U, xf, tr, rows, cnt, box, obs, tol_obj=1e-7):
+    Xg, Ug, Sg, og = (out[k].cpu().numpy() for k in ("X", "U", "slack_coll", "obj"))
+    for a in agents:
+        prob = _dense_prob(model, dn[a], sig[a], X[a], U[a], xf[a], tr[a], rows[a], cnt[a], box, obs)
+        with np.errstate(all="ignore"):
+            Xd, Ud, objd, info = qd.solve_agent(prob, tol=1e-10, maxit=150)
+        assert info["status"] == "optimal", (a, info["status"])
+        assert abs(og[a] - objd) <= tol_obj * max(1.0, abs(objd)), (a, og[a], objd)
+        viol = qd.constraint_violation(prob, Xg[a], Ug[a], Sg[a])
+        assert max(viol.values()) < 1e-7, (a, viol)
+
+
+def test_c4_lattice_shard_matches_dense_and_full_rows(cuda):
+    """Rank 0's 512 agents of C4 at the first Jacobi iteration: FOH -> culled rows (j_max 8) -> QP."""
+    import torch
+    from scvx_hip import workloads
+    sc = workloads.synthetic_lattice(side=16, K=50, seed=2, sigma=30.0)
+    n_loc, K = 512, 50
+    X_all = _t(sc["X"], cuda)
+    sl = slice(0, n_loc)
+    X, U, sig = _t(sc["X"][sl], cuda), _t(sc["U"][sl], cuda), _t(sc["sigma"][sl], cuda)
+    disc = scvx_hip.foh_batched("di", X, U, sig)
+    rows, cnt = scvx_hip.collision_rows(X_all, 0, n_loc, 2.3, j_max=8)
+    box = [(0, -50.0, 50.0), (1, -50.0, 50.0)]
+    spec = scvx_hip.QPSpec(model="di", K=K, box=box, j_max=8, w_coll=1e4, tol=1e-9, max_iter=60)
+    tr = np.full(n_loc, 0.25)
+    out = scvx_hip.qp_solve_batched(spec, disc, sig, X, U, _t(sc["x_init"][sl], cuda), _t(sc["x_final"][sl], cuda),
+                                    _t(tr, cuda), rows, cnt)
+    st, it = out["status"].cpu().numpy(), out["iters"].cpu().numpy()
+    assert (st == 0).mean() >= 0.99, np.bincount(st, minlength=3)
+    assert (it > 0).all()
+    rng = np.random.default_rng(0)
+    sample = rng.choice(np.nonzero(st == 0)[0], 3, replace=False)
+    _check_against_dense("di", sample, out, disc.cpu().numpy(), sc["sigma"][sl], sc["X"][sl], sc["U"][sl],
+                         sc["x_final"][sl], tr, rows.cpu().numpy(), cnt.cpu().numpy(), box, [])
+    # every one of the 4095 reference rows per node at the culled solution
+    viol, vmax = scvx_hip.collision_check(X_all, 0, out["X"], out["slack_coll"], 2.3, tol=1e-7)
+    viol, vmax = viol.cpu().numpy(), vmax.cpu().numpy()
+    ok = viol.sum(1) == 0
+    # where no dropped row binds, the culled solution satisfies the full reference problem: a
+    # relaxation whose optimum is feasible for the full problem is its optimum
+    a = int(np.nonzero(ok & (st == 0))[0][0])
+    Xg, Sg = out["X"].cpu().numpy()[a], out["slack_coll"].cpu().numpy()[a]
+    d = Xg - sc["X"][a]
+    for t in range(K - 1):
+        diff = sc["X"][a, t, :3] - sc["X"][:, t, :3]
+        nr = np.linalg.norm(diff, axis=1)
+        nr[a] = np.inf
+        v = (4.6 - nr) - (diff @ d[t, :3]) / nr - Sg[t]
+        assert v.max() <= 1e-7
+        assert abs(v.max() - vmax[a, t]) < 1e-9
+
+
+def test_c5_quadrotors_n64(cuda):
+    """C5 construction at N = 64: every subproblem solves (no exit at 0 iterations), sampled agents
+    match the dense oracle on the same rows; three coupled SCvx iterations stay healthy."""
+    import torch
+    from scvx_hip import workloads
+    from scvx_hip.scvx import CouplingSpec, JacobiSCvx
+    N, K = 64, 50
+    sc = workloads.synthetic_quad(N, K=K, seed=3, obstacles=8)
+    X, U, sig = _t(sc["X"], cuda), _t(sc["U"], cuda), _t(sc["sigma"], cuda)
+    disc = scvx_hip.foh_batched("quad", X, U, sig)
+    rows, cnt = scvx_hip.collision_rows(X, 0, N, 0.5, j_max=8)
+    box = [(0, -12.0, 12.0), (1, -12.0, 12.0)]
+    spec = scvx_hip.QPSpec(model="quad", K=K, box=box, obs=sc["obs"], w_obs=1e6, j_max=8, w_coll=1e4, tol=1e-9,
+                           max_iter=60)
+    tr = np.full(N, 0.25)
+    out = scvx_hip.qp_solve_batched(spec, disc, sig, X, U, _t(sc["x_init"], cuda), _t(sc["x_final"], cuda),
+                                    _t(tr, cuda), rows, cnt)
+    st, it = out["status"].cpu().numpy(), out["iters"].cpu().numpy()
+    assert (st != 2).mean() >= 0.99 and (it > 0).all(), (np.bincount(st, minlength=3), it.min())
+    rng = np.random.default_rng(1)
+    sample = rng.choice(np.nonzero(st == 0)[0], 2, replace=False)
+    _check_against_dense("quad", sample, out, disc.cpu().numpy(), sc["sigma"], sc["X"], sc["U"], sc["x_final"], tr,
+                         rows.cpu().numpy(), cnt.cpu().numpy(), box, sc["obs"], tol_obj=1e-6)
+    drv = JacobiSCvx(spec, _t(sc["x_init"], cuda), _t(sc["x_final"], cuda), sig, 0.25,
+                     coupling=CouplingSpec(R=0.5), tr_rule="global")
+    Xc, Uc = X.clone(), U.clone()
+    for _ in range(3):
+        Xc, Uc, o = drv.step(Xc, Uc)
+        s = o["status"].cpu().numpy()
+        assert (s != 2).mean() >= 0.99 and (o["iters"].cpu().numpy() > 0).all(), np.bincount(s, minlength=3)
+    assert torch.isfinite(Xc).all()
+
+
+def _cluster(N=33, K=30, seed=5):
+    """N double integrators crossing a small region: every pair comes within 2R somewhere."""
+    rng = np.random.default_rng(seed)
+    ang = rng.uniform(0, 2 * np.pi, N)
+    el = rng.uniform(-0.5, 0.5, N)
+    dirs = np.stack([np.cos(ang) * np.cos(el), np.sin(ang) * np.cos(el), np.sin(el)], 1)
+    p0 = 6.0 * dirs + rng.normal(0, 0.3, (N, 3))
+    pf = -6.0 * dirs + rng.normal(0, 0.3, (N, 3))
+    a = np.linspace(0, 1, K)[None, :, None]
+    X = np.zeros((N, K, 6))
+    X[:, :, :3] = p0[:, None] * (1 - a) + pf[:, None] * a
+    return X, np.zeros((N, K, 3))
+
+
+def test_culled_plus_check_equals_all_rows(cuda):
+    """33 agents, every neighbour within reach: j_max = 8 + full-row check + re-solve with 32 rows
+    gives the j_max = 32 (= all N-1 neighbours, the reference's row set) result."""
+    import torch
+    from scvx_hip.scvx import CouplingSpec, JacobiSCvx
+    N, K = 33, 30
+    Xn, Un = _cluster(N, K)
+    X, U = _t(Xn, cuda), _t(Un, cuda)
+    sig = _t(np.full(N, 20.0), cuda)
+    xi, xf = _t(Xn[:, 0], cuda), _t(Xn[:, -1], cuda)
+    box = [(0, -20.0, 20.0), (1, -20.0, 20.0)]
+    res = {}
+    for name, jm, check in (("full", 32, False), ("culled", 8, True), ("raw", 8, False)):
+        spec = scvx_hip.QPSpec(model="di", K=K, box=box, j_max=jm, w_coll=1e4, tol=1e-10, max_iter=80)
+        drv = JacobiSCvx(spec, xi, xf, sig, 0.5, coupling=CouplingSpec(R=1.0, check=check), tr_rule="global")
+        Xo, Uo, o = drv.step(X, U)
+        res[name] = (Xo.cpu().numpy(), o["status"].cpu().numpy(), drv.last_check)
+    assert (res["full"][1] == 0).all()
+    assert (res["culled"][1] == 0).all()
+    chk = res["culled"][2]
+    assert chk["violated"] > 0 and chk["overflow"] == 0, chk      # the check found culled rows that bind
+    np.testing.assert_allclose(res["culled"][0], res["full"][0], rtol=0, atol=1e-8)
+    # without the re-solve, the agents the check flags are exactly those that differ from all rows
+    diff = np.abs(res["raw"][0] - res["full"][0]).max(axis=(1, 2))
+    sc = scvx_hip.QPSpec(model="di", K=K, box=box, j_max=8, w_coll=1e4, tol=1e-10, max_iter=80)
+    drv = JacobiSCvx(sc, xi, xf, sig, 0.5, coupling=CouplingSpec(R=1.0, check=False), tr_rule="global")
+    Xo, Uo, o = drv.step(X, U)
+    viol, _ = scvx_hip.collision_check(X, 0, o["X"], o["slack_coll"], 1.0, tol=1e-7)
+    flagged = viol.sum(1).cpu().numpy() > 0
+    assert (diff[~flagged] < 1e-8).all()
+    assert flagged.sum() == chk["violated"]
+
+
+def test_iteration_cap_far_from_optimum_is_a_failure(cuda):
+    """An IPM stopped by max_iter far from the optimum reports status 2 (solver_error), never
+    'optimal_inaccurate' (status 1): status 1 requires the reduced tolerances of ECOS / Clarabel."""
+    N, K = 16, 50
+    sc = pb.synthetic_di(N, K=K, seed=1, obstacles=8)
+    X, U, sig = _t(sc["X"], cuda), _t(sc["U"], cuda), _t(sc["sigma"], cuda)
+    disc = scvx_hip.foh_batched("di", X, U, sig)
+    box = [(0, -12, 12), (1, -12, 12)]
+    args = (disc, sig, X, U, _t(sc["x_init"], cuda), _t(sc["x_final"], cuda), _t(np.full(N, 0.25), cuda))
+    capped = scvx_hip.qp_solve_batched(scvx_hip.QPSpec(model="di", K=K, box=box, obs=sc["obs"], u_max=1.0,
+                                                       max_iter=3), *args)
+    assert (capped["status"].cpu().numpy() == 2).all()
+    assert (capped["iters"].cpu().numpy() == 3).all()
+    full = scvx_hip.qp_solve_batched(scvx_hip.QPSpec(model="di", K=K, box=box, obs=sc["obs"], u_max=1.0,
+                                                     max_iter=60), *args)
+    assert (full["status"].cpu().numpy() == 0).all()

@@ -36,6 +36,22 @@ class OracleBackend:
                 count[a, t] = len(rr[t])
         return rows, count
 
+    def collision_check(self, X_all, i0, X_new, slack, R, pos_dim, tol):
+        Xa, Xn, S = X_all.numpy(), X_new.numpy(), slack.numpy()
+        n_local, K = Xn.shape[0], Xn.shape[1]
+        viol = np.zeros((n_local, K), np.int32)
+        vmax = np.zeros((n_local, K))
+        for a in range(n_local):
+            for t in range(K - 1):
+                pi = Xa[i0 + a, t, :pos_dim]
+                dp = Xn[a, t, :pos_dim] - pi
+                v = [2 * R - np.linalg.norm(pi - Xa[j, t, :pos_dim])
+                     - (pi - Xa[j, t, :pos_dim]) @ dp / np.linalg.norm(pi - Xa[j, t, :pos_dim]) - S[a, t]
+                     for j in range(Xa.shape[0]) if j != i0 + a]
+                viol[a, t] = sum(x > tol for x in v)
+                vmax[a, t] = max(v)
+        return torch.from_numpy(viol), torch.from_numpy(vmax)
+
     def qp_solver(self, spec, N, device):
         return _CpuQP(spec)
 
@@ -73,6 +89,7 @@ def _run(rank, world, port, q):
     for _ in range(ITERS):
         Xn, Un, out = drv.step(X, U)
         X, U = Xn.clone(), Un.clone()
+    assert drv.last_check["violated"] == 0   # every row is in the solve (j_max = N_total - 1)
     q.put((rank, X.numpy(), drv.tr.numpy(), int(out["status"].max())))
     if world > 1:
         torch.distributed.destroy_process_group()
