@@ -121,7 +121,7 @@ def make_coupled(config, world, rank, device):
         model, R, obs, box, j_max = "di", 2.3, [], [(0, -50.0, 50.0), (1, -50.0, 50.0)], 8   # lattice spans +-45
     else:
         sc = workloads.synthetic_quad(1024, K=K, seed=3, sigma=SIGMA, obstacles=N_OBS)
-        model, R, obs, box, j_max = "quad", 0.5, sc["obs"], BOX, 8
+        model, R, obs, box, j_max = "quad", 0.5, sc["obs"], workloads.QUAD_BOX, 8
     N_total = sc["X"].shape[0]
     if N_total % world:
         raise SystemExit(f"{config}: {N_total} agents do not shard over {world} ranks")

@@ -1348,12 +1348,13 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     degl += soc ? 1.0 : 0.0;
     const double deg = fmax(wave_sum(degl), 1.0);
     const double tol = T.tol > 0 ? T.tol : 1e-9;
-    double qscl = 1.0;  // max objective weight
-    if (nobs > 0) qscl = fmax(qscl, T.w_obs);
-    if (has_coll) qscl = fmax(qscl, T.w_coll);
+    double qnorm = 0.0;  // ||q||_inf: the linear objective weights of the slack groups
+    if (nobs > 0) qnorm = fmax(qnorm, T.w_obs);
+    if (has_coll) qnorm = fmax(qnorm, T.w_coll);
 
     // ------------------------------------------------------------------ IPM iterations
     const long long cyc_all0 = __builtin_amdgcn_s_memtime();
+    double dres_best = 1e300, pres_best = 1e300;
     stamp(-1);
     // the residuals are evaluated once more after the last step: an iterate that reaches the
     // iteration cap is reported `optimal_inaccurate` only if it meets the reduced tolerances below,
@@ -1370,16 +1371,42 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         dyn_residual(z, dt, rp);
         // dual residual rd = Pz + q + A'y + G'lam (z and group parts)
         double rd[NZ], rda[NGA];
-        double pres = 0.0, dres = 0.0, gap = 0.0, hsc = 1.0, pobj = 0.0;
+        // residual norms and Clarabel's normalisation of them (the solver dist_scvx_3d.py:110 calls):
+        // primal ||r_p|| <= tol max(1, ||b|| + ||x|| + ||s||), dual ||r_d|| <= tol max(1, ||q|| + ||x|| + ||z||)
+        // (inf-norms; b = every constant of the equality and inequality rows, x = primal variables,
+        // s = slacks, z = every multiplier: rows, cone, dynamics, boundary conditions)
+        double pres = 0.0, dres = 0.0, gap = 0.0, nb = 0.0, nxv = 0.0, nsl = 0.0, nzd = 0.0, pobj = 0.0;
 #pragma unroll
         for (int i = 0; i < NX; ++i) pres = fmax(pres, fabs(rp[i]));
+        if (t < K - 1) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i)
+                nb = fmax(nb, fabs(fma(dt[NX * NX + 2 * NX * NU + i], sig, dt[NX * NX + 2 * NX * NU + NX + i])));
+        }
+        if (act) {
+#pragma unroll
+            for (int i = 0; i < NZ; ++i) nxv = fmax(nxv, fabs(z[i]));
+#pragma unroll
+            for (int g = 0; g < NG; ++g) nxv = fmax(nxv, grp_on(g) ? fabs(av[g]) : 0.0);
+            if (t < K - 1) {
+#pragma unroll
+                for (int i = 0; i < NX; ++i) nzd = fmax(nzd, fabs(y[i]));
+            }
+        }
+        if (lane < NX) nzd = fmax(nzd, fmax(fabs(lds[V_YI + lane]), fin ? fabs(lds[V_YF + lane]) : 0.0));
         if (t == 0) {
 #pragma unroll
-            for (int i = 0; i < NX; ++i) pres = fmax(pres, fabs(z[i] - a.x_init[agent * NX + i]));
+            for (int i = 0; i < NX; ++i) {
+                pres = fmax(pres, fabs(z[i] - a.x_init[agent * NX + i]));
+                nb = fmax(nb, fabs(a.x_init[agent * NX + i]));
+            }
         }
         if (act && t == K - 1 && fin) {
 #pragma unroll
-            for (int i = 0; i < NX; ++i) pres = fmax(pres, fabs(z[i] - a.x_final[agent * NX + i]));
+            for (int i = 0; i < NX; ++i) {
+                pres = fmax(pres, fabs(z[i] - a.x_final[agent * NX + i]));
+                nb = fmax(nb, fabs(a.x_final[agent * NX + i]));
+            }
         }
 #pragma unroll
         for (int i = 0; i < NX; ++i) rd[i] = 0.0;
@@ -1394,7 +1421,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             if (row_on(r)) {
                 const double rcr = gz + s_(r) - h;
                 pres = fmax(pres, fabs(rcr));
-                hsc = fmax(hsc, fabs(h));
+                nb = fmax(nb, fabs(h));
+                nsl = fmax(nsl, s_(r));
+                nzd = fmax(nzd, l_(r));
                 gap += s_(r) * l_(r);
                 row_accT(r, l_(r), rd, rda);
             }
@@ -1404,8 +1433,13 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
             for (int j = 0; j < NU; ++j) { rcq[1 + j] = sq[1 + j] - z[NX + j]; rd[NX + j] -= lq[1 + j]; }
 #pragma unroll
-            for (int j = 0; j < NQ; ++j) { pres = fmax(pres, fabs(rcq[j])); gap += sq[j] * lq[j]; }
-            hsc = fmax(hsc, T.u_max);
+            for (int j = 0; j < NQ; ++j) {
+                pres = fmax(pres, fabs(rcq[j]));
+                gap += sq[j] * lq[j];
+                nsl = fmax(nsl, fabs(sq[j]));
+                nzd = fmax(nzd, fabs(lq[j]));
+            }
+            nb = fmax(nb, T.u_max);
         } else {
 #pragma unroll
             for (int j = 0; j < NQ; ++j) rcq[j] = 0.0;
@@ -1456,23 +1490,35 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 for (int j = 0; j < NU; ++j) pobj += wu * z[NX + j] * z[NX + j];
             }
         }
-        pres = wave_max(pres); dres = wave_max(dres); hsc = wave_max(hsc);
+        pres = wave_max(pres); dres = wave_max(dres);
+        nb = wave_max(nb); nxv = wave_max(nxv); nsl = wave_max(nsl); nzd = wave_max(nzd);
         gap = wave_sum(gap); pobj = wave_sum(pobj);
+        const double pnorm = fmax(1.0, nb + nxv + nsl), dnorm = fmax(1.0, qnorm + nxv + nzd);
         const double mu = gap / deg;
         if (!isfinite(pres + dres + mu)) { status = SCVX_STATUS_NUMERICAL; fail_code = 3.0; break; }
-        if (pres <= tol * hsc && dres <= tol * qscl && gap <= tol * fmax(1.0, fabs(pobj))) {
+        if (pres <= tol * pnorm && dres <= tol * dnorm && gap <= tol * fmax(1.0, fabs(pobj))) {
             status = SCVX_STATUS_OPTIMAL;
             break;
         }
         // reduced accuracy ("optimal_inaccurate"): what a numerical breakdown below leaves is still
         // usable if it meets the reduced tolerances of the reference's solvers (Clarabel / ECOS:
         // feasibility 1e-4, gap 5e-5 relative)
-        const bool near = pres <= 1e-4 * hsc && dres <= 1e-4 * qscl && gap <= 5e-5 * fmax(1.0, fabs(pobj));
+        const bool near = pres <= 1e-4 * pnorm && dres <= 1e-4 * dnorm && gap <= 5e-5 * fmax(1.0, fabs(pobj));
         if (it >= T.max_iter) {
             status = near ? SCVX_STATUS_MAX_ITER : SCVX_STATUS_NUMERICAL;
             fail_code = 5.0;
             break;
         }
+        // insufficient progress (Clarabel's rule): a residual that jumps by 100x once the reduced
+        // tolerances hold is the Newton system losing its accuracy at extreme barrier scalings;
+        // stop at reduced accuracy instead of wandering on a corrupted direction
+        if (near && (dres > fmax(100.0 * dres_best, tol * dnorm) || pres > fmax(100.0 * pres_best, tol * pnorm))) {
+            status = SCVX_STATUS_MAX_ITER;
+            fail_code = 7.0;
+            break;
+        }
+        dres_best = fmin(dres_best, dres);
+        pres_best = fmin(pres_best, pres);
         // SOC Nesterov-Todd scaling (hyperbolic-rotation form, W lam = W^-1 s)
         double Wi2uu[NU * NU];
 #pragma unroll

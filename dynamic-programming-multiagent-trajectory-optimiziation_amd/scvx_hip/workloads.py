@@ -7,11 +7,18 @@
                        goals a random permutation of the lattice sites inside 2x2x2 cells, so straight
                        paths cross (and every goal is reachable under the trust region).
     synthetic_quad     C5: 12-state quadrotor (models.hpp Quadrotor) from hover: positions as C2,
-                       attitude / rates 0, U = hover thrust (m g, 0, 0, 0).
+                       attitude / rates 0, U = hover thrust (m g, 0, 0, 0).  QUAD_BOX adds a roll /
+                       pitch envelope |phi|, |theta| <= 1 rad to the x / y box: the model is build-defined
+                       (SURVEY §8a M2) with Euler angles, whose kinematics are singular at |theta| = pi/2;
+                       without the envelope the trust region on the inputs alone lets a subproblem
+                       solution tilt past 90 degrees, and the next FOH linearisation is degenerate.
 
 All arrays are agent-major (N, K, n) / (N, K, m) float64, the layout of include/scvx_hip.h.
 """
 import numpy as np
+
+BOX = [(0, -12.0, 12.0), (1, -12.0, 12.0)]                 # C2/C3/C5 x, y box (dist_scvx_3d.py:87-90 widened)
+QUAD_BOX = BOX + [(6, -1.0, 1.0), (7, -1.0, 1.0)]        # C5: + roll / pitch envelope (rad)
 
 
 def _obstacles(obstacles, obs_seed):

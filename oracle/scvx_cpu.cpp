@@ -654,9 +654,21 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
     int it = 0;
     const double tol = T->tol > 0 ? T->tol : 1e-9;
     if (!init_point(ag)) { iters_out = 0; obj_out = 0.0; return SCVX_STATUS_NUMERICAL; }
+    double dres_best = 1e300, pres_best = 1e300;
     for (it = 0;; ++it) {  // the residuals are evaluated once more after the last step (kernel: cap check)
         // ---- residuals
-        double pres = 0.0, dres = 0.0, gap = 0.0, hscale = 1.0, qscale = 1.0;
+        // Clarabel's normalisation (kernel: pnorm / dnorm): primal max(1, ||b|| + ||x|| + ||s||),
+        // dual max(1, ||q|| + ||x|| + ||z||), inf-norms over every constant / variable / multiplier
+        double pres = 0.0, dres = 0.0, gap = 0.0, nb = 0.0, nxv = 0.0, nsl = 0.0, nzd = 0.0, nq = 0.0;
+        for (int i = 0; i < n; ++i) {
+            nb = std::max({nb, std::fabs(ag.x_init[i]), T->has_final ? std::fabs(ag.x_final[i]) : 0.0});
+            nzd = std::max({nzd, std::fabs(ag.y_init[i]), T->has_final ? std::fabs(ag.y_fin[i]) : 0.0});
+        }
+        for (double v : ag.y) nzd = std::max(nzd, std::fabs(v));
+        for (int t = 0; t < K - 1; ++t)
+            for (int i = 0; i < n; ++i) nb = std::max(nb, std::fabs(ag.c[t][i]));
+        for (int t = 0; t < K; ++t)
+            for (int j = 0; j < ag.nd[t].nv; ++j) nxv = std::max(nxv, std::fabs(ag.nd[t].z[j]));
         std::vector<Vec> rp(K - 1, Vec(n));
         Vec rpi(n), rpf(n, 0.0);
         for (int i = 0; i < n; ++i) rpi[i] = ag.nd[0].z[i] - ag.x_init[i];
@@ -683,18 +695,25 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
                 for (int j = 0; j < N.nv; ++j) v += N.G(r, j) * N.z[j];
                 l.rc[r] = v;
                 pres = std::max(pres, std::fabs(v));
-                hscale = std::max(hscale, std::fabs(N.h[r]));
+                nb = std::max(nb, std::fabs(N.h[r]));
+                nsl = std::max(nsl, N.s[r]);
+                nzd = std::max(nzd, N.lam[r]);
                 gap += N.s[r] * N.lam[r];
             }
             if (N.soc) {
                 l.rcs.assign(m + 1, 0.0);
                 l.rcs[0] = N.ssoc[0] - T->u_max;
                 for (int j = 0; j < m; ++j) l.rcs[1 + j] = N.ssoc[1 + j] - N.z[n + j];
-                for (int j = 0; j <= m; ++j) { pres = std::max(pres, std::fabs(l.rcs[j])); gap += N.ssoc[j] * N.lsoc[j]; }
-                hscale = std::max(hscale, T->u_max);
+                for (int j = 0; j <= m; ++j) {
+                    pres = std::max(pres, std::fabs(l.rcs[j]));
+                    gap += N.ssoc[j] * N.lsoc[j];
+                    nsl = std::max(nsl, std::fabs(N.ssoc[j]));
+                    nzd = std::max(nzd, std::fabs(N.lsoc[j]));
+                }
+                nb = std::max(nb, T->u_max);
             }
             l.rd.assign(N.nv, 0.0);
-            for (int j = 0; j < N.nv; ++j) { l.rd[j] = N.pdiag[j] * N.z[j] + N.q[j]; qscale = std::max(qscale, std::fabs(N.q[j])); }
+            for (int j = 0; j < N.nv; ++j) { l.rd[j] = N.pdiag[j] * N.z[j] + N.q[j]; nq = std::max(nq, std::fabs(N.q[j])); }
             for (int r = 0; r < N.nr; ++r)
                 for (int j = 0; j < N.nv; ++j) l.rd[j] += N.G(r, j) * N.lam[r];
             if (N.soc)
@@ -730,14 +749,22 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
             }
         if (std::getenv("SCVX_DEBUG")) std::fprintf(stderr, "it %d pres %.3e dres %.3e mu %.3e pobj %.6e\n", it, pres, dres, mu, pobj);
         if (!std::isfinite(pres + dres + mu)) { status = SCVX_STATUS_NUMERICAL; break; }
-        if (pres <= tol * hscale && dres <= tol * qscale && gap <= tol * std::max(1.0, std::fabs(pobj))) {
+        const double pnorm = std::max(1.0, nb + nxv + nsl), dnorm = std::max(1.0, nq + nxv + nzd);
+        if (pres <= tol * pnorm && dres <= tol * dnorm && gap <= tol * std::max(1.0, std::fabs(pobj))) {
             status = SCVX_STATUS_OPTIMAL;
             break;
         }
         // reduced tolerances (kernel: `near`): a breakdown below ends with MAX_ITER ("inaccurate")
-        const bool near = pres <= 1e-4 * hscale && dres <= 1e-4 * qscale && gap <= 5e-5 * std::max(1.0, std::fabs(pobj));
+        const bool near = pres <= 1e-4 * pnorm && dres <= 1e-4 * dnorm && gap <= 5e-5 * std::max(1.0, std::fabs(pobj));
         const int fail_status = near ? SCVX_STATUS_MAX_ITER : SCVX_STATUS_NUMERICAL;
         if (it >= T->max_iter) { status = fail_status; break; }
+        // insufficient progress (kernel: fail code 7)
+        if (near && (dres > std::max(100.0 * dres_best, tol * dnorm) || pres > std::max(100.0 * pres_best, tol * pnorm))) {
+            status = SCVX_STATUS_MAX_ITER;
+            break;
+        }
+        dres_best = std::min(dres_best, dres);
+        pres_best = std::min(pres_best, pres);
         // ---- scaling and node Hessians (aux eliminated)
         for (int t = 0; t < K; ++t) {
             Node& N = ag.nd[t];

@@ -12,7 +12,9 @@ sys.path.insert(0, os.path.join(REPO, "dynamic-programming-multiagent-trajectory
 sys.path.insert(0, REPO)
 
 
-def main(cfg="c4", agent=None, cap=80):
+def main(cfg="c4", agent=None, cap=None):
+    cap = int(cap or os.environ.get("CAP", 60))
+    tol = float(os.environ.get("TOL", 1e-8))
     import torch
     import scvx_hip
     from scvx_hip import workloads
@@ -24,21 +26,30 @@ def main(cfg="c4", agent=None, cap=80):
         model, n_loc, R, box, obs = "di", 512, 2.3, [(0, -50.0, 50.0), (1, -50.0, 50.0)], []
     else:
         sc = workloads.synthetic_quad(64, K=50, seed=3, obstacles=8)
-        model, n_loc, R, box, obs = "quad", 64, 0.5, [(0, -12.0, 12.0), (1, -12.0, 12.0)], sc["obs"]
+        model, n_loc, R, box, obs = "quad", 64, 0.5, workloads.QUAD_BOX, sc["obs"]
     n, m = scvx_hip.MODEL_DIMS[model]
     sl = slice(0, n_loc)
     X_all = T(sc["X"])
     X, U, sig = T(sc["X"][sl]), T(sc["U"][sl]), T(sc["sigma"][sl])
     disc = scvx_hip.foh_batched(model, X, U, sig)
     rows, cnt = scvx_hip.collision_rows(X_all, 0, n_loc, R, j_max=8)
-    spec = scvx_hip.QPSpec(model=model, K=50, box=box, obs=obs, w_obs=1e6, j_max=8, w_coll=1e4, tol=1e-9,
+    spec = scvx_hip.QPSpec(model=model, K=50, box=box, obs=obs, w_obs=1e6, j_max=8, w_coll=1e4, tol=tol,
                            max_iter=cap)
     solver = scvx_hip.QPSolver(spec, n_loc, device=dev)
     tr = np.full(n_loc, 0.25)
     out = solver.solve(disc, sig, X, U, T(sc["x_init"][sl]), T(sc["x_final"][sl]), T(tr), rows, cnt)
     st, it = out["status"].cpu().numpy(), out["iters"].cpu().numpy()
     print("status", np.bincount(st, minlength=3), "iters hist", dict(zip(*np.unique(it, return_counts=True))))
-    a = int(agent) if agent is not None else int(np.nonzero(st == 2)[0][0]) if (st == 2).any() else 0
+    codes = torch.zeros(n_loc, dtype=torch.float64, device=dev)
+    scvx_hip.lib().scvx_qp_set_trace(ctypes.c_void_p(codes.data_ptr()), -1, 0)
+    out = solver.solve(disc, sig, X, U, T(sc["x_init"][sl]), T(sc["x_final"][sl]), T(tr), rows, cnt)
+    torch.cuda.synchronize()
+    scvx_hip.lib().scvx_qp_set_trace(None, 0, 0)
+    cd = codes.cpu().numpy().astype(int)
+    for s_ in (1, 2):
+        print(f"status {s_} agents / exit codes / iters:", [(int(i), int(cd[i]), int(it[i])) for i in np.nonzero(st == s_)[0][:24]])
+    a = int(agent) if agent is not None else int(np.nonzero(st == 2)[0][0]) if (st == 2).any() else \
+        int(np.nonzero(st == 1)[0][0]) if (st == 1).any() else 0
     buf = torch.zeros(8 * cap + 32, dtype=torch.float64, device=dev)
     scvx_hip.lib().scvx_qp_set_trace(ctypes.c_void_p(buf.data_ptr()), a, cap)
     out = solver.solve(disc, sig, X, U, T(sc["x_init"][sl]), T(sc["x_final"][sl]), T(tr), rows, cnt)
@@ -115,8 +126,53 @@ def run(cfg="c5", iters=7):
         U.copy_(Un)
 
 
+def jac(iters=3):
+    """The C5 n64 test's coupled loop: per step, status histogram; for agents that exit at 0 IPM
+    iterations, a re-solve of the step's subproblems with per-agent exit codes."""
+    import torch
+    import scvx_hip
+    from scvx_hip import workloads
+    from scvx_hip.scvx import CouplingSpec, JacobiSCvx
+    dev = torch.device("cuda:0")
+    T = lambda x: torch.tensor(np.ascontiguousarray(x), device=dev, dtype=torch.float64)  # noqa: E731
+    N, K = 64, 50
+    sc = workloads.synthetic_quad(N, K=K, seed=3, obstacles=8)
+    box = workloads.QUAD_BOX
+    spec = scvx_hip.QPSpec(model="quad", K=K, box=box, obs=sc["obs"], w_obs=1e6, j_max=8, w_coll=1e4, tol=1e-8,
+                           max_iter=60)
+    drv = JacobiSCvx(spec, T(sc["x_init"]), T(sc["x_final"]), T(sc["sigma"]), 0.25, coupling=CouplingSpec(R=0.5),
+                     tr_rule="global")
+    X, U = T(sc["X"]), T(sc["U"])
+    for k in range(int(iters)):
+        Xp, Up, trp = X.clone(), U.clone(), drv.tr.clone()
+        X, U, o = drv.step(X, U)
+        st, it = o["status"].cpu().numpy(), o["iters"].cpu().numpy()
+        print(f"step {k}: tr {trp[0].item():.4g} status {np.bincount(st, minlength=3)} zero-it {np.nonzero(it == 0)[0]}")
+        if (it == 0).any():
+            codes = torch.zeros(N, dtype=torch.float64, device=dev)
+            scvx_hip.lib().scvx_qp_set_trace(ctypes.c_void_p(codes.data_ptr()), -1, 0)
+            o2 = drv.solver.solve(drv.disc, drv.sigma, Xp, Up, drv.x_init, drv.x_final, trp, drv.rows, drv.count)
+            torch.cuda.synchronize()
+            scvx_hip.lib().scvx_qp_set_trace(None, 0, 0)
+            z = np.nonzero(o2["iters"].cpu().numpy() == 0)[0]
+            print("   re-solve zero-it agents", z, "codes", codes.cpu().numpy()[z], "U min thrust",
+                  [float(Up[a, :, 0].min()) for a in z])
+            for a in z:
+                d = drv.disc[a].cpu().numpy()
+                xa = Xp[a].cpu().numpy()
+                print(f"   agent {a}: disc finite {np.isfinite(d).all()} max|disc| {np.abs(d).max():.3e} "
+                      f"max|angles| {np.abs(xa[:, 6:9]).max():.3f} max|rates| {np.abs(xa[:, 9:12]).max():.3f} "
+                      f"max|v| {np.abs(xa[:, 3:6]).max():.3f} U range {Up[a].min().item():.3f} {Up[a].max().item():.3f}")
+                np.savez(f"gpurun_out/c5_zero_{k}_{a}.npz", disc=d, X=xa, U=Up[a].cpu().numpy(), tr=trp[a].item(),
+                         rows=drv.rows[a].cpu().numpy(), count=drv.count[a].cpu().numpy(),
+                         x_init=drv.x_init[a].cpu().numpy(), x_final=drv.x_final[a].cpu().numpy(),
+                         sigma=drv.sigma[a].item())
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "run":
         run(*sys.argv[2:])
+    elif len(sys.argv) > 1 and sys.argv[1] == "jac":
+        jac(*sys.argv[2:])
     else:
         main(*sys.argv[1:])
