@@ -260,3 +260,16 @@ def test_parameter_accepts_singleton_axes():
     s = Parameter(())
     s.value = np.array([2.5])
     assert s.value == 2.5
+
+
+def test_initial_guess_matches_reference_goldens():
+    """SCvx/utils/initial_guess.py restatement vs the reference's own outputs (tests/golden/
+    make_initial_guess_goldens.py: the default 3-agent scenario + 21 seeded multi-obstacle cases)."""
+    import os
+    from SCvx.utils.initial_guess import initial_guess
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "initial_guess.npz"))
+    for i in range(int(g["n"])):
+        obs = [([o[0], o[1]], o[2]) for o in g[f"obs_{i}"]]
+        X0, U0 = initial_guess(g[f"p0_{i}"], g[f"p1_{i}"], obs, float(g[f"clear_{i}"]), int(g[f"K_{i}"]))
+        np.testing.assert_array_equal(X0, g[f"X0_{i}"])
+        assert U0.shape == (2, int(g[f"K_{i}"])) and not U0.any()

@@ -1,33 +1,60 @@
-"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate runs) into per-launch HBM-side
-bytes per kernel, with the gfx950 correction of /opt/skills/guides/MI355X_MICROARCH.md (HBM section):
-FETCH_SIZE (KiB) counts half the bytes of wide coalesced reads -> x2; WRITE_SIZE (KiB) is exact.
-Usage: python tools/pmc_summary.py <fetch_dir> <write_dir> <out.json>"""
+"""Summarise the rocprofv3 --pmc passes of tools/gpu_pmc.sh (one counter group per run) for one kernel.
+
+HBM-side bytes per launch follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE (KiB)
+counts half the bytes of wide coalesced reads on gfx950 -> x2; WRITE_SIZE (KiB) is exact.  SQ cycle
+counters (SQ_WAVE_CYCLES, SQ_WAIT_*, SQ_ACTIVE_INST_*) count quad-cycles (x4 = shader cycles); the
+SQ_INSTS_* counters count wave-instructions.
+
+usage: python tools/pmc_summary.py <gpurun_out/pmc_TAG> <out.json> [kernel-substring]
+       (reads every <gpurun_out/pmc_TAG>_*/run_counter_collection.csv)"""
+import collections
 import csv
+import glob
 import json
 import sys
 
 
-def per_kernel(path, counter):
-    agg = {}
-    for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter:
-            continue
-        agg.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in agg.items()}
+def collect(prefix, kernel):
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    names = {}
+    for f in sorted(glob.glob(prefix + "_*/run_counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            if kernel not in r["Kernel_Name"]:
+                continue
+            key = (f, r["Dispatch_Id"])
+            per[r["Counter_Name"]][key] += float(r["Counter_Value"])
+            names[r["Counter_Name"]] = r["Kernel_Name"]
+    return {c: sum(v.values()) / len(v) for c, v in per.items()}, names
 
 
-def main(fetch_dir, write_dir, out):
-    f = per_kernel(fetch_dir + "/run_counter_collection.csv", "FETCH_SIZE")
-    w = per_kernel(write_dir + "/run_counter_collection.csv", "WRITE_SIZE")
-    res = {}
-    for k in sorted(set(f) | set(w)):
-        if "scvx::" not in k:
-            continue
-        short = k.split("(")[0].replace("void ", "")
-        fb = 2.0 * 1024 * f.get(k, 0.0)
-        wb = 1024 * w.get(k, 0.0)
-        res[short] = {"fetch_bytes_corrected": fb, "write_bytes": wb, "traffic_bytes": fb + wb,
-                      "raw_FETCH_SIZE_KiB": f.get(k), "raw_WRITE_SIZE_KiB": w.get(k)}
+def main(prefix, out, kernel="qp_ipm_kernel<scvx::QPCfg<6, 3, 2, 8, 0>"):
+    c, names = collect(prefix, kernel)
+    res = {"kernel": next(iter(names.values()), kernel).split("(")[0].replace("void ", ""),
+           "source": prefix + "_*", "raw_per_launch": c}
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        fb, wb = 2.0 * 1024 * c["FETCH_SIZE"], 1024 * c["WRITE_SIZE"]
+        res.update(fetch_bytes_corrected=fb, write_bytes=wb, traffic_bytes=fb + wb)
+    w = c.get("SQ_WAVES")
+    if w and "SQ_WAVE_CYCLES" in c:
+        cyc = 4 * c["SQ_WAVE_CYCLES"] / w
+        d = {"wave_cycles": cyc}
+        for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS",
+                  "SQ_ACTIVE_INST_VMEM", "SQ_ACTIVE_INST_SCA"):
+            if k in c:
+                d[k.lower().replace("sq_", "") + "_frac"] = 4 * c[k] / w / cyc
+        for k in ("SQ_INSTS_VALU", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                  "SQ_INSTS_VALU_TRANS_F64", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_SALU"):
+            if k in c:
+                d[k.lower().replace("sq_", "") + "_per_wave"] = c[k] / w
+        if "SQ_INSTS_VALU_FMA_F64" in c:
+            f64 = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                               "SQ_INSTS_VALU_TRANS_F64"))
+            d["f64_share_of_valu_insts"] = f64 / max(c.get("SQ_INSTS_VALU", 1.0), 1.0)
+            d["issued_f64_flop_per_launch_64lanes"] = 64 * (2 * c["SQ_INSTS_VALU_FMA_F64"] + c.get("SQ_INSTS_VALU_ADD_F64", 0)
+                                                             + c.get("SQ_INSTS_VALU_MUL_F64", 0))
+        res["per_wave"] = d
+    if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
+        res["l2_hit_rate"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
