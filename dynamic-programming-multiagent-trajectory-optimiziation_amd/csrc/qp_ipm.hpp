@@ -248,7 +248,15 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     const int ccount = (ineq && has_coll) ? min((int)a.coll_count[agent * K + t], min(T.j_max, NC)) : 0;
     const double trv = a.tr[agent];
     const double sig = a.sigma[agent];
-    const double wu = (t < K - 1) ? 1.0 : T.w_last;
+    // objective scaling: the problem is solved with its objective divided by its largest weight
+    // (osc = max(1, ||q||_inf), the slack-group weights, 1e4..1e6 here), so the multipliers are O(1);
+    // the iterates then start better centred (C3: 17 -> 13 IPM iterations on average).  The minimiser is
+    // unchanged; the reported objective and the gap test are in the caller's units.
+    double qnorm = 0.0;  // ||q||_inf: the linear objective weights of the slack groups
+    if (nobs > 0) qnorm = fmax(qnorm, T.w_obs);
+    if (has_coll) qnorm = fmax(qnorm, T.w_coll);
+    const double osc = fmax(1.0, qnorm), iosc = 1.0 / osc;
+    const double wu = ((t < K - 1) ? 1.0 : T.w_last) * iosc;
     const bool fixed_u = act && (t == K - 1) && T.fix_last_input;
     const double* disc = a.disc + agent * (long long)(K - 1) * C::DSTR;
     double* ws = a.ws + agent * a.ws_agent;
@@ -1060,7 +1068,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             gav[r - C::R_GRP] -= c;
         }
     };
-    auto gweight = [&](int g) __attribute__((always_inline)) -> double { return g < NO ? T.w_obs : T.w_coll; };
+    auto gweight = [&](int g) __attribute__((always_inline)) -> double { return (g < NO ? T.w_obs : T.w_coll) * iosc; };
 
     // Node Hessian (row scaling D_r = l/s or 1, SOC block Wi2uu) -> packet Q, S, R (xi/u
     // coordinates); group elimination factors -> columns C_GRP.  Also writes e = -rp.
@@ -1348,9 +1356,6 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     degl += soc ? 1.0 : 0.0;
     const double deg = fmax(wave_sum(degl), 1.0);
     const double tol = T.tol > 0 ? T.tol : 1e-9;
-    double qnorm = 0.0;  // ||q||_inf: the linear objective weights of the slack groups
-    if (nobs > 0) qnorm = fmax(qnorm, T.w_obs);
-    if (has_coll) qnorm = fmax(qnorm, T.w_coll);
 
     // ------------------------------------------------------------------ IPM iterations
     const long long cyc_all0 = __builtin_amdgcn_s_memtime();
@@ -1493,17 +1498,17 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         pres = wave_max(pres); dres = wave_max(dres);
         nb = wave_max(nb); nxv = wave_max(nxv); nsl = wave_max(nsl); nzd = wave_max(nzd);
         gap = wave_sum(gap); pobj = wave_sum(pobj);
-        const double pnorm = fmax(1.0, nb + nxv + nsl), dnorm = fmax(1.0, qnorm + nxv + nzd);
+        const double pnorm = fmax(1.0, nb + nxv + nsl), dnorm = fmax(iosc, (qnorm + nxv) * iosc + nzd);  // caller's units / osc
         const double mu = gap / deg;
         if (!isfinite(pres + dres + mu)) { status = SCVX_STATUS_NUMERICAL; fail_code = 3.0; break; }
-        if (pres <= tol * pnorm && dres <= tol * dnorm && gap <= tol * fmax(1.0, fabs(pobj))) {
+        if (pres <= tol * pnorm && dres <= tol * dnorm && gap * osc <= tol * fmax(1.0, fabs(pobj * osc))) {
             status = SCVX_STATUS_OPTIMAL;
             break;
         }
         // reduced accuracy ("optimal_inaccurate"): what a numerical breakdown below leaves is still
         // usable if it meets the reduced tolerances of the reference's solvers (Clarabel / ECOS:
         // feasibility 1e-4, gap 5e-5 relative)
-        const bool near = pres <= 1e-4 * pnorm && dres <= 1e-4 * dnorm && gap <= 5e-5 * fmax(1.0, fabs(pobj));
+        const bool near = pres <= 1e-4 * pnorm && dres <= 1e-4 * dnorm && gap * osc <= 5e-5 * fmax(1.0, fabs(pobj * osc));
         if (it >= T.max_iter) {
             status = near ? SCVX_STATUS_MAX_ITER : SCVX_STATUS_NUMERICAL;
             fail_code = 5.0;
@@ -1667,18 +1672,49 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             dsr = -rcr - gd;
             dlr = (rco_of(r, corr) + l_(r) * (rcr + gd)) / s_(r);
         };
-        auto max_step = [&](bool corr) __attribute__((always_inline)) {
-            double am = 1e300;
+        // One pass over the rows for the step length: the ratio test without divisions (the best
+        // candidate kept as a fraction bn / bd, bd > 0, compared by cross-multiplication; one division
+        // at the end), the coefficients of the complementarity after a step a,
+        //   sum (s + a ds)(l + a dl) = q0 + a q1 + a^2 q2   (predictor: mu_aff without another pass),
+        // the predictor products ds dl the corrector needs (stored), and a NaN / Inf probe of every
+        // live direction (0 * x poisons the sum).
+        auto max_step = [&](bool corr, double* quad, double& probe) __attribute__((always_inline)) {
+            double bn = 1e300, bd = 1.0, q0 = 0.0, q1 = 0.0, q2 = 0.0, pr = 0.0;
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
                 if (row_on(r)) {
                     double dsr, dlr;
                     row_dir(r, corr, dsr, dlr);
-                    if (dsr < 0) am = fmin(am, -s_(r) / dsr);
-                    if (dlr < 0) am = fmin(am, -l_(r) / dlr);
+                    const double sr = s_(r), lr = l_(r);
+                    const bool c1 = dsr < 0.0 && sr * bd < bn * -dsr;
+                    bn = c1 ? sr : bn;
+                    bd = c1 ? -dsr : bd;
+                    const bool c2 = dlr < 0.0 && lr * bd < bn * -dlr;
+                    bn = c2 ? lr : bn;
+                    bd = c2 ? -dlr : bd;
+                    q0 = fma(sr, lr, q0);
+                    q1 += fma(sr, dlr, lr * dsr);
+                    q2 = fma(dsr, dlr, q2);
+                    pr += 0.0 * (dsr + dlr);
+                    if (!corr) cst(C::C_CP + r, dsr * dlr);
                 }
             }
-            if (soc) { am = fmin(am, soc_step(sq, dsq)); am = fmin(am, soc_step(lq, dlq)); }
+            double am = bn / bd;
+            if (soc) {
+                am = fmin(am, soc_step(sq, dsq));
+                am = fmin(am, soc_step(lq, dlq));
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) {
+                    q0 = fma(sq[j], lq[j], q0);
+                    q1 += fma(sq[j], dlq[j], lq[j] * dsq[j]);
+                    q2 = fma(dsq[j], dlq[j], q2);
+                    pr += 0.0 * (dsq[j] + dlq[j]);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < NZ; ++i) pr += 0.0 * dz[i];
+            quad[0] = q0; quad[1] = q1; quad[2] = q2;
+            probe = pr;
             return wave_min(am);
         };
 
@@ -1702,22 +1738,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             }
         }
         newton(false, rcq2);
-        const double aa = fmin(1.0, max_step(false));
-        double gap_a = 0.0;
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            if (row_on(r)) {
-                double dsr, dlr;
-                row_dir(r, false, dsr, dlr);
-                gap_a += (s_(r) + aa * dsr) * (l_(r) + aa * dlr);
-                cst(C::C_CP + r, dsr * dlr);
-            }
-        }
-        if (soc) {
-#pragma unroll
-            for (int j = 0; j < NQ; ++j) gap_a += (sq[j] + aa * dsq[j]) * (lq[j] + aa * dlq[j]);
-        }
-        gap_a = wave_sum(gap_a);
+        double quad[3], probe;
+        const double aa = fmin(1.0, max_step(false, quad, probe));
+        const double gap_a = wave_sum(fma(aa, fma(aa, quad[2], quad[1]), quad[0]));
         const double mu_a = gap_a / deg;
         const double sgm = mu > 0 ? pow(fmax(mu_a, 0.0) / mu, 3.0) : 0.0;
         // ---- corrector
@@ -1736,27 +1759,12 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
         stamp(3);
         newton(true, rcq2);
-        const double al = fmin(1.0, 0.99 * max_step(true));
+        // step fraction: 0.99, or 0.999 once the affine predictor takes a (nearly) full step (the end
+        // game, where a 0.99 cap alone limits the gap reduction to 100x per iteration)
+        const double al = fmin(1.0, (aa >= 0.99 ? 0.999 : 0.99) * max_step(true, quad, probe));
         stamp(3);
         {
-            double chk = al;
-#pragma unroll
-            for (int i = 0; i < NZ; ++i) chk += 0.0 * dz[i];
-            if (act) {  // slack / dual directions of the live rows (unused group / costate slots excluded)
-#pragma unroll
-                for (int r = 0; r < NR; ++r) {
-                    if (row_on(r)) {
-                        double dsr, dlr;
-                        row_dir(r, true, dsr, dlr);
-                        chk += 0.0 * (dsr + dlr);
-                    }
-                }
-                if (soc) {
-#pragma unroll
-                    for (int j = 0; j < NQ; ++j) chk += 0.0 * (dsq[j] + dlq[j]);
-                }
-            }
-            chk = wave_sum(chk);  // NaN / Inf anywhere in the direction poisons the sum
+            const double chk = wave_sum(al + probe);  // NaN / Inf anywhere in the direction poisons the sum
             if (!(chk == chk) || !(al > 0.0)) {
                 status = near ? SCVX_STATUS_MAX_ITER : SCVX_STATUS_NUMERICAL;
                 fail_code = 4.0;
@@ -1773,7 +1781,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
         if (a.trace && agent == a.trace_agent && lane == 0 && it < a.trace_cap) {
             double* tr_ = a.trace + 8 * it;
-            tr_[0] = pres; tr_[1] = dres; tr_[2] = gap; tr_[3] = pobj; tr_[4] = aa; tr_[5] = al; tr_[6] = sgm; tr_[7] = mu;
+            tr_[0] = pres; tr_[1] = dres; tr_[2] = gap; tr_[3] = pobj * osc; tr_[4] = aa; tr_[5] = al; tr_[6] = sgm; tr_[7] = mu;
         }
         // ---- update
 #pragma unroll
@@ -1825,7 +1833,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     }
     pobj = wave_sum(pobj);
     if (lane == 0) {
-        a.obj[agent] = pobj;
+        a.obj[agent] = pobj * osc;
         a.status[agent] = status;
         a.iters[agent] = it;
         if (a.trace && a.trace_agent < 0) a.trace[agent] = fail_code;  // diagnostics: every agent's exit code

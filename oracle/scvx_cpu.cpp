@@ -653,6 +653,15 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
     int status = SCVX_STATUS_MAX_ITER;
     int it = 0;
     const double tol = T->tol > 0 ? T->tol : 1e-9;
+    // objective scaling (kernel: osc): solve with the objective divided by max(1, ||q||_inf); the gap test
+    // and the reported objective are in the caller's units
+    double osc = 1.0;
+    for (int t = 0; t < K; ++t)
+        for (double v : ag.nd[t].q) osc = std::max(osc, std::fabs(v));
+    for (int t = 0; t < K; ++t) {
+        for (double& v : ag.nd[t].q) v /= osc;
+        for (double& v : ag.nd[t].pdiag) v /= osc;
+    }
     if (!init_point(ag)) { iters_out = 0; obj_out = 0.0; return SCVX_STATUS_NUMERICAL; }
     double dres_best = 1e300, pres_best = 1e300;
     for (it = 0;; ++it) {  // the residuals are evaluated once more after the last step (kernel: cap check)
@@ -749,13 +758,13 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
             }
         if (std::getenv("SCVX_DEBUG")) std::fprintf(stderr, "it %d pres %.3e dres %.3e mu %.3e pobj %.6e\n", it, pres, dres, mu, pobj);
         if (!std::isfinite(pres + dres + mu)) { status = SCVX_STATUS_NUMERICAL; break; }
-        const double pnorm = std::max(1.0, nb + nxv + nsl), dnorm = std::max(1.0, nq + nxv + nzd);
-        if (pres <= tol * pnorm && dres <= tol * dnorm && gap <= tol * std::max(1.0, std::fabs(pobj))) {
+        const double pnorm = std::max(1.0, nb + nxv + nsl), dnorm = std::max(1.0 / osc, nq + nxv / osc + nzd);  // caller's units / osc
+        if (pres <= tol * pnorm && dres <= tol * dnorm && gap * osc <= tol * std::max(1.0, std::fabs(pobj * osc))) {
             status = SCVX_STATUS_OPTIMAL;
             break;
         }
         // reduced tolerances (kernel: `near`): a breakdown below ends with MAX_ITER ("inaccurate")
-        const bool near = pres <= 1e-4 * pnorm && dres <= 1e-4 * dnorm && gap <= 5e-5 * std::max(1.0, std::fabs(pobj));
+        const bool near = pres <= 1e-4 * pnorm && dres <= 1e-4 * dnorm && gap * osc <= 5e-5 * std::max(1.0, std::fabs(pobj * osc));
         const int fail_status = near ? SCVX_STATUS_MAX_ITER : SCVX_STATUS_NUMERICAL;
         if (it >= T->max_iter) { status = fail_status; break; }
         // insufficient progress (kernel: fail code 7)
@@ -982,7 +991,11 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
                 }
             }
             if (!newton(rco, rcq, dz, ds, dl, dsq, dlq, dy, dyi, dyf)) { status = fail_status; break; }
-            double al = std::min(1.0, 0.99 * max_step(ds, dl, dsq, dlq));
+            // step fraction (kernel: the same rule): 0.99 of the way to the boundary, 0.999 once the
+            // affine predictor takes a (nearly) full step -- the end game, where a 0.99 cap alone
+            // limits the gap reduction to 100x per iteration
+            const double eta = (aa >= 0.99) ? 0.999 : 0.99;
+            double al = std::min(1.0, eta * max_step(ds, dl, dsq, dlq));
             if (near && al < 1e-2) { status = SCVX_STATUS_MAX_ITER; break; }  // stall at reduced accuracy (kernel)
             if (std::getenv("SCVX_DEBUG")) {
                 std::fprintf(stderr, "   alpha_aff %.3e sigma %.3e alpha %.3e\n", aa, sig, al);
@@ -1008,7 +1021,7 @@ done:
             double zj = ag.nd[t].z[j];
             pobj += 0.5 * ag.nd[t].pdiag[j] * zj * zj + ag.nd[t].q[j] * zj;
         }
-    obj_out = pobj;
+    obj_out = pobj * osc;
     iters_out = it;
     return status;
 }
