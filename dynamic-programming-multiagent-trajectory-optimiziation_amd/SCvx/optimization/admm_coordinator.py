@@ -24,10 +24,12 @@ import numpy as np
 import scvx_hip
 
 from ..discretization.first_order_hold import FirstOrderHold
-from ..global_parameters import K
+from ..global_parameters import TRUST_RADIUS0, WEIGHT_NU, WEIGHT_SIGMA, WEIGHT_SLACK, K
 from ..utils.multi_agent_logging import print_iteration, print_summary
-from .admm_utils import dual_residual, primal_residual
-from .agent_solver import AgentSolver, solve_agents_batched
+from .admm_utils import WEIGHT_COLLISION_SLACK
+from .agent_solver import AgentSolver
+from .sc_problem import _solver
+from .variables import ProblemResult, SolverError
 
 
 def discretize_batched(discretizers, X_list, U_list, sigma):
@@ -61,51 +63,99 @@ class ADMMCoordinator:
         self.discretizers = [FirstOrderHold(multi_agent_model.models[i], K) for i in range(self.N)]
 
     def solve(self, X_refs: list, U_refs: list, sigma_ref: float, verbose: bool = True):
-        pd = self.pos_dim
-        for solver in self.agent_solvers:
-            for j in solver.Y:
-                solver.Y[j].value = np.asarray(X_refs[j])[0:pd, :]
-                solver.Lambda[j].value = np.zeros((pd, K))
-        X_curr, U_curr = list(X_refs), list(U_refs)
-        primal_hist, dual_hist = [], []
+        """The reference's rounds (admm_coordinator.py:53-118) with every iterate device-resident:
+        per round one FOH launch, the subproblems (one batched launch in Jacobi mode, N single-agent
+        launches in the reference's Gauss-Seidel order), one consensus / dual-update launch
+        (scvx_admm_consensus_batched) for all (i, j) pairs.  The host reads one status word per round
+        (a failed subproblem raises SolverError, where cvxpy would) and the residual history at the end."""
+        import torch
+        pd, N, Kn = self.pos_dim, self.N, K
+        d0 = self.discretizers[0]
+        dev = d0._device
+        T = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=float), dtype=torch.float64, device=dev)  # noqa: E731
+        X = T(np.stack([np.asarray(x, float).T for x in X_refs]))          # (N, K, n)
+        U = T(np.stack([np.asarray(u, float).T for u in U_refs]))          # (N, K, m)
+        X0, U0 = X.clone(), U.clone()
+        nbr_h = np.array([[j for j in range(N) if j != i] for i in range(N)], dtype=np.int32).reshape(N, N - 1)
+        nbr = torch.as_tensor(nbr_h, device=dev)
+        nbr_l = nbr.long()
+        # Y_ij <- X_refs[j] positions, Lambda_ij <- 0 (:64-68); layout (N, N-1, K, pos_dim)
+        Y = X[nbr_l][..., :pd].contiguous()
+        Lam = torch.zeros_like(Y)
+        pr = torch.zeros((self.max_iter, N, N - 1), dtype=torch.float64, device=dev)
+        du = torch.zeros_like(pr)
+        probs = [s.scp for s in self.agent_solvers]
+        for p in probs:
+            p.set_parameters(weight_nu=WEIGHT_NU, weight_slack=WEIGHT_SLACK, weight_sigma=WEIGHT_SIGMA,
+                             tr_radius=TRUST_RADIUS0, sigma_ref=float(sigma_ref))
+        spec = probs[0].spec(n_nbr=N - 1, rho=float(self.rho_admm), d_min=float(self.model.d_min),
+                             w_coll=WEIGHT_COLLISION_SLACK, max_iter=100, tol=1e-9)
+        key = bytes(spec.to_c())
+        for p in probs[1:]:
+            if bytes(p.spec(n_nbr=N - 1, rho=float(self.rho_admm), d_min=float(self.model.d_min),
+                            w_coll=WEIGHT_COLLISION_SLACK, max_iter=100, tol=1e-9).to_c()) != key:
+                raise ValueError("ADMMCoordinator: agents must share one subproblem template")
+        cons = [p.model.scp_constraints() for p in probs]
+        x_init = T(np.stack([np.asarray(c["x_init"], float).reshape(-1) for c in cons]))
+        x_final = T(np.stack([np.asarray(c["x_final"], float).reshape(-1) for c in cons]))
+        sig = torch.full((N,), float(sigma_ref), dtype=torch.float64, device=dev)
+        tr = torch.full((N,), float(TRUST_RADIUS0), dtype=torch.float64, device=dev)
+        batch = _solver(spec, N, dev) if self.mode == "jacobi" else _solver(spec, 1, dev)
+        disc = None
+        out = None
         t0 = time.time()
         for it in range(self.max_iter):
-            mats = discretize_batched(self.discretizers, X_curr, U_curr, sigma_ref)
-            new_positions = [None] * self.N
+            disc = scvx_hip.foh_batched(d0._name, X, U, sig, nsub=d0._nsub, params=d0._params, out=disc)
+            Xr, Ur = (X0, U0) if self.trust_ref_is_initial else (X, U)
             if self.mode == "jacobi":
-                snap = list(X_curr)
-                for i, solver in enumerate(self.agent_solvers):
-                    solver.setup(self._tr_ref(i, X_refs, X_curr), self._tr_ref(i, U_refs, U_curr), sigma_ref,
-                                 mats[i], {j: snap[j] for j in range(self.N) if j != i})
-                res = solve_agents_batched(self.agent_solvers)
-                for i, (X_i, U_i, _, _, p_i) in enumerate(res):
-                    X_curr[i], U_curr[i], new_positions[i] = X_i, U_i, p_i
+                pos = X[nbr_l][..., :pd].contiguous()                # every agent sees the previous round
+                out = batch.solve(disc, Xr.clone(), Ur.clone(), sig, tr, x_init, x_final, nbr_pos=pos, nbr_Y=Y,
+                                  nbr_Lam=Lam)
+                bad = out["status"] >= 2
+                X, U = out["X"].clone(), out["U"].clone()
             else:
-                for i, solver in enumerate(self.agent_solvers):
-                    solver.setup(self._tr_ref(i, X_refs, X_curr), self._tr_ref(i, U_refs, U_curr), sigma_ref,
-                                 mats[i], {j: X_curr[j] for j in range(self.N) if j != i})
-                    X_i, U_i, _, _, p_i = solver.solve(solver="ECOS")
-                    X_curr[i], U_curr[i], new_positions[i] = X_i, U_i, p_i
-            pr_vals, du_vals = [], []
-            for solver in self.agent_solvers:
-                for j in solver.Y:
-                    p_j = new_positions[j]
-                    Y_old = solver.Y[j].value
-                    Y_new = 0.5 * (Y_old + p_j)
-                    solver.Y[j].value = Y_new
-                    solver.Lambda[j].value = solver.Lambda[j].value + self.rho_admm * (p_j - Y_new)
-                    pr_vals.append(primal_residual(p_j, Y_new))
-                    du_vals.append(dual_residual(Y_new, Y_old))
-            pr_avg, du_avg = float(np.mean(pr_vals)), float(np.mean(du_vals))
-            primal_hist.append(pr_avg)
-            dual_hist.append(du_avg)
+                bad = torch.zeros(N, dtype=torch.bool, device=dev)
+                outs = []
+                for i in range(N):                                    # agent i sees agents j < i of this round
+                    s_ = slice(i, i + 1)
+                    pos = X[nbr_l[i]][..., :pd].unsqueeze(0).contiguous()
+                    o = batch.solve(disc[s_], Xr[s_].clone(), Ur[s_].clone(), sig[s_], tr[s_], x_init[s_], x_final[s_],
+                                    nbr_pos=pos, nbr_Y=Y[s_], nbr_Lam=Lam[s_])
+                    bad[i] = o["status"][0] >= 2
+                    X[i], U[i] = o["X"][0], o["U"][0]
+                    outs.append({k: v.clone() for k, v in o.items()})
+                out = {k: torch.cat([o[k] for o in outs]) for k in outs[0]}
+            if bool(bad.any()):                                       # one host read per round
+                i = int(bad.nonzero()[0, 0])
+                raise SolverError(f"ADMM round {it}: subproblem of agent {i} failed (status "
+                                  f"{int(out['status'][i])})")
+            scvx_hip.admm_consensus(X, nbr, self.rho_admm, Y, Lam, pd, primal=pr[it], dual=du[it], check_index=False)
             if verbose:
-                print_iteration(it, nu_norm=0.0, slack_norm=0.0, primal_res=pr_avg, dual_res=du_avg, dx=0.0, ds=0.0,
-                                sigma=sigma_ref, tr_radius=self.rho_admm)
+                print_iteration(it, nu_norm=0.0, slack_norm=0.0, primal_res=float(pr[it].mean()),
+                                dual_res=float(du[it].mean()), dx=0.0, ds=0.0, sigma=sigma_ref, tr_radius=self.rho_admm)
         runtime = time.time() - t0
+        primal_hist = [float(v) for v in pr.mean(dim=(1, 2)).cpu().numpy()]
+        dual_hist = [float(v) for v in du.mean(dim=(1, 2)).cpu().numpy()]
+        self._publish(X, U, Y, Lam, out)
         if verbose:
             print_summary(len(primal_hist), sigma_ref, runtime)
-        return X_curr, U_curr, sigma_ref, primal_hist, dual_hist
+        Xh, Uh = X.cpu().numpy(), U.cpu().numpy()
+        return [Xh[i].T.copy() for i in range(N)], [Uh[i].T.copy() for i in range(N)], sigma_ref, primal_hist, dual_hist
+
+    def _publish(self, X, U, Y, Lam, out):
+        """The reference's host-visible state after solve(): Y / Lambda parameters, every AgentSolver's
+        last subproblem solution (.scp .var / .prob) and collision slacks."""
+        host = {k: v.cpu().numpy() for k, v in out.items()}
+        Yh, Lh = Y.cpu().numpy(), Lam.cpu().numpy()
+        for i, solver in enumerate(self.agent_solvers):
+            js = sorted(solver.Y)
+            solver.scp.store(host, i)
+            solver.prob = ProblemResult()
+            solver.prob.status, solver.prob.value = solver.scp.prob.status, solver.scp.prob.value
+            for slot, j in enumerate(js):
+                solver.Y[j].value = Yh[i, slot].T.copy()
+                solver.Lambda[j].value = Lh[i, slot].T.copy()
+                solver.S[j].value = np.maximum(host["s_nbr"][i][slot], 0.0).reshape(-1, 1)
 
     def _tr_ref(self, i, refs, curr):
         return refs[i] if self.trust_ref_is_initial else curr[i]

@@ -364,6 +364,35 @@ class SCPSolver:
                     s_nbr=self.s_nbr[:, :self.spec.n_nbr], obj=self.obj, status=self.status, iters=self.iters)
 
 
+def admm_consensus(X_new, nbr, rho, Y, Lam, pos_dim, primal=None, dual=None, stream=None, check_index=True):
+    """ADMM consensus / dual update of every (agent, neighbour slot) in one launch
+    (scvx_admm_consensus_batched; the host loop of SCvx/optimization/admm_coordinator.py:80-96).
+    X_new (N,K,n) float64, nbr (N,n_nbr) int32 neighbour indices, Y / Lam (N,n_nbr,K,pos_dim) updated in
+    place.  Returns device tensors primal, dual (N,n_nbr): ||p_j - Y_new||_F, ||Y_new - Y_old||_F.
+    check_index=False skips the range check of nbr (a device -> host read) for callers that built nbr
+    themselves (the coordinators validate it once)."""
+    torch = _torch()
+    N, K, n = X_new.shape
+    n_nbr = nbr.shape[1] if nbr.dim() == 2 else 0
+    shp = (N, n_nbr, K, pos_dim)
+    if tuple(nbr.shape) != (N, n_nbr) or tuple(Y.shape) != shp or tuple(Lam.shape) != shp:
+        raise ValueError(f"admm_consensus: nbr (N,n_nbr), Y / Lam {shp} expected")
+    if not 1 <= pos_dim <= n:
+        raise ValueError("admm_consensus: pos_dim out of range")
+    if check_index and n_nbr and (int(nbr.min()) < 0 or int(nbr.max()) >= N):
+        raise ValueError("admm_consensus: neighbour index out of range")
+    if primal is None:
+        primal = torch.empty((N, n_nbr), dtype=torch.float64, device=X_new.device)
+    if dual is None:
+        dual = torch.empty((N, n_nbr), dtype=torch.float64, device=X_new.device)
+    rc = lib().scvx_admm_consensus_batched(N, n_nbr, K, pos_dim, n, _dev(X_new, name="X_new"),
+                                           _dev(nbr, torch.int32, "nbr"), float(rho), _dev(Y, name="Y"),
+                                           _dev(Lam, name="Lam"), _dev(primal, name="primal"), _dev(dual, name="dual"),
+                                           _stream(stream))
+    check(rc, "scvx_admm_consensus_batched")
+    return primal, dual
+
+
 def intersample_batched(model, X, U, sigma, obstacles, proj=None, dt=1.0, seg_dt=None, num_samples=100, eps=1e-4,
                         tol=1e-6, max_crit=8, nsub=None, params=None, stream=None):
     """Inter-sample obstacle minima for every (agent, segment, obstacle) (scvx_intersample_batched;

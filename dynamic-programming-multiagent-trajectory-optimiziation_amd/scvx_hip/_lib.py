@@ -19,7 +19,7 @@ STATUS = {0: "optimal", 1: "optimal_inaccurate", 2: "solver_error"}
 EXPORTS = ("scvx_version", "scvx_last_error", "scvx_foh_batched", "scvx_integrate_nonlinear_batched",
            "scvx_qp_solve_batched", "scvx_qp_workspace_bytes", "scvx_qp_set_trace",
            "scvx_collision_rows_batched", "scvx_collision_check_batched", "scvx_scp_solve_batched", "scvx_scp_workspace_bytes",
-           "scvx_intersample_batched")
+           "scvx_intersample_batched", "scvx_admm_consensus_batched")
 
 
 class ScvxError(RuntimeError):
@@ -96,6 +96,7 @@ def lib():
         L.scvx_scp_workspace_bytes.restype = sz
         L.scvx_scp_solve_batched.argtypes = [ctypes.POINTER(SCPTemplate), i32] + [vp] * 19 + [vp, sz, vp]
         L.scvx_intersample_batched.argtypes = [ctypes.POINTER(IntersampleTemplate), vp, i32, i32] + [vp] * 9
+        L.scvx_admm_consensus_batched.argtypes = [i32, i32, i32, i32, i32, vp, vp, dbl, vp, vp, vp, vp, vp]
         sized = ("scvx_last_error", "scvx_qp_workspace_bytes", "scvx_scp_workspace_bytes")
         for fn in EXPORTS:
             getattr(L, fn).restype = getattr(L, fn).restype if fn in sized else i32

@@ -270,6 +270,20 @@ int scvx_intersample_batched(const scvx_intersample_template* tpl, const double*
                              const double* X, const double* U, const double* sigma, int32_t* n_crit,
                              double* t_crit, double* h0, double* grad_x, double* grad_u, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * ADMM consensus / dual update of the multi-agent coordinators: replaces the host loop of
+ * SCvx/optimization/admm_coordinator.py:80-96 (si_admm_coordinator.py:91-102).  For agent i and
+ * neighbour slot s (j = nbr[i][s]), p_j = X_new[j][:, 0:pos_dim]:
+ *     Y_new = (Y + p_j) / 2;  Lam += rho (p_j - Y_new);
+ *     primal[i][s] = ||p_j - Y_new||_F;  dual[i][s] = ||Y_new - Y||_F   (admm_utils.py:20-38)
+ * Device buffers: X_new [N][K][n_x], nbr [N][n_nbr] int32, Y / Lam [N][n_nbr][K][pos_dim] (updated in
+ * place; the layout of scvx_scp_solve_batched's nbr_Y / nbr_Lam), primal / dual [N][n_nbr].  The
+ * element updates are bit-identical to the reference's numpy expressions.
+ */
+int scvx_admm_consensus_batched(int N, int n_nbr, int K, int pos_dim, int n_x, const double* X_new,
+                                const int32_t* nbr, double rho, double* Y, double* Lam, double* primal,
+                                double* dual, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

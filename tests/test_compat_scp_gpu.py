@@ -200,3 +200,30 @@ def test_si_admm_coordinator_jacobi_runs(cuda):
     for X, m in zip(X_out, mam.models):
         assert X.shape == (3, K) and np.allclose(X[:, 0], m.x_init) and np.allclose(X[:, -1], m.x_final)
         assert np.all(np.linalg.norm(np.diff(X, axis=1), axis=0) < 1e3)
+
+
+def test_admm_consensus_kernel_matches_reference_update(cuda):
+    """scvx_admm_consensus_batched vs the reference's host loop (admm_coordinator.py:80-91): the
+    consensus and dual variables bit for bit, the residual norms (admm_utils.py) to rounding."""
+    import torch
+    import scvx_hip
+    rng = np.random.default_rng(3)
+    N, K, n, pd, rho = 5, 37, 6, 3, 0.7
+    Xn = rng.normal(size=(N, K, n))
+    nbr = np.array([[j for j in range(N) if j != i] for i in range(N)], np.int32)
+    Y0 = rng.normal(size=(N, N - 1, K, pd))
+    L0 = rng.normal(size=(N, N - 1, K, pd))
+    T = lambda a, dt=torch.float64: torch.tensor(a, device=cuda, dtype=dt)  # noqa: E731
+    Y, Lam = T(Y0), T(L0)
+    pr, du = scvx_hip.admm_consensus(T(Xn), T(nbr, torch.int32), rho, Y, Lam, pd)
+    Yh, Lh, prh, duh = Y.cpu().numpy(), Lam.cpu().numpy(), pr.cpu().numpy(), du.cpu().numpy()
+    for i in range(N):
+        for s, j in enumerate(nbr[i]):
+            p_j = Xn[j][:, :pd].T                       # (pd, K), the reference's X_j[0:pd, :]
+            Y_old = Y0[i, s].T
+            Y_new = 0.5 * (Y_old + p_j)
+            Lam_new = L0[i, s].T + rho * (p_j - Y_new)
+            np.testing.assert_array_equal(Yh[i, s].T, Y_new)
+            np.testing.assert_array_equal(Lh[i, s].T, Lam_new)
+            assert prh[i, s] == pytest.approx(np.linalg.norm(p_j - Y_new), rel=1e-14)
+            assert duh[i, s] == pytest.approx(np.linalg.norm(Y_new - Y_old), rel=1e-14)
