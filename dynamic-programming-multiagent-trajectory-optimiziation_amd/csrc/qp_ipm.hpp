@@ -79,8 +79,9 @@ constexpr int qp_ncol(int nx, int nu, int nb, int ns, int ng) {
     return qp_dstr(nx, nu) + nx * nu + 4 * ns + 4 * ng + (nx + nu) + ng + ((1 << nu) + 2 * nb + ns + ng) + nu +
            ((nx + nu) + nx + 2 * (nu + 1) + ng) + (3 * (nu + 1) + 1 + (nu + 1));
 }
-// factor outputs per stage (stage-major block): K, kappa, LD, W2, P, Pi, u, Acl
-constexpr int qp_fbs(int nx, int nu) { return 3 * nu * nx + nu * nu + 3 * nx * nx + nx; }
+// factor outputs per stage (stage-major block): K, kappa, LD, W2, P, Pi, u, Acl, one junk slot (the
+// global store of lanes without an output of their own)
+constexpr int qp_fbs(int nx, int nu) { return 3 * nu * nx + nu * nu + 3 * nx * nx + nx + 1; }
 constexpr long long qp_ws_doubles(int nx, int nu, int nb, int ns, int ng) {
     return (long long)qp_ncol(nx, nu, nb, ns, ng) * 64 + 64LL * qp_pkt(nx, nu) + 64LL * qp_fbs(nx, nu) + 64;
 }
@@ -111,7 +112,8 @@ struct QPCfg {
     static constexpr int B_PI = B_P + NX * NX;     // Pi_t
     static constexpr int B_U = B_PI + NX * NX;     // P_{t+1} e_t
     static constexpr int B_ACL = B_U + NX;         // Acl_t = A_t + Bt_t K_t (row-major)
-    static constexpr int FBS = B_ACL + NX * NX;
+    static constexpr int B_JNK = B_ACL + NX * NX;  // junk slot (stores of lanes without an output)
+    static constexpr int FBS = B_JNK + 1;
     static_assert(FBS == qp_fbs(NX, NU), "factor block");
     // stage-minor workspace columns
     static constexpr int C_DT = 0;                 // disc, transposed: A (col-major) | B | C | S | z
@@ -131,9 +133,9 @@ struct QPCfg {
     static constexpr int NCOL = C_RHO + NQ;
     static_assert(NCOL == qp_ncol(NX, NU, NB, NS, NG), "column count");
     // LDS (doubles, compile-time offsets except the K-sized blocks at the end):
-    // factor: 2-slot packet ring, P', Pi' (col-major), T1, T2 (col-major), W1, W2 (col-major), Qh,
+    // factor: the current stage's packet, P', Pi' (col-major), T1, T2 (col-major), W1, W2 (col-major), Qh,
     // Sh (col-major), Rh, [K | kappa] (col-major), sink
-    static constexpr int F_RING = 0, F_PP = 2 * PKT, F_PIP = F_PP + NX * NX, F_T1 = F_PIP + NX * NX,
+    static constexpr int F_RING = 0, F_PP = PKT, F_PIP = F_PP + NX * NX, F_T1 = F_PIP + NX * NX,
                          F_T2 = F_T1 + NX * NX, F_W1 = F_T2 + NX * NU, F_W2 = F_W1 + NX * NX,
                          F_QH = F_W2 + NU * NX, F_SH = F_QH + NX * NX, F_RH = F_SH + NU * NX,
                          F_KK = F_RH + NU * NU, F_SINK = F_KK + 2 * NU * NX, F_END = qp_even(F_SINK + 8);
@@ -145,11 +147,12 @@ struct QPCfg {
     static constexpr int lds_doubles(int K) { return L_VAR + K * NX + (K + 1) * NX; }
 };
 
-// packed phase descriptors (all operands are contiguous LDS vectors):
-//   operand = LDS offset (15 bits) | ring-slot relative << 15
-//   output  = LDS offset | accumulate << 15 | stage-relative (Acl block) << 16 | (global column + 1) << 17
-//   base    = LDS offset | ring-slot relative << 15 | kind << 16   (kind 0: none, 1: always, 2: last stage)
-__host__ __device__ constexpr int qp_dpk(int off, int slot) { return off | (slot << 15); }
+// packed phase descriptors (all operands are contiguous LDS vectors; the stage packet always sits at
+// F_RING, so every offset is stage-invariant):
+//   operand = LDS offset (15 bits)
+//   output  = LDS offset | accumulate << 15 | (global column + 1) << 17
+//   base    = LDS offset | kind << 16   (kind 0: none, 1: always, 2: last stage)
+__host__ __device__ constexpr int qp_dpk(int off, int) { return off; }
 
 // Agent workspace accessor: raw buffer loads/stores with the lane part of the address in one
 // VGPR (voffset) and the column part as a (rematerialisable) SGPR constant (soffset), so no
@@ -186,10 +189,34 @@ __device__ __forceinline__ double qp_mask(int a, int b) {
     return (double)m;
 }
 
+// One lane's repetition of a factor phase, decoded once per sweep (the offsets are stage-invariant)
+struct QPRep {
+    int L, R, B, O, G;   // LDS operand / base / output offsets; byte voffset of the global store
+    double b1, b2, acc;  // base multipliers (every stage, last stage only); 1 if the output accumulates
+};
+// lsink: LDS sink (outputs that go nowhere in LDS, and accumulating outputs, which live in registers
+// during the sweep); jnk: the junk slot of the stage block
+__device__ __forceinline__ QPRep qp_decode(const int (&d)[4], int one, int lsink, int jnk) {
+    QPRep q;
+    q.L = d[0] & 0x7FFF;
+    q.R = d[1] & 0x7FFF;
+    const int bk = d[3] >> 16;
+    q.B = bk ? (d[3] & 0x7FFF) : one;
+    q.b1 = bk == 1 ? 1.0 : 0.0;
+    q.b2 = bk == 2 ? 1.0 : 0.0;
+    const int O = d[2];
+    const bool on = O >= 0, acc = on && ((O >> 15) & 1);
+    q.O = (on && !acc) ? (O & 0x7FFF) : lsink;
+    q.acc = acc ? 1.0 : 0.0;
+    const int g = on ? (O >> 17) - 1 : -1;
+    q.G = (g >= 0 ? g : jnk) * 8;
+    return q;
+}
+
 template <int KK>
-__device__ __forceinline__ double qp_dot(const double* lds, int L, int R, int soff) {
-    const double* lp = lds + (L & 0x7FFF) + ((L >> 15) & 1) * soff;
-    const double* rp = lds + (R & 0x7FFF) + ((R >> 15) & 1) * soff;
+__device__ __forceinline__ double qp_dot(const double* lds, int L, int R) {
+    const double* lp = lds + L;
+    const double* rp = lds + R;
     double acc0 = 0.0, acc1 = 0.0;
 #pragma unroll
     for (int k = 0; k < KK; ++k) {
@@ -198,35 +225,22 @@ __device__ __forceinline__ double qp_dot(const double* lds, int L, int R, int so
     return acc0 + acc1;
 }
 
-// One element-parallel phase of the factor sweep: every lane evaluates its NREP descriptors
-// (out = base + sum_k L[k] R[k]).  The descriptors are made opaque once, at the top of the phase
-// (one scheduling barrier), so their decoding is neither hoisted out of the sweep (register
-// pressure) nor serialised between the repetitions.
+// One element-parallel phase of the factor sweep: every lane evaluates its NREP repetitions
+// (out = base + sum_k L[k] R[k]), writes each to its LDS slot and its global column, and adds the
+// accumulating ones (M, xe: summed over the stages) into registers -- no LDS read-modify-write on the
+// sweep's chain.
 template <int KK, int NREP>
-__device__ __forceinline__ void qp_phase(double* lds, const int (&d)[NREP][4], int soff, bool last, int acl_off,
-                                         const QPBuf& wb, int fbo, int lsink, int vsink) {
-    int Ld[NREP], Rd[NREP], Od[NREP], Bd[NREP];
-#pragma unroll
-    for (int r = 0; r < NREP; ++r) {
-        Ld[r] = d[r][0]; Rd[r] = d[r][1]; Od[r] = d[r][2]; Bd[r] = d[r][3];
-        asm volatile("" : "+v"(Ld[r]), "+v"(Rd[r]), "+v"(Od[r]), "+v"(Bd[r]));
-    }
+__device__ __forceinline__ void qp_phase(double* lds, const QPRep (&d)[NREP], double blast, const QPBuf& wb, int fbo,
+                                         double (&areg)[NREP]) {
     double val[NREP];
 #pragma unroll
-    for (int r = 0; r < NREP; ++r) {
-        const int bk = Bd[r] >> 16;
-        const double bv = lds[(Bd[r] & 0x7FFF) + ((Bd[r] >> 15) & 1) * soff];
-        val[r] = qp_dot<KK>(lds, Ld[r], Rd[r], soff) + ((bk == 1 || (bk == 2 && last)) ? bv : 0.0);
-    }
+    for (int r = 0; r < NREP; ++r)
+        val[r] = fma(lds[d[r].B], d[r].b1 + blast * d[r].b2, qp_dot<KK>(lds, d[r].L, d[r].R));
 #pragma unroll
     for (int r = 0; r < NREP; ++r) {
-        const int O = Od[r];
-        const bool on = O >= 0;
-        const int oo = on ? (O & 0x7FFF) + ((O >> 16) & 1) * acl_off : lsink;
-        const double old = lds[oo];
-        lds[oo] = (on && ((O >> 15) & 1)) ? old + val[r] : val[r];
-        const int g = on ? (O >> 17) - 1 : -1;
-        wb.st(g >= 0 ? g * 8 : vsink, fbo, val[r]);
+        lds[d[r].O] = val[r];
+        areg[r] = fma(d[r].acc, val[r], areg[r]);
+        wb.st(d[r].G, fbo, val[r]);
     }
 }
 
@@ -265,7 +279,6 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     const int vt = t * 8;  // this lane's element of a stage-minor column
     constexpr int PKB = C::NCOL * WAVE * 8;  // byte offset of the packets [t][PKT]
     constexpr int FBB = PKB + WAVE * PKT * 8;  // byte offset of the factor output blocks [t][FBS]
-    constexpr int SKB = FBB + WAVE * C::FBS * 8;  // byte offset of the per-lane store sink (past every block)
     const int vpk = t * PKT * 8;
     const int vfb = t * C::FBS * 8;
     // Loads go through `vcur`, this lane's offset re-derived (opaquely) at the start of every
@@ -482,12 +495,22 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 d4[rep][0] = L; d4[rep][1] = R; d4[rep][2] = O; d4[rep][3] = B;
             }
         }
+        // decoded once per sweep; accumulating outputs (xe, M) are summed in registers
+        QPRep q1[R1], q2[R2], q4[R4];
+        double a1[R1], a2[R2], a4[R4];
+#pragma unroll
+        for (int r = 0; r < R1; ++r) { q1[r] = qp_decode(d1[r], V_ONE, C::F_SINK, C::B_JNK); a1[r] = 0.0; }
+#pragma unroll
+        for (int r = 0; r < R2; ++r) { q2[r] = qp_decode(d2[r], V_ONE, C::F_SINK, C::B_JNK); a2[r] = 0.0; }
+#pragma unroll
+        for (int r = 0; r < R4; ++r) { q4[r] = qp_decode(d4[r], V_ONE, C::F_SINK, C::B_JNK); a4[r] = 0.0; }
         for (int e = lane; e < NX * NX; e += WAVE) { lds[C::F_PP + e] = 0.0; lds[C::F_PIP + e] = 0.0; lds[V_M + e] = 0.0; }
         if (lane < NX) lds[V_XE + lane] = 0.0;
         if (lane == 0) lds[V_FLAG] = 0.0;
         __syncthreads();  // the node phase wrote the packets (global) from other lanes
-        // packets stream through a 2-slot LDS ring, loads issued 3 stages ahead (register buffers
-        // pf[0..2], so the stage loop is unrolled by 3 to keep their indices static)
+        // packets stream through one LDS slot (a stage's packet is overwritten by the next one after its
+        // last read), loads issued 3 stages ahead (register buffers pf[0..2], so the stage loop is
+        // unrolled by 3 to keep their indices static)
         double pf[3][PFN];
         auto pf_load = [&](int ts, double* b) __attribute__((always_inline)) {
 #pragma unroll
@@ -500,7 +523,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
             for (int k = 0; k < PFN; ++k) {
                 const int e = lane + WAVE * k;
-                lds[e < PKT ? C::F_RING + (ts & 1) * PKT + e : C::F_SINK] = b[k];
+                lds[e < PKT ? C::F_RING + e : C::F_SINK] = b[k];
             }
         };
         pf_load(K - 1, pf[0]);
@@ -512,21 +535,16 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         bool bad = false;
         // one stage; buffer `nb` receives stage ts-3 (issued now), buffer `cb` holds stage ts-1
         auto stage = [&](int ts, double* nb, const double* cb) __attribute__((always_inline)) {
-            const int soff = (ts & 1) * PKT;
             const bool last = ts == K - 1;
-            const int acl_off = ts * NX * NX;
+            const double blast = last ? 1.0 : 0.0;
             const int fbo = FBB + ts * C::FBS * 8;  // byte offset of this stage's output block
             pf_load(ts - 3, nb);  // unconditional: stage K-1 re-issues K-4, ts-3 < 0 reads zeros
-            const bool fst = ts >= 20 && ts < 30;
-            if (fst) stamp(-1);
             // ---- phase 1: T1 = P'A, T2 = P'Bt, W1 = A'Pi', W2 = Bt'Pi', u = P'e, xe += Pi''e
-            qp_phase<NX, R1>(lds, d1, soff, last, acl_off, wb, fbo, C::F_SINK, SKB - fbo + lane * 8);
+            qp_phase<NX, R1>(lds, q1, blast, wb, fbo, a1);
             wsync();
-            if (fst) stamp(11);
             // ---- phase 2: Qh = Q + A'T1, Sh = S' + Bt'T1, Rh = R + Bt'T2
-            qp_phase<NX, R2>(lds, d2, soff, last, acl_off, wb, fbo, C::F_SINK, SKB - fbo + lane * 8);
+            qp_phase<NX, R2>(lds, q2, blast, wb, fbo, a2);
             wsync();
-            if (fst) stamp(12);
             // ---- phase 3: Rh = L D L' in registers (every lane); [K | kappa] = -Rh^-1 [Sh | W2]
             {
                 const bool fx = last && T.fix_last_input;
@@ -590,7 +608,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                     for (int i = 0; i < NU; ++i) {
                         const double v = fx ? 0.0 : -x[i];
                         lds[kl ? C::F_KK + c * NU + i : C::F_SINK] = v;
-                        wb.st(kl ? (g + i * NX) * 8 : SKB - fbo + lane * 8, fbo, v);
+                        wb.st((kl ? g + i * NX : C::B_JNK) * 8, fbo, v);
                     }
                 }
                 {
@@ -600,18 +618,16 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                         const int ei = e / NU, ej = e % NU;
                         v = fma(qp_mask(e, lane), (ei > ej) ? Lm[e] : (ei == ej ? dinv[ei] : 0.0), v);
                     }
-                    wb.st(lane < NU * NU ? (C::B_LD + lane) * 8 : SKB - fbo + lane * 8, fbo, v);
+                    wb.st((lane < NU * NU ? C::B_LD + lane : C::B_JNK) * 8, fbo, v);
                 }
             }
             wsync();
-            if (fst) stamp(13);
             // ---- phase 4: P = Qh + Sh'K, Pi = W1 + Sh'kappa, M += W2'kappa, Acl = A + Bt K
-            qp_phase<NU, R4>(lds, d4, soff, last, acl_off, wb, fbo, C::F_SINK, SKB - fbo + lane * 8);
+            qp_phase<NU, R4>(lds, q4, blast, wb, fbo, a4);
             if (ts > 0) pf_store(ts - 1, cb);
             wsync();
-            if (fst) stamp(14);
         };
-        // stage K-1 uses slot (K-1)&1 (stored), K-2 in pf[1], K-3 in pf[2], K-4 in pf[0]
+        // stage K-1's packet is in LDS, K-2 in pf[1], K-3 in pf[2], K-4 in pf[0]
         int ts = K - 1;
         stage(ts, pf[0], pf[1]);  // (its load of K-4 went out before the loop)
         --ts;
@@ -624,6 +640,13 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             --ts;
         }
         if (bad) lds[V_FLAG] = 1.0;  // any lane (all agree)
+        // the register-accumulated outputs (xe, M) to their LDS homes
+#pragma unroll
+        for (int r = 0; r < R1; ++r)
+            if (d1[r][2] >= 0 && ((d1[r][2] >> 15) & 1)) lds[d1[r][2] & 0x7FFF] = a1[r];
+#pragma unroll
+        for (int r = 0; r < R4; ++r)
+            if (d4[r][2] >= 0 && ((d4[r][2] >> 15) & 1)) lds[d4[r][2] & 0x7FFF] = a4[r];
         wsync();
         // Pi_0 -> persistent; LU with partial pivoting of M (lane 0, registers)
         for (int e = lane; e < NX * NX; e += WAVE) lds[V_PI0 + e] = lds[C::F_PIP + (e % NX) * NX + e / NX];
