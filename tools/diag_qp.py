@@ -101,7 +101,7 @@ def run(cfg="c5", iters=7):
         scvx_hip.lib().scvx_qp_set_trace(None, 0, 0)
         st = o["status"].cpu().numpy()
         cd = codes.cpu().numpy().astype(int)
-        print(f"iter {it}: tr {trp[0].item():.4g} status {np.bincount(st, minlength=3)} exit codes "
+        print(f"iter {it}: tr {trp.min().item():.4g}..{trp.max().item():.4g} status {np.bincount(st, minlength=3)} exit codes "
               f"{dict(zip(*np.unique(cd[st == 2], return_counts=True)))} iters mean {o['iters'].float().mean().item():.1f} "
               f"check {drv.last_check}", flush=True)
         bad = np.nonzero(st == 2)[0]
