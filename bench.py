@@ -98,8 +98,10 @@ def committed_traffic(kernel_prefix="scvx::qp_ipm_kernel<scvx::QPCfg<6, 3, 2, 8,
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")))  # round-tagged names
     for f in reversed(files):
         d = json.load(open(f))
-        for k, v in d.items():
-            if k.startswith(kernel_prefix):
+        if str(d.get("kernel", "")).startswith(kernel_prefix) and "traffic_bytes" in d:   # tools/pmc_summary.py
+            return d["traffic_bytes"], os.path.relpath(f, REPO)
+        for k, v in d.items():                                                            # round-1 format
+            if k.startswith(kernel_prefix) and isinstance(v, dict):
                 return v["traffic_bytes"], os.path.relpath(f, REPO)
     return None, None
 
@@ -175,15 +177,19 @@ def cpu_baseline(sc, n_sample, threads, min_seconds=8.0, tol=1e-9):
 
 
 def cpu_baselines(sc, n_sample, tol):
-    """All-core (nproc threads, OpenMP over agents) and single-core CPU figures of the restatement."""
+    """All-core and single-core CPU figures of the restatement.  "All cores" is every CPU this process may
+    run on: nproc, capped by the cgroup CPU quota when one is set (the GPU box grants 16 CPUs of a
+    256-thread host; more OpenMP threads than that only time-slice)."""
     info = host_info()
-    threads = info["nproc"]
+    quota = info.get("cgroup_cpu_quota")
+    threads = max(1, min(info["nproc"], int(quota))) if quota else info["nproc"]
     v_all, reps, el = cpu_baseline(sc, n_sample, threads, tol=tol)
     n1 = min(n_sample, 64)
     v_one, reps1, el1 = cpu_baseline(sc, n1, 1, tol=tol)
     return dict(value=v_all, unit="SCvx-iterations/s (N=1024-agent equivalent)", cores=threads, kind="port",
                 sample=f"{reps} x one SCvx iteration of {n_sample} of the {N_AGENTS} agents (FOH C + structured IPM "
-                       f"C++, -O3 x86-64-v3, OpenMP over agents on {threads} threads), {el:.1f} s wall",
+                       f"C++, -O3 x86-64-v3, OpenMP over agents on {threads} threads = the CPUs this process may use: "
+                       f"nproc {info['nproc']}, cgroup quota {quota}), {el:.1f} s wall",
                 single_core={"value": v_one, "cores": 1,
                              "sample": f"{reps1} x one SCvx iteration of {n1} agents on 1 thread, {el1:.1f} s wall"},
                 host=info)
