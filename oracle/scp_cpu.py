@@ -20,6 +20,8 @@ Newton systems are solved by a Riccati recursion over the nodes (state n+4, inpu
 """
 import itertools
 
+import os
+
 import numpy as np
 from scipy.linalg import solve_triangular
 
@@ -162,13 +164,27 @@ def build_nodes(p):
 
 def ldl_solve(M, b, rel=1e-13):
     """LDL' solve of a symmetric (quasi-)definite block, pivots below rel * max|diag| clamped --
-    the dynamic regularisation the kernel applies (IPM end-game normal matrices lose definiteness
-    in rounding when barrier curvatures span > 1e16)."""
+    the dynamic regularisation the kernel applies (csrc/scp_ipm.hip ldl_factor; IPM end-game normal
+    matrices lose definiteness in rounding when barrier curvatures span > 1e16).
+
+    Near the optimum the LP-like directions (nu, the norm epigraphs) carry curvature ~reg against ~1e6
+    elsewhere, so the Riccati Schur complements are conditioned ~1e16; rounding can then leave a pivot
+    clearly negative (-7e-2 on the ADMM unicycle instance of tests/test_scp_gpu.py), the clamp turns it
+    into a 1e12 gain and the recursion overflows within a few stages.  The kernel (different rounding
+    order) did not hit it on that instance.  Both treat a non-finite factor or direction as a breakdown
+    (reduced-accuracy exit), so the overflow is an expected, handled event here: no FP warnings.  A
+    max(|d|, clamp) pivot rule removes the overflow but perturbed the kernel's directions enough to fail
+    two GPU parity tests, so it is not used."""
     nn = M.shape[0]
     Lm = np.eye(nn)
     d = np.zeros(nn)
     A = M.copy()
     dmax = np.abs(np.diag(M)).max()
+    with np.errstate(over="ignore", invalid="ignore"):
+        return _ldl_solve(A, Lm, d, dmax, nn, b, rel)
+
+
+def _ldl_solve(A, Lm, d, dmax, nn, b, rel):
     for j in range(nn):
         dj = A[j, j] - (Lm[j, :j] ** 2) @ d[:j]
         dj = max(dj, rel * dmax + 1e-300)
@@ -341,6 +357,13 @@ class SCPSolver:
             Wn = [self._nt(nd, s[k], lam[k]) for k, nd in enumerate(nodes)]
             lt = [self._Wmul(nd, Wn[k], lam[k], 0) for k, nd in enumerate(nodes)]   # lambda~ = W lam
             Hs = []
+            if os.environ.get("SCP_DEBUG"):
+                dm = max((float((1.0 / Wn[k][0] ** 2).max(initial=0)), k) for k in range(K))
+                kk = dm[1]
+                dd = 1.0 / Wn[kk][0] ** 2
+                rr = int(np.argmax(dd))
+                print(f"it {it} pres {pres:.2e} dres {dres:.2e} gap {gap:.2e} max D {dm[0]:.3e} node {kk} row {rr} "
+                      f"s {s[kk][rr]:.3e} lam {lam[kk][rr]:.3e} nh {len(nodes[kk]['hard'])}")
             for k, nd in enumerate(nodes):
                 H = nd["P"].copy()
                 wl, socW = Wn[k]
@@ -455,6 +478,7 @@ class SCPSolver:
             kk = -ldl_solve(Quu, qu)
             P = Qxx + Qux.T @ Kk
             P = 0.5 * (P + P.T)
+
             pv = qx + Qux.T @ kk
             Ps[k], ps[k], Ks[k], ks[k] = P, pv, Kk, kk
         # stage 0: x part fixed, g part free
