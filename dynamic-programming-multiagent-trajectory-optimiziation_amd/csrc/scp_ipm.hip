@@ -40,6 +40,7 @@ struct SCPArgs {
     scvx_scp_template T;
     int N;
     const double *disc, *Xref, *Uref, *sigma_ref, *tr, *x_init, *x_final, *nbr_pos, *nbr_Y, *nbr_Lam;
+    const double *X_prev, *slab_z, *slab_P;  // Nash best response (T.game)
     double *X, *U, *nu, *sigma, *s_obs, *s_nbr, *obj;
     int32_t *status, *iters;
     double* ws;
@@ -53,13 +54,18 @@ struct SCPLay {
         o_t, o_rho, o_rhs, o_dz, o_dsig, o_ds, o_dl, o_dsa, o_dla, o_y, o_yp, o_rp, o_K, o_Pr, o_pv, o_kv, o_LD, o_nh;
 };
 
+// augmented game states: u~_k = u_{k-1} (m), th~_k = th_{k-1} (1 when the model has a heading)
+__host__ __device__ inline int scp_ne(const scvx_scp_template& T) {
+    return T.game ? T.n_u + (T.theta_idx >= 0 ? 1 : 0) : 0;
+}
+
 __host__ __device__ inline SCPLay scp_layout(const scvx_scp_template& T) {
     const int n = T.n_x, m = T.n_u;
-    const int NXA = n + SCP_NG, NUA = m + n, NZ = NXA + NUA;
+    const int NXA = n + SCP_NG + scp_ne(T), NUA = m + n, NZ = NXA + NUA;
     SCPLay L{};
     int sides = 0;
     for (int b = 0; b < T.n_ubound; ++b) sides += (T.ub_has_lo[b] ? 1 : 0) + (T.ub_has_hi[b] ? 1 : 0);
-    L.RH = (1 << n) + (1 << m) + (1 << n) + sides + 2 * T.n_xbound + 3;
+    L.RH = (1 << n) + (1 << m) + (1 << n) + sides + 2 * T.n_xbound + 3 + (T.game ? T.n_slab : 0);
     L.NS = T.n_obs + T.n_nbr;
     L.Q = T.has_soc ? m + 1 : 0;
     L.RL = L.RH + 2 * L.NS + L.Q;
@@ -204,15 +210,17 @@ struct Soc {
     }
 };
 
-template <int NX, int NU>
+template <int NX, int NU, int NE>
 __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restrict__ ws_all, const double* __restrict__ disc_all) {
     // workspace and disc come in as kernel pointer arguments (known global address space): read out
     // of the by-value struct they would be FLAT accesses, which also count against lgkmcnt, so every
     // LDS wait would drain the outstanding global loads
-    constexpr int NXA = NX + SCP_NG, NUA = NU + NX, NZ = NXA + NUA, RS = NZ + 1;
-    constexpr int SIG = NX, TX = NX + 1, TU = NX + 2, TN = NX + 3, ZU = NX + SCP_NG, ZN = ZU + NU;
+    constexpr int NXA = NX + SCP_NG + NE, NUA = NU + NX, NZ = NXA + NUA, RS = NZ + 1;
+    constexpr int SIG = NX, TX = NX + 1, TU = NX + 2, TN = NX + 3, E0 = NX + SCP_NG, ZU = NXA, ZN = ZU + NU;
+    // game terms (NE > 0): E0..E0+NU-1 = u~, E0+NU = th~ (when T.theta_idx >= 0)
     constexpr int QM = NU + 1;
     const scvx_scp_template& T = a.T;
+    const bool sfix = NE > 0 && T.sigma_fixed != 0;
     const int K = T.K, lane = threadIdx.x, pd = T.pos_dim;
     const long long agent = blockIdx.x;
     const SCPLay Ly = scp_layout(T);
@@ -299,6 +307,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
                 av[SIG] -= sv;
                 h -= hz;
             }
+            if (sfix) { h -= av[SIG] * sref; av[SIG] = 0.0; }  // sigma == sigma_ref is data
             // FOH transform: a_u += C_{t-1}' a_x
             #pragma unroll
             for (int j = 0; j < NU; ++j) {
@@ -353,10 +362,22 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             clr(); av[i] = 1.0; put(r++, av, T.xb_hi[b]);
             clr(); av[i] = -1.0; put(r++, av, -T.xb_lo[b]);
         }
+        if (NE > 0)  // slab rows -z'p_k <= -r - z'P_k (game_model.py:121-124)
+            for (int j = 0; j < T.n_slab; ++j) {
+                clr();
+                const long long base = ((agent * T.n_slab + j) * K + t) * pd;
+                double h = -T.r_slab;
+                for (int i = 0; i < pd; ++i) { av[i] = -a.slab_z[base + i]; h -= a.slab_z[base + i] * a.slab_P[base + i]; }
+                put(r++, av, h);
+            }
         if (t == 0) {
-            clr(); av[SIG] = -1.0; put(r++, av, 0.0);
-            clr(); av[SIG] = 1.0; av[TX] = 1.0; av[TU] = 1.0; put(r++, av, trv + sref);
-            clr(); av[SIG] = -1.0; av[TX] = 1.0; av[TU] = 1.0; put(r++, av, trv - sref);
+            if (sfix) {  // |sigma - sigma_ref| = 0: tau_x + tau_u <= tr
+                clr(); av[TX] = 1.0; av[TU] = 1.0; put(r++, av, trv);
+            } else {
+                clr(); av[SIG] = -1.0; put(r++, av, 0.0);
+                clr(); av[SIG] = 1.0; av[TX] = 1.0; av[TU] = 1.0; put(r++, av, trv + sref);
+                clr(); av[SIG] = -1.0; av[TX] = 1.0; av[TU] = 1.0; put(r++, av, trv - sref);
+            }
         }
         B[Ly.o_nh] = (double)r;
         degl += r + 2 * NS + (Q > 0 ? 1 : 0);
@@ -389,7 +410,10 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
         double qv[NZ];
         #pragma unroll
         for (int i = 0; i < NZ; ++i) qv[i] = 0.0;
-        if (t == 0) { qv[SIG] = T.w_sigma * ics; qv[TN] = T.w_nu * ics; }
+        if (t == 0) { qv[SIG] = sfix ? 0.0 : T.w_sigma * ics; qv[TN] = T.w_nu * ics; }
+        if (NE > 0 && T.w_in > 0.0)  // inertia: w_in ||x_t - xprev_t||^2 -> q_x = -2 w_in xprev_t
+            #pragma unroll
+            for (int i = 0; i < NX; ++i) qv[i] -= 2.0 * T.w_in * ics * a.X_prev[(agent * K + t) * NX + i];
         double pv = 0.0;
         for (int j = 0; j < T.n_nbr; ++j) {
             const long long base = ((agent * T.n_nbr + j) * K + t) * pd;
@@ -418,6 +442,52 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
                 }
                 B[Ly.o_P + i * NZ + j] = v;
             }
+        if (NE > 0) {
+            // game_model.py:87-100 in z coordinates (x_t = xi_t + C_{t-1} u_t), each term / cs
+            auto padd = [&](int i, int j, double v) { B[Ly.o_P + i * NZ + j] += v; };
+            const double cu = 2.0 * T.w_u2 * ics, cr = 2.0 * T.w_du * ics, cth = 2.0 * T.w_dth * ics,
+                         ci = 2.0 * T.w_in * ics;
+            #pragma unroll
+            for (int j = 0; j < NU; ++j) padd(ZU + j, ZU + j, cu);
+            if (t > 0) {
+                #pragma unroll
+                for (int j = 0; j < NU; ++j) {  // (u_t - u~_t)^2
+                    padd(ZU + j, ZU + j, cr); padd(E0 + j, E0 + j, cr);
+                    padd(ZU + j, E0 + j, -cr); padd(E0 + j, ZU + j, -cr);
+                }
+                if (NE > NU && T.theta_idx >= 0) {  // (th_t - th~_t)^2, th_t = xi[th] + C[th,:] u_t
+                    const int th = T.theta_idx;
+                    double c[NZ];
+                    #pragma unroll
+                    for (int i = 0; i < NZ; ++i) c[i] = 0.0;
+                    c[th] = 1.0;
+                    c[E0 + NU] = -1.0;
+                    #pragma unroll
+                    for (int j = 0; j < NU; ++j) c[ZU + j] = Cp[th * NU + j];
+                    #pragma unroll
+                    for (int i = 0; i < NZ; ++i)
+                        #pragma unroll
+                        for (int j = 0; j < NZ; ++j)
+                            if (c[i] != 0.0 && c[j] != 0.0) padd(i, j, cth * c[i] * c[j]);
+                }
+            }
+            if (T.w_in > 0.0)  // ||x_t - xprev_t||^2: T'T with T = [I 0 0 C 0]
+                #pragma unroll
+                for (int i = 0; i < NZ; ++i)
+                    #pragma unroll
+                    for (int j = 0; j < NZ; ++j) {
+                        const bool xi = i < NX, xj = j < NX, ui = i >= ZU && i < ZN, uj = j >= ZU && j < ZN;
+                        if (!((xi || ui) && (xj || uj))) continue;
+                        double v = 0.0;
+                        for (int l = 0; l < NX; ++l) {
+                            const double ti = xi ? (i == l ? 1.0 : 0.0) : Cp[l * NU + (i - ZU)];
+                            const double tj = xj ? (j == l ? 1.0 : 0.0) : Cp[l * NU + (j - ZU)];
+                            v += ti * tj;
+                        }
+                        padd(i, j, ci * v);
+                    }
+            if (sfix && t == 0) padd(SIG, SIG, 1.0);  // sigma is data: a decoupled z_sigma -> 0
+        }
         // dynamics to node t+1 (Riccati coordinates)
         if (t < K - 1) {
             double* At = B + Ly.o_At;
@@ -444,6 +514,18 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
                     }
                     Bt[i * NUA + NU + i] = 1.0;
                     ct[i] = dk[NX * NX + 2 * NX * NU + NX + i];
+                    if (sfix) { ct[i] += At[i * NXA + SIG] * sref; At[i * NXA + SIG] = 0.0; }
+                }
+            }
+            if (NE > 0) {  // u~_{t+1} = u_t; th~_{t+1} = th_t = xi_t[th] + C_{t-1}[th,:] u_t
+                #pragma unroll
+                for (int j = 0; j < NU; ++j) { Bt[(E0 + j) * NUA + j] = 1.0; ct[E0 + j] = 0.0; }
+                if (NE > NU) {
+                    const int th = T.theta_idx;
+                    At[(E0 + NU) * NXA + th] = 1.0;
+                    #pragma unroll
+                    for (int j = 0; j < NU; ++j) Bt[(E0 + NU) * NUA + j] = Cp[th * NU + j];
+                    ct[E0 + NU] = 0.0;
                 }
             }
             #pragma unroll
@@ -672,6 +754,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
                 if (lane == i) sXi[0][lane] = dx[i];
             for (int i = 0; i < SCP_NG; ++i)
                 if (lane == NX + i) sXi[0][lane] = g[i];
+            if (lane >= E0 && lane < NXA) sXi[0][lane] = 0.0;  // u~_0, th~_0: no predecessor, no cost
             __syncthreads();
             if (lane < NX) {
                 double v = B0[Ly.o_pv + lane];
@@ -848,6 +931,9 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
     // ------------------------------------------------------------------ IPM iterations
     int status = 1, it = 0;
     bool near_ok = false;
+    // primal regularisation of the iteration's Newton systems: raised x100 to retry an iteration whose
+    // direction broke down (Riccati overflow in the end-game), relaxed x0.01 after every taken step
+    double regv = T.reg;
 #ifdef SCP_TRACE
     long long tr_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     long long tr_last = __builtin_amdgcn_s_memtime();
@@ -958,6 +1044,11 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
         near_ok = pres < fmax(1e-4, T.tol) * pscale && dres < fmax(1e-4, T.tol) * dscale &&
                   gap < fmax(5e-5, T.tol) * fmax(1.0, fabs(pobj));  // ECOS reduced tolerances
         const double mu = gap / deg;
+#ifdef SCP_DEBUG
+        if (agent == 0 && lane == 0)
+            printf("SCP_DEBUG it=%d pres=%.3e/%.3e dres=%.3e/%.3e gap=%.3e pobj=%.9e near=%d\n", it, pres, pscale, dres,
+                   dscale, gap, pobj, (int)near_ok);
+#endif
         if (lane < NX) sMisc[lane] = nb(0)[Ly.o_z + lane] - xinit[lane];  // r_init
         // ---- scaling and node Hessians
         for (int t = lane; t < K; t += WAVE) {
@@ -1029,7 +1120,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
                 }
             }
             #pragma unroll
-            for (int i = 0; i < NZ; ++i) Hu[i * NZ + i] += T.reg;
+            for (int i = 0; i < NZ; ++i) Hu[i * NZ + i] += regv;
             #pragma unroll
             for (int e = 0; e < NZ * NZ; ++e) B[Ly.o_H + e] = Hu[e / NZ <= e % NZ ? e : (e % NZ) * NZ + e / NZ];  // upper triangle, mirrored
         }
@@ -1204,12 +1295,24 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             if (t < K - 1)
                 #pragma unroll
                 for (int i = 0; i < NXA; ++i) acc += B[Ly.o_yp + i];
-            if (!(fabs(acc) < INFINITY)) badl = 1.0;
+            if (!(fabs(acc) < INFINITY)) {
+                badl = 1.0;
+#ifdef SCP_DEBUG
+                if (agent == 0) printf("SCP_DEBUG breakdown at node %d (it=%d al=%.3e)\n", t, it, al);
+#endif
+            }
         }
         #pragma unroll
         for (int i = 0; i < NX; ++i)
             if (!(fabs(sMisc[8 + i]) < INFINITY)) badl = 1.0;
-        if (wave_max(badl) > 0.0) { status = near_ok ? 1 : 2; break; }
+#ifdef SCP_DEBUG
+        if (agent == 0 && lane == 0) printf("SCP_DEBUG aa=%.3e sigma=%.3e al=%.3e\n", aa, sg, al);
+#endif
+        if (wave_max(badl) > 0.0) {
+            if (regv < 1e-5) { regv *= 100.0; __syncthreads(); continue; }   // retry, stiffer
+            status = near_ok ? 1 : 2;
+            break;
+        }
         // ---- update
         for (int t = lane; t < K; t += WAVE) {
             double* B = nb(t);
@@ -1228,6 +1331,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
         }
         #pragma unroll
         for (int i = 0; i < NX; ++i) y0[i] += al * (sMisc[8 + i] - y0[i]);
+        regv = fmax(T.reg, 0.01 * regv);
         __syncthreads();
         SCP_TR(6)
     }
@@ -1239,7 +1343,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
 
     if (status == 1 && it == T.max_iter && !near_ok) status = 2;   // cap reached far from optimal
     // ------------------------------------------------------------------ outputs
-    double sigv = nb(0)[Ly.o_z + SIG];
+    double sigv = sfix ? sref : nb(0)[Ly.o_z + SIG];
     double numaxl = 0.0, softl = 0.0, admml = 0.0;
     for (int t = lane; t < K; t += WAVE) {
         double* B = nb(t);
@@ -1302,10 +1406,34 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
         }
         numaxl = fmax(numaxl, s1);
     }
-    const double numax = wave_max(numaxl), soft = wave_sum(softl), admm = wave_sum(admml);
+    double gamel = 0.0;
+    if (NE > 0) {  // the game cost at the solution (game_model.py:87-100)
+        __syncthreads();
+        for (int t = lane; t < K; t += WAVE) {
+            const double* x = a.X + (agent * K + t) * NX;
+            const double* u = a.U + (agent * K + t) * NU;
+            #pragma unroll
+            for (int j = 0; j < NU; ++j) gamel += T.w_u2 * u[j] * u[j];
+            if (T.w_in > 0.0)
+                #pragma unroll
+                for (int i = 0; i < NX; ++i) {
+                    const double d = x[i] - a.X_prev[(agent * K + t) * NX + i];
+                    gamel += T.w_in * d * d;
+                }
+            if (t > 0) {
+                #pragma unroll
+                for (int j = 0; j < NU; ++j) { const double d = u[j] - u[j - NU]; gamel += T.w_du * d * d; }
+                if (T.theta_idx >= 0) {
+                    const double d = x[T.theta_idx] - x[T.theta_idx - NX];
+                    gamel += T.w_dth * d * d;
+                }
+            }
+        }
+    }
+    const double numax = wave_max(numaxl), soft = wave_sum(softl), admm = wave_sum(admml), game = wave_sum(gamel);
     if (lane == 0) {
         a.sigma[agent] = sigv;
-        a.obj[agent] = T.w_nu * numax + soft + T.w_sigma * sigv + admm;
+        a.obj[agent] = T.w_nu * numax + soft + T.w_sigma * sigv + admm + game;
         a.status[agent] = status;
         a.iters[agent] = it;
     }
@@ -1322,12 +1450,12 @@ extern "C" size_t scvx_scp_workspace_bytes(const scvx_scp_template* T, int N) {
     return sizeof(double) * (size_t)N * (size_t)L.stride * (size_t)T->K;
 }
 
-extern "C" int scvx_scp_solve_batched(const scvx_scp_template* T, int N, const double* disc, const double* Xref,
-                                      const double* Uref, const double* sigma_ref, const double* tr,
-                                      const double* x_init, const double* x_final, const double* nbr_pos,
-                                      const double* nbr_Y, const double* nbr_Lam, double* X, double* U, double* nu,
-                                      double* sigma, double* s_obs, double* s_nbr, double* obj, int32_t* status,
-                                      int32_t* iters, void* workspace, size_t workspace_bytes, void* stream) {
+static int scp_launch(const scvx_scp_template* T, int N, const double* disc, const double* Xref, const double* Uref,
+                      const double* sigma_ref, const double* tr, const double* x_init, const double* x_final,
+                      const double* nbr_pos, const double* nbr_Y, const double* nbr_Lam, const double* X_prev,
+                      const double* slab_z, const double* slab_P, double* X, double* U, double* nu, double* sigma,
+                      double* s_obs, double* s_nbr, double* obj, int32_t* status, int32_t* iters, void* workspace,
+                      size_t workspace_bytes, void* stream) {
     if (!T || N < 0) return set_error(SCVX_EINVAL, "scp: null template");
     if (N == 0) return SCVX_OK;
     if (T->K < 3 || T->K > SCP_KMAX) return set_error(SCVX_EUNSUPPORTED, "scp: K must be in [3, 256]");
@@ -1344,6 +1472,15 @@ extern "C" int scvx_scp_solve_batched(const scvx_scp_template* T, int N, const d
     if (!disc || !Xref || !Uref || !sigma_ref || !tr || !x_init || !x_final || !X || !U || !nu || !sigma || !obj ||
         !status || !iters || (T->n_obs && !s_obs) || (T->n_nbr && (!nbr_pos || !nbr_Y || !nbr_Lam || !s_nbr)))
         return set_error(SCVX_EINVAL, "scp: null buffer");
+    if (T->game) {
+        if (T->n_nbr != 0) return set_error(SCVX_EUNSUPPORTED, "scp game: no ADMM terms (n_nbr must be 0)");
+        if (T->n_slab < 0 || T->n_slab > SCVX_MAX_NBR) return set_error(SCVX_EINVAL, "scp game: n_slab");
+        if (T->theta_idx >= T->n_x) return set_error(SCVX_EINVAL, "scp game: theta_idx");
+        if (!(T->w_u2 >= 0.0) || !(T->w_du >= 0.0) || !(T->w_dth >= 0.0) || !(T->w_in >= 0.0))
+            return set_error(SCVX_EINVAL, "scp game: negative weight");
+        if ((T->w_in > 0.0 && !X_prev) || (T->n_slab && (!slab_z || !slab_P)))
+            return set_error(SCVX_EINVAL, "scp game: null buffer");
+    }
     const size_t need = scvx_scp_workspace_bytes(T, N);
     if (!workspace || workspace_bytes < need) return set_error(SCVX_EWORKSPACE, "scp: workspace too small");
     SCPArgs a{};
@@ -1351,18 +1488,88 @@ extern "C" int scvx_scp_solve_batched(const scvx_scp_template* T, int N, const d
     a.N = N;
     a.disc = disc; a.Xref = Xref; a.Uref = Uref; a.sigma_ref = sigma_ref; a.tr = tr; a.x_init = x_init;
     a.x_final = x_final; a.nbr_pos = nbr_pos; a.nbr_Y = nbr_Y; a.nbr_Lam = nbr_Lam;
+    a.X_prev = X_prev; a.slab_z = slab_z; a.slab_P = slab_P;
     a.X = X; a.U = U; a.nu = nu; a.sigma = sigma; a.s_obs = s_obs; a.s_nbr = s_nbr; a.obj = obj;
     a.status = status; a.iters = iters;
     a.ws = (double*)workspace;
     a.ws_agent = (long long)scp_layout(*T).stride * T->K;
     hipStream_t st = (hipStream_t)stream;
+    const int ne = scp_ne(*T);
     if (T->model_id == SCVX_MODEL_UNICYCLE && T->n_x == 3 && T->n_u == 2) {
         if (T->has_soc) return set_error(SCVX_EUNSUPPORTED, "scp: SOC rows need n_u + 1 <= 4");
-        hipLaunchKernelGGL((scp_ipm_kernel<3, 2>), dim3(N), dim3(WAVE), 0, st, a, a.ws, a.disc);
+        if (ne == 0)
+            hipLaunchKernelGGL((scp_ipm_kernel<3, 2, 0>), dim3(N), dim3(WAVE), 0, st, a, a.ws, a.disc);
+        else if (ne == 3)
+            hipLaunchKernelGGL((scp_ipm_kernel<3, 2, 3>), dim3(N), dim3(WAVE), 0, st, a, a.ws, a.disc);
+        else
+            return set_error(SCVX_EUNSUPPORTED, "scp game: unicycle needs theta_idx = 2");
     } else if (T->model_id == SCVX_MODEL_SINGLE_INTEGRATOR && T->n_x == 3 && T->n_u == 3) {
-        hipLaunchKernelGGL((scp_ipm_kernel<3, 3>), dim3(N), dim3(WAVE), 0, st, a, a.ws, a.disc);
+        if (ne == 0)
+            hipLaunchKernelGGL((scp_ipm_kernel<3, 3, 0>), dim3(N), dim3(WAVE), 0, st, a, a.ws, a.disc);
+        else if (ne == 3)
+            hipLaunchKernelGGL((scp_ipm_kernel<3, 3, 3>), dim3(N), dim3(WAVE), 0, st, a, a.ws, a.disc);
+        else
+            return set_error(SCVX_EUNSUPPORTED, "scp game: single integrator has no heading (theta_idx = -1)");
     } else {
         return set_error(SCVX_EUNSUPPORTED, "scp: model (unicycle n=3 m=2, single integrator n=3 m=3)");
     }
     return check_launch("scp_ipm_kernel");
+}
+
+extern "C" int scvx_scp_solve_batched(const scvx_scp_template* T, int N, const double* disc, const double* Xref,
+                                      const double* Uref, const double* sigma_ref, const double* tr,
+                                      const double* x_init, const double* x_final, const double* nbr_pos,
+                                      const double* nbr_Y, const double* nbr_Lam, double* X, double* U, double* nu,
+                                      double* sigma, double* s_obs, double* s_nbr, double* obj, int32_t* status,
+                                      int32_t* iters, void* workspace, size_t workspace_bytes, void* stream) {
+    if (T && T->game) return set_error(SCVX_EINVAL, "scp: game template: use scvx_scp_game_solve_batched");
+    return scp_launch(T, N, disc, Xref, Uref, sigma_ref, tr, x_init, x_final, nbr_pos, nbr_Y, nbr_Lam, nullptr,
+                      nullptr, nullptr, X, U, nu, sigma, s_obs, s_nbr, obj, status, iters, workspace, workspace_bytes,
+                      stream);
+}
+
+extern "C" int scvx_scp_game_solve_batched(const scvx_scp_template* T, int N, const double* disc, const double* Xref,
+                                           const double* Uref, const double* sigma_ref, const double* tr,
+                                           const double* x_init, const double* x_final, const double* X_prev,
+                                           const double* slab_z, const double* slab_P, double* X, double* U,
+                                           double* nu, double* sigma, double* s_obs, double* obj, int32_t* status,
+                                           int32_t* iters, void* workspace, size_t workspace_bytes, void* stream) {
+    if (!T || !T->game) return set_error(SCVX_EINVAL, "scp game: template without game = 1");
+    return scp_launch(T, N, disc, Xref, Uref, sigma_ref, tr, x_init, x_final, nullptr, nullptr, nullptr, X_prev,
+                      slab_z, slab_P, X, U, nu, sigma, s_obs, nullptr, obj, status, iters, workspace, workspace_bytes,
+                      stream);
+}
+
+// ---------------------------------------------------------------------------------------------
+// ACS slab update (game_model.py:54-66): z = d/||d|| (0 when ||d|| < 1e-6), one lane per (agent, j, k)
+namespace scvx {
+namespace {
+__global__ __launch_bounds__(256) void slab_update_kernel(int N, int n_slab, int K, int pd, int n_x,
+                                                          const double* __restrict__ p, const double* __restrict__ P,
+                                                          double* __restrict__ z) {
+    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long total = (long long)N * n_slab * K;
+    if (e >= total) return;
+    const int k = (int)(e % K);
+    const long long a = e / ((long long)n_slab * K);
+    double d[3] = {0.0, 0.0, 0.0}, nn = 0.0;
+    for (int i = 0; i < pd; ++i) {
+        d[i] = p[(a * K + k) * n_x + i] - P[e * pd + i];
+        nn += d[i] * d[i];
+    }
+    nn = sqrt(nn);
+    for (int i = 0; i < pd; ++i) z[e * pd + i] = nn < 1e-6 ? 0.0 : d[i] / nn;
+}
+}  // namespace
+}  // namespace scvx
+
+extern "C" int scvx_slab_update_batched(int N, int n_slab, int K, int pos_dim, int n_x, const double* p,
+                                        const double* P, double* z, void* stream) {
+    if (N < 0 || n_slab < 0 || K < 1 || pos_dim < 1 || pos_dim > 3 || pos_dim > n_x || !p || !P || !z)
+        return set_error(SCVX_EINVAL, "slab_update: bad args");
+    const long long total = (long long)N * n_slab * K;
+    if (total == 0) return SCVX_OK;
+    hipLaunchKernelGGL(slab_update_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       N, n_slab, K, pos_dim, n_x, p, P, z);
+    return check_launch("slab_update_kernel");
 }

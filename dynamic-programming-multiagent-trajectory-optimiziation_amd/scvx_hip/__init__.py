@@ -25,7 +25,7 @@ from ._lib import MODEL_DIMS, MODEL_IDS, STATUS, QPTemplate, SCPTemplate, ScvxEr
 DEFAULT_NSUB = {"di": 1, "si": 1, "unicycle": 16, "quad": 16}
 QUAD_PARAMS = (1.0, 9.81, 0.02, 0.02, 0.04)
 
-__all__ = ["foh_batched", "integrate_nonlinear", "collision_rows", "collision_check", "qp_solve_batched", "QPSpec", "SCPSpec", "SCPSolver",
+__all__ = ["foh_batched", "integrate_nonlinear", "collision_rows", "collision_check", "qp_solve_batched", "QPSpec", "SCPSpec", "SCPSolver", "slab_update",
            "intersample_batched",
            "disc_stride", "unpack_disc", "ScvxError", "MODEL_DIMS", "DEFAULT_NSUB"]
 
@@ -288,6 +288,16 @@ class SCPSpec:
     max_iter: int = 100
     tol: float = 1e-9
     reg: float = 1e-10
+    # Nash best-response terms (scvx_scp_game_solve_batched; game_model.py:68-126)
+    game: bool = False
+    sigma_fixed: bool = False
+    w_u2: float = 0.0
+    w_du: float = 0.0
+    w_dth: float = 0.0
+    theta_idx: int = -1
+    w_in: float = 0.0
+    n_slab: int = 0
+    r_slab: float = 0.0
 
     def to_c(self):
         n, m = MODEL_DIMS[self.model]
@@ -317,6 +327,16 @@ class SCPSpec:
         t.w_nu, t.w_slack, t.w_sigma = float(self.w_nu), float(self.w_slack), float(self.w_sigma)
         t.n_nbr, t.rho, t.d_min, t.w_coll = int(self.n_nbr), float(self.rho), float(self.d_min), float(self.w_coll)
         t.max_iter, t.tol, t.reg = int(self.max_iter), float(self.tol), float(self.reg)
+        if self.game:
+            if self.n_nbr:
+                raise ValueError("game template: no ADMM neighbour terms")
+            if self.n_slab > _lib.SCVX_MAX_NBR:
+                raise ValueError("too many slab neighbours")
+            t.game, t.sigma_fixed = 1, int(self.sigma_fixed)
+            t.w_u2, t.w_du, t.w_dth, t.w_in = float(self.w_u2), float(self.w_du), float(self.w_dth), float(self.w_in)
+            t.theta_idx, t.n_slab, t.r_slab = int(self.theta_idx), int(self.n_slab), float(self.r_slab)
+        else:
+            t.theta_idx = -1
         return t
 
 
@@ -362,6 +382,53 @@ class SCPSolver:
         check(rc, "scvx_scp_solve_batched")
         return dict(X=self.X, U=self.U, nu=self.nu, sigma=self.sigma, s_obs=self.s_obs[:, :len(self.spec.obs)],
                     s_nbr=self.s_nbr[:, :self.spec.n_nbr], obj=self.obj, status=self.status, iters=self.iters)
+
+    def solve_game(self, disc, Xref, Uref, sigma_ref, tr, x_init, x_final, X_prev=None, slab_z=None, slab_P=None,
+                   stream=None):
+        """Nash best responses (scvx_scp_game_solve_batched; spec.game must be set): inputs as solve(),
+        plus X_prev (N,K,n) when spec.w_in > 0 and slab_z / slab_P (N,n_slab,K,pos_dim) when
+        spec.n_slab > 0.  Returns dict of device tensors (reused buffers)."""
+        sp_ = self.spec
+        if not sp_.game:
+            raise ValueError("solve_game needs a game template (SCPSpec.game=True)")
+        N, K, pd = self.N, sp_.K, sp_.pos_dim
+        if sp_.w_in > 0 and (X_prev is None or tuple(X_prev.shape) != tuple(self.X.shape)):
+            raise ValueError(f"X_prev {tuple(self.X.shape)} required (inertia_weight > 0)")
+        if sp_.n_slab > 0:
+            shp = (N, sp_.n_slab, K, pd)
+            if slab_z is None or slab_P is None or tuple(slab_z.shape) != shp or tuple(slab_P.shape) != shp:
+                raise ValueError(f"slab_z / slab_P {shp} required")
+        d = self._dummy
+        rc = lib().scvx_scp_game_solve_batched(
+            ctypes.byref(self.ctpl), N, _dev(disc, name="disc"), _dev(Xref, name="Xref"), _dev(Uref, name="Uref"),
+            _dev(sigma_ref, name="sigma_ref"), _dev(tr, name="tr"), _dev(x_init, name="x_init"),
+            _dev(x_final, name="x_final"), _dev(X_prev if X_prev is not None else d, name="X_prev"),
+            _dev(slab_z if slab_z is not None else d, name="slab_z"),
+            _dev(slab_P if slab_P is not None else d, name="slab_P"), _dev(self.X), _dev(self.U), _dev(self.nu),
+            _dev(self.sigma), _dev(self.s_obs), _dev(self.obj), _dev(self.status, _torch().int32),
+            _dev(self.iters, _torch().int32), _dev(self.workspace), ctypes.c_size_t(self.workspace.numel() * 8),
+            _stream(stream))
+        check(rc, "scvx_scp_game_solve_batched")
+        return dict(X=self.X, U=self.U, nu=self.nu, sigma=self.sigma, s_obs=self.s_obs[:, :len(sp_.obs)],
+                    obj=self.obj, status=self.status, iters=self.iters)
+
+
+def slab_update(p, P, pos_dim, z=None, stream=None):
+    """ACS slab normals for every (agent, neighbour, node) in one launch (scvx_slab_update_batched;
+    GameUnicycleModel.update_slabs, game_model.py:54-66): z = d/||d||, d = p[a,k,:pos_dim] - P[a,j,k],
+    0 where ||d|| < 1e-6.  p (N,K,n) float64, P (N,n_slab,K,pos_dim); returns z like P."""
+    torch = _torch()
+    N, K, n = p.shape
+    if P.dim() != 4 or P.shape[0] != N or P.shape[2] != K or P.shape[3] != pos_dim:
+        raise ValueError(f"slab_update: P (N={N}, n_slab, K={K}, pos_dim={pos_dim}) expected")
+    if z is None:
+        z = torch.empty_like(P)
+    elif tuple(z.shape) != tuple(P.shape):
+        raise ValueError("slab_update: z must have P's shape")
+    rc = lib().scvx_slab_update_batched(N, P.shape[1], K, pos_dim, n, _dev(p, name="p"), _dev(P, name="P"),
+                                        _dev(z, name="z"), _stream(stream))
+    check(rc, "scvx_slab_update_batched")
+    return z
 
 
 def admm_consensus(X_new, nbr, rho, Y, Lam, pos_dim, primal=None, dual=None, stream=None, check_index=True):

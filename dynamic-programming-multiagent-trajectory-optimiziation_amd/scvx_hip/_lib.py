@@ -19,7 +19,8 @@ STATUS = {0: "optimal", 1: "optimal_inaccurate", 2: "solver_error"}
 EXPORTS = ("scvx_version", "scvx_last_error", "scvx_foh_batched", "scvx_integrate_nonlinear_batched",
            "scvx_qp_solve_batched", "scvx_qp_workspace_bytes", "scvx_qp_set_trace",
            "scvx_collision_rows_batched", "scvx_collision_check_batched", "scvx_scp_solve_batched", "scvx_scp_workspace_bytes",
-           "scvx_intersample_batched", "scvx_admm_consensus_batched")
+           "scvx_intersample_batched", "scvx_admm_consensus_batched", "scvx_scp_game_solve_batched",
+           "scvx_slab_update_batched")
 
 
 class ScvxError(RuntimeError):
@@ -56,6 +57,9 @@ class SCPTemplate(ctypes.Structure):
         ("w_nu", ctypes.c_double), ("w_slack", ctypes.c_double), ("w_sigma", ctypes.c_double),
         ("n_nbr", ctypes.c_int32), ("rho", ctypes.c_double), ("d_min", ctypes.c_double), ("w_coll", ctypes.c_double),
         ("max_iter", ctypes.c_int32), ("tol", ctypes.c_double), ("reg", ctypes.c_double),
+        ("game", ctypes.c_int32), ("sigma_fixed", ctypes.c_int32), ("w_u2", ctypes.c_double),
+        ("w_du", ctypes.c_double), ("w_dth", ctypes.c_double), ("theta_idx", ctypes.c_int32),
+        ("w_in", ctypes.c_double), ("n_slab", ctypes.c_int32), ("r_slab", ctypes.c_double),
     ]
 
 
@@ -97,6 +101,8 @@ def lib():
         L.scvx_scp_solve_batched.argtypes = [ctypes.POINTER(SCPTemplate), i32] + [vp] * 19 + [vp, sz, vp]
         L.scvx_intersample_batched.argtypes = [ctypes.POINTER(IntersampleTemplate), vp, i32, i32] + [vp] * 9
         L.scvx_admm_consensus_batched.argtypes = [i32, i32, i32, i32, i32, vp, vp, dbl, vp, vp, vp, vp, vp]
+        L.scvx_scp_game_solve_batched.argtypes = [ctypes.POINTER(SCPTemplate), i32] + [vp] * 18 + [vp, sz, vp]
+        L.scvx_slab_update_batched.argtypes = [i32, i32, i32, i32, i32, vp, vp, vp, vp]
         sized = ("scvx_last_error", "scvx_qp_workspace_bytes", "scvx_scp_workspace_bytes")
         for fn in EXPORTS:
             getattr(L, fn).restype = getattr(L, fn).restype if fn in sized else i32

@@ -212,6 +212,16 @@ typedef struct scvx_scp_template {
     int32_t max_iter;
     double tol;
     double reg;             /* primal regularisation of the Newton systems (scaled units), e.g. 1e-10 */
+    /* Nash best-response terms (scvx_scp_game_solve_batched; zero for SCProblem / AgentSolver) */
+    int32_t game;           /* 1: the terms below are active */
+    int32_t sigma_fixed;    /* sigma == sigma_ref (agent_best_response.py:77) */
+    double w_u2;            /* control_weight       * ||U||_F^2                       (game_model.py:88) */
+    double w_du;            /* control_rate_weight  * sum_k ||u_{k+1} - u_k||^2       (:91-93) */
+    double w_dth;           /* curvature_weight     * sum_k (x_{k+1}[th] - x_k[th])^2 (:94-96) */
+    int32_t theta_idx;      /* state index of th (unicycle 2), -1: no curvature state */
+    double w_in;            /* inertia_weight       * ||X - X_prev||_F^2              (:99-100) */
+    int32_t n_slab;         /* slab rows z_{j,k}'(p_k - P_{j,k}) >= r_slab per node (:121-124), <= SCVX_MAX_NBR */
+    double r_slab;          /* collision_radius */
 } scvx_scp_template;
 
 /*
@@ -228,8 +238,36 @@ int scvx_scp_solve_batched(const scvx_scp_template* tpl, int N, const double* di
                            double* X, double* U, double* nu, double* sigma, double* s_obs, double* s_nbr, double* obj,
                            int32_t* status, int32_t* iters, void* workspace, size_t workspace_bytes, void* stream);
 
-/* Bytes of caller-owned device scratch scvx_scp_solve_batched needs for N agents. */
+/* Bytes of caller-owned device scratch scvx_scp_solve_batched / scvx_scp_game_solve_batched need for
+ * N agents (depends on the game fields: the game kernel carries extra Riccati states). */
 size_t scvx_scp_workspace_bytes(const scvx_scp_template* tpl, int N);
+
+/* ------------------------------------------------------------------------------------------
+ * Batched Nash best response: AgentBestResponse.setup/solve (SCvx/optimization/agent_best_response.py:
+ * 35-113, si_agent_best_response.py:36-127) = the SCProblem above (without ADMM terms) plus the
+ * GameUnicycleModel / GameSIModel cost and slab constraints (game_model.py:68-126,
+ * game_si_model.py:90-136) and sigma == sigma_ref:
+ *
+ *   + w_u2 ||U||_F^2 + w_du sum_k ||u_{k+1} - u_k||^2 + w_dth sum_k (th_{k+1} - th_k)^2
+ *   + w_in ||X - X_prev||_F^2,      s.t.  z_{j,k}'(p_k - P_{j,k}) >= r_slab   (j < n_slab, every k)
+ *
+ * The cross-node terms ride on augmented Riccati states u~_k = u_{k-1}, th~_k = th_{k-1}.
+ * Extra inputs (device): X_prev [N][K][n] (read when w_in > 0), slab_z / slab_P
+ * [N][n_slab][K][pos_dim] (the slab normals z and neighbour positions P).  obj includes the game
+ * cost and w_sigma sigma_ref.  Requires tpl->game = 1 and tpl->n_nbr = 0; models as above.
+ * ------------------------------------------------------------------------------------------ */
+int scvx_scp_game_solve_batched(const scvx_scp_template* tpl, int N, const double* disc, const double* Xref,
+                                const double* Uref, const double* sigma_ref, const double* tr,
+                                const double* x_init, const double* x_final, const double* X_prev,
+                                const double* slab_z, const double* slab_P, double* X, double* U, double* nu,
+                                double* sigma, double* s_obs, double* obj, int32_t* status, int32_t* iters,
+                                void* workspace, size_t workspace_bytes, void* stream);
+
+/* Slab normals of the ACS dual update (GameUnicycleModel.update_slabs, game_model.py:54-66 /
+ * game_si_model.py:69-88): z[a][j][k] = d / ||d|| with d = p[a][k] - P[a][j][k], 0 when ||d|| < 1e-6.
+ * p [N][K][n_x] (positions = the first pos_dim states), P [N][n_slab][K][pos_dim], z likewise. */
+int scvx_slab_update_batched(int N, int n_slab, int K, int pos_dim, int n_x, const double* p, const double* P,
+                             double* z, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Batched inter-sample obstacle clearance: SCvx/utils/intersample_collision.py (make_segment_f

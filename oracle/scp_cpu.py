@@ -255,6 +255,7 @@ class SCPSolver:
 
     def __init__(self, p, tol=1e-9, max_iter=100, reg=1e-10):
         self.p, self.tol, self.max_iter, self.reg = p, tol, max_iter, reg
+        self._regv = reg
         self.nodes, self.L = build_nodes(p)
         self.K = len(self.nodes)
 
@@ -313,6 +314,7 @@ class SCPSolver:
         pscale, dscale = 1.0 + hmax, 1.0 + qmax
         status, it, near_ok = "max_iter", 0, False
         self.trace = []
+        self._regv = self.reg     # kernel: regv (x100 retry after a breakdown, x0.01 after a step)
         for it in range(self.max_iter):
             # residuals
             rd, rsig, rc, rpv = [], [], [], []
@@ -432,6 +434,9 @@ class SCPSolver:
             fin = np.isfinite(alpha) and alpha > 0 and np.isfinite(dz).all() and np.isfinite(yp).all() and \
                 np.isfinite(y0p).all() and all(np.isfinite(x).all() for x in dsg + ds + dl)
             if not fin:
+                if self._regv < 1e-5:
+                    self._regv *= 100.0
+                    continue
                 status = "inaccurate" if near_ok else "numerical"
                 break
             z = z + alpha * dz
@@ -441,6 +446,7 @@ class SCPSolver:
                 lam[k] = lam[k] + alpha * dl[k]
             y = y + alpha * (yp - y)
             y0 = y0 + alpha * (y0p - y0)
+            self._regv = max(self.reg, 0.01 * self._regv)
         else:
             it = self.max_iter
             if not near_ok:
@@ -456,7 +462,7 @@ class SCPSolver:
         Ps, ps, Ks, ks = [None] * K, [None] * K, [None] * K, [None] * K
         Hm = []
         for k, nd in enumerate(nodes):
-            H = Hs[k] + self.reg * np.eye(L.nz); f = fs[k].copy()
+            H = Hs[k] + self._regv * np.eye(L.nz); f = fs[k].copy()
             pin = nd["pin"]
             H[pin, :] = 0.0; H[:, pin] = 0.0
             H[pin, pin] = 1.0

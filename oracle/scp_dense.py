@@ -124,16 +124,23 @@ def _nt_scaling(dims, s, z):
     return sp.block_diag(Wb, format="csr"), sp.block_diag(Wib, format="csr")
 
 
-def solve_conic_qp_sparse(P, q, A, b, G, h, dims, tol=1e-10, maxit=100):
-    """Returns dict(x, y, s, z, status, iters).  P, A, G scipy sparse."""
+def solve_conic_qp_sparse(P, q, A, b, G, h, dims, tol=1e-10, maxit=100, osc=1.0, trace=None):
+    """Returns dict(x, y, s, z, status, iters).  P, A, G scipy sparse.  osc: objective scale (the
+    iteration runs on (P, q)/osc, the duals are returned in the caller's units; the gap test stays
+    relative to the unscaled objective)."""
+    P, q = P / osc, q / osc
     n, p, m = len(q), len(b), len(h)
     e = _unit(dims, m)
     deg = dims["l"] + len(dims["q"])
     P, A, G = sp.csr_matrix(P), sp.csr_matrix(A), sp.csr_matrix(G)
 
     def factor(Wi2):
-        Kmat = sp.bmat([[P + G.T @ Wi2 @ G, A.T], [A, None]], format="csc")
-        return spla.splu(Kmat)
+        H = P + G.T @ Wi2 @ G
+        try:
+            return spla.splu(sp.bmat([[H, A.T], [A, None]], format="csc"))
+        except RuntimeError:     # exactly singular (a pivot underflowed): static regularisation; the
+            d = 1e-11 * max(1.0, abs(H).max())  # residuals stay exact, later iterations absorb it
+            return spla.splu(sp.bmat([[H + d * sp.identity(n), A.T], [A, -d * sp.identity(p)]], format="csc"))
 
     def ksolve(lu, rx, ry):
         sol = lu.solve(np.concatenate([rx, ry]))
@@ -146,6 +153,7 @@ def solve_conic_qp_sparse(P, q, A, b, G, h, dims, tol=1e-10, maxit=100):
     s = s + max(0.0, 1.0 - _min_eig(dims, s)) * e
     z = z + max(0.0, 1.0 - _min_eig(dims, z)) * e
     status, it = "max_iter", 0
+    best = (np.inf, 0, x, y, s, z)
     pscale = 1.0 + max(np.abs(h).max(initial=0), np.abs(b).max(initial=0))
     dscale = 1.0 + np.abs(q).max(initial=0)
     for it in range(maxit):
@@ -155,32 +163,50 @@ def solve_conic_qp_sparse(P, q, A, b, G, h, dims, tol=1e-10, maxit=100):
         mu = (s @ z) / deg
         pobj = 0.5 * x @ (P @ x) + q @ x
         pres = max(np.abs(rp).max(initial=0), np.abs(rc).max(initial=0))
-        if pres < tol * pscale and np.abs(rd).max() < tol * dscale and s @ z < tol * max(1.0, abs(pobj)):
+        if trace is not None:
+            trace.append((pres / pscale, np.abs(rd).max() / dscale, s @ z, pobj * osc))
+        if pres < tol * pscale and np.abs(rd).max() < tol * dscale and s @ z < tol * max(1.0 / osc, abs(pobj)):
             status = "optimal"
             break
-        W, Wi = _nt_scaling(dims, s, z)
-        Wi2 = Wi @ Wi
-        lam = W @ z
-        lu = factor(Wi2)
+        # ECOS-style reduced accuracy: keep the best iterate by max(scaled residuals, relative gap);
+        # when 15 iterations bring no improvement (a conditioning floor), or at the cap, the best
+        # iterate within 1e-8 feasibility and 1e-6 relative gap is returned as "optimal_inaccurate"
+        merit = max(pres / pscale, np.abs(rd).max() / dscale, (s @ z) / max(1.0 / osc, abs(pobj)))
+        if merit < best[0]:
+            best = (merit, it, x.copy(), y.copy(), s.copy(), z.copy())
+        if it - best[1] > 15:
+            break
+        try:
+            W, Wi = _nt_scaling(dims, s, z)
+            Wi2 = Wi @ Wi
+            lam = W @ z
+            lu = factor(Wi2)
 
-        def direction(rcomp):
-            rho = _jdiv(dims, lam, rcomp)
-            t = Wi @ rho + Wi2 @ rc
-            dx, dy = ksolve(lu, -rd - G.T @ t, -rp)
-            dz = Wi @ rho + Wi2 @ (rc + G @ dx)
-            ds = -rc - G @ dx
-            return dx, dy, ds, dz
+            def direction(rcomp):
+                rho = _jdiv(dims, lam, rcomp)
+                t = Wi @ rho + Wi2 @ rc
+                dx, dy = ksolve(lu, -rd - G.T @ t, -rp)
+                dz = Wi @ rho + Wi2 @ (rc + G @ dx)
+                ds = -rc - G @ dx
+                return dx, dy, ds, dz
 
-        lam2 = _jprod(dims, lam, lam)
-        dxa, dya, dsa, dza = direction(-lam2)
-        alpha = min(1.0, _max_step(dims, s, dsa), _max_step(dims, z, dza))
-        mu_a = ((s + alpha * dsa) @ (z + alpha * dza)) / deg
-        sig = (mu_a / mu) ** 3
-        corr = _jprod(dims, Wi @ dsa, W @ dza)
-        dx, dy, ds, dz = direction(-lam2 - corr + sig * mu * e)
-        alpha = min(1.0, 0.99 * min(_max_step(dims, s, ds), _max_step(dims, z, dz)))
+            lam2 = _jprod(dims, lam, lam)
+            dxa, dya, dsa, dza = direction(-lam2)
+            alpha = min(1.0, _max_step(dims, s, dsa), _max_step(dims, z, dza))
+            mu_a = ((s + alpha * dsa) @ (z + alpha * dza)) / deg
+            sig = (mu_a / mu) ** 3
+            corr = _jprod(dims, Wi @ dsa, W @ dza)
+            dx, dy, ds, dz = direction(-lam2 - corr + sig * mu * e)
+            alpha = min(1.0, 0.99 * min(_max_step(dims, s, ds), _max_step(dims, z, dz)))
+            if not (np.isfinite(alpha) and np.all(np.isfinite(dx)) and np.all(np.isfinite(dz))):
+                raise FloatingPointError("non-finite direction")
+        except (RuntimeError, FloatingPointError):   # boundary round-off (SOC J < 0) or a singular
+            break                                     # factor: the best iterate is returned below
         x, y, s, z = x + alpha * dx, y + alpha * dy, s + alpha * ds, z + alpha * dz
-    return dict(x=x, y=y, s=s, z=z, status=status, iters=it)
+    if status != "optimal" and best[0] < 1e-6:
+        # (merit mixes scaled residuals and the relative gap: 1e-6 bounds all three)
+        status, (x, y, s, z) = "optimal_inaccurate", best[2:]
+    return dict(x=x, y=y * osc, s=s, z=z * osc, status=status, iters=it)
 
 
 def kkt_certificate(P, q, A, b, G, h, dims, sol):
@@ -214,6 +240,9 @@ def build_scproblem(prob):
       x_bounds: [(i, lo, hi)]                          position box with robot radius (:98-101 / :107-110)
       obs: [(center, r_total)], pos_dim               linearized obstacles with slack s_prime (:103-114)
       nbrs: [dict(Pref (K,pd), Y (K,pd), Lam (K,pd))], rho, d_min    AgentSolver terms (agent_solver.py:78-95)
+      game: dict(w_u2, w_du, w_dth, theta_idx, w_in, X_prev (K,n), slabs [(z (K,pd), P (K,pd))], r_slab)
+            Nash best response (agent_best_response.py:46-81 with game_model.py:84-124): the cost
+            terms, the slab rows z_k'(p_k - P_k) >= r_slab and sigma == sigma_ref
     Returns (P, q, A, b, G, h, dims, idx).
     """
     A_, B_, C_, S_, z_ = prob["A"], prob["B"], prob["C"], prob["S"], prob["z"]
@@ -267,6 +296,9 @@ def build_scproblem(prob):
     for j in range(m):
         eq([(U(0, j), 1.0)], 0.0)
         eq([(U(K - 1, j), 1.0)], 0.0)
+    game = prob.get("game")
+    if game is not None:
+        eq([(SG, 1.0)], prob["sigma_ref"])                      # agent_best_response.py:77
     # dynamics X_{k+1} = A X_k + B U_k + C U_{k+1} + S sigma + z + nu   (sc_problem.py:53-68)
     for k in range(K - 1):
         for i in range(n):
@@ -286,6 +318,8 @@ def build_scproblem(prob):
 
     for (j, lo, hi) in prob.get("u_bounds") or []:
         for k in range(K):
+            if k in (0, K - 1) and (lo is None or lo <= 0.0) and (hi is None or hi >= 0.0):
+                continue        # U[:,0] = U[:,-1] = 0 satisfies the bound: a row without interior
             if hi is not None:
                 le([(U(k, j), 1.0)], hi)
             if lo is not None:
@@ -309,6 +343,11 @@ def build_scproblem(prob):
             le([(X(k, i), -a[k, i]) for i in range(pd)] + [(SC(jn, k), -1.0)],
                -prob["d_min"] - a[k] @ nb["Y"][k])
             le([(SC(jn, k), -1.0)], 0.0)
+    if game is not None:
+        for (zs, Ps) in game["slabs"]:
+            for k in range(K):
+                # z_k'(p_k - P_k) >= r   (game_model.py:121-124)
+                le([(X(k, i), -zs[k, i]) for i in range(pd)], -game["r_slab"] - zs[k] @ Ps[k])
     # trust region  norm(dx,1) + norm(du,1) + |ds| <= tr   (induced norms, sc_problem.py:71-74)
     for k in range(K):
         for i in range(n):
@@ -360,8 +399,26 @@ def build_scproblem(prob):
                 q[X(k, i)] += nb["Lam"][k, i] - rho * nb["Y"][k, i]
                 Pd[X(k, i)] += rho
             q[SC(jn, k)] = WEIGHT_COLLISION_SLACK
-    P = sp.diags(Pd, format="csr")
+    Pr, Pc, Pv = list(range(nv)), list(range(nv)), list(Pd)
     const = sum(float(np.sum(-nb["Lam"] * nb["Y"]) + 0.5 * rho * np.sum(nb["Y"] ** 2)) for nb in nbrs)
+    if game is not None:
+        def sq(a, b, w):        # w (z_a - z_b)^2
+            Pr.extend([a, b, a, b]), Pc.extend([a, b, b, a]), Pv.extend([2 * w, 2 * w, -2 * w, -2 * w])
+        for k in range(K):
+            for j in range(m):
+                Pr.append(U(k, j)), Pc.append(U(k, j)), Pv.append(2 * game["w_u2"])     # game_model.py:88
+                if k < K - 1 and game["w_du"] > 0:
+                    sq(U(k + 1, j), U(k, j), game["w_du"])                                # :91-93
+            if k < K - 1 and game["w_dth"] > 0 and game["theta_idx"] is not None:
+                th = game["theta_idx"]
+                sq(X(k + 1, th), X(k, th), game["w_dth"])                                 # :94-96
+            if game["w_in"] > 0:                                                          # :99-100
+                for i in range(n):
+                    Pr.append(X(k, i)), Pc.append(X(k, i)), Pv.append(2 * game["w_in"])
+                    q[X(k, i)] -= 2 * game["w_in"] * game["X_prev"][k, i]
+        if game["w_in"] > 0:
+            const += game["w_in"] * float(np.sum(game["X_prev"] ** 2))
+    P = sp.csr_matrix((Pv, (Pr, Pc)), shape=(nv, nv))
     idx["const"] = const
     return P, q, Aeq, np.array(beq), G, h, dict(l=nl, q=qd), idx
 
@@ -369,7 +426,8 @@ def build_scproblem(prob):
 def solve_scproblem(prob, tol=1e-10, maxit=100):
     """Returns dict(X (K,n), U (K,m), nu (K-1,n), sigma, s_prime (nobs,K), S (nnb,K), obj, status, cert)."""
     P, q, A, b, G, h, dims, idx = build_scproblem(prob)
-    sol = solve_conic_qp_sparse(P, q, A, b, G, h, dims, tol=tol, maxit=maxit)
+    osc = max(1.0, np.abs(q).max(initial=0.0), abs(P).max() if P.nnz else 0.0)
+    sol = solve_conic_qp_sparse(P, q, A, b, G, h, dims, tol=tol, maxit=maxit, osc=osc)
     x = sol["x"]
     K, n = prob["Xref"].shape
     m = prob["Uref"].shape[1]
@@ -387,6 +445,13 @@ def scp_objective(prob, X, U, nu, sigma, s_prime=None, S=None):
     K = X.shape[0]
     pd = prob.get("pos_dim", 2)
     obj = prob["w_nu"] * np.abs(nu).sum(axis=1).max() + prob["w_sigma"] * sigma
+    game = prob.get("game")
+    if game is not None:
+        obj += game["w_u2"] * np.sum(U ** 2) + game["w_du"] * np.sum(np.diff(U, axis=0) ** 2)
+        if game["theta_idx"] is not None:
+            obj += game["w_dth"] * np.sum(np.diff(X[:, game["theta_idx"]]) ** 2)
+        if game["w_in"] > 0:
+            obj += game["w_in"] * np.sum((X - game["X_prev"]) ** 2)
     for o, (c, r_tot) in enumerate(prob.get("obs") or []):
         a = obstacle_normals(prob["Xref"], c, pd)
         viol = np.maximum(0.0, r_tot - np.einsum("ki,ki->k", a, X[:, :pd] - np.asarray(c, float)[None, :pd]))
@@ -405,6 +470,7 @@ def scp_objective(prob, X, U, nu, sigma, s_prime=None, S=None):
 def scp_violation(prob, X, U, nu, sigma):
     """Max violation of the hard constraints of build_scproblem at (X, U, nu, sigma)."""
     K, n = X.shape
+    pd = prob.get("pos_dim", 2)
     v = [np.abs(X[0] - prob["x_init"]).max(), np.abs(X[-1] - prob["x_final"]).max(),
          np.abs(U[0]).max(), np.abs(U[-1]).max(), max(0.0, -sigma)]
     for k in range(K - 1):
@@ -420,6 +486,11 @@ def scp_violation(prob, X, U, nu, sigma):
         v.append(max(0.0, (X[:, i] - hi).max(), (lo - X[:, i]).max()))
     if prob.get("u_soc") is not None:
         v.append(max(0.0, (np.linalg.norm(U, axis=1) - prob["u_soc"]).max()))
+    game = prob.get("game")
+    if game is not None:
+        v.append(abs(sigma - prob["sigma_ref"]))
+        for (zs, Ps) in game["slabs"]:
+            v.append(max(0.0, (game["r_slab"] - np.einsum("ki,ki->k", zs, X[:, :pd] - Ps)).max()))
     tr_used = np.abs(X - prob["Xref"]).sum(axis=1).max() + np.abs(U - prob["Uref"]).sum(axis=1).max() \
         + abs(sigma - prob["sigma_ref"])
     v.append(max(0.0, tr_used - prob["tr"]))

@@ -1,0 +1,236 @@
+"""GPU parity of the Nash best-response path (scvx_scp_game_solve_batched, scvx_slab_update_batched and
+the NashSolver / AgentBestResponse drop-ins) against oracle/nash_ref.py + oracle/scp_dense.py -- the
+reference's best-response formulation (agent_best_response.py:46-98 with game_model.py:84-124) solved
+by an independent sparse conic IPM.
+
+The unicycle best response is NOT unique in X: sigma is fixed, so the dynamics are met through the
+virtual control nu, whose cost is the induced 1-norm max_k ||nu_k||_1 (sc_problem.py:79) -- every
+column below the maximum is free.  Parity is therefore stated on the optimal VALUE (relative 1e-6:
+the checker's own accuracy floor on these 1e6-weighted problems is ~1e-7), feasibility (1e-7), and U,
+which the control-effort term makes unique (||U - U*||_F^2 <= gap / w_u2 from the measured value gap).
+The NashSolver loop is checked step by step on its own trace: every best response against the oracle
+on the same data, the slab normals against the oracle's update_slabs, the Gauss-Seidel neighbour
+positions and the ACS stopping rule (nash_solver.py:66-143)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+OBS_G = [([1.0, 1.0], 0.25), ([1.0, -0.3], 0.02)]                # SCvx/config/default_game.py:14-17
+GAME = [((0.0, -1.0, 0.0), (2.0, 3.0, 0.0)), ((2.0, -1.0, 0.0), (0.0, 3.0, 0.0)), ((1.0, -1.5, 0.0), (1.0, 3.0, 0.0))]
+WTS = dict(control_weight=5.0, control_rate_weight=5.0, curvature_weight=100.0)   # :21-26
+SI_OBS = [([0.0, 0.0, 0.0], 0.8)]                                   # SCvx/config/SI_default_game.py:16-18
+SI_GAME = [((-4.0, 0.0, 0.0), (4.0, 0.0, 0.0)), ((0.0, -4.0, 0.0), (0.0, 4.0, 0.0)), ((0.0, 0.0, -4.0), (0.0, 0.0, 4.0))]
+SI_WTS = dict(control_weight=5.0, control_rate_weight=5.0)
+
+
+def _mam():
+    from SCvx.models.game_model import GameUnicycleModel
+    from SCvx.models.multi_agent_model import MultiAgentModel
+    params = [dict(r_init=np.array(a), r_final=np.array(b), obstacles=OBS_G) for a, b in GAME]
+    mam = MultiAgentModel(params)
+    for i, p in enumerate(params):     # SCvx/examples/compare_admm_vs_nash.py:84-95
+        mam.models[i] = GameUnicycleModel(r_init=p["r_init"], r_final=p["r_final"], obstacles=OBS_G,
+                                          control_weight=5.0, collision_weight=10.0, collision_radius=0.5,
+                                          control_rate_weight=5.0, curvature_weight=100.0)
+    return mam
+
+
+def _warm(K, game=GAME, obs=OBS_G):
+    from SCvx.utils.initial_guess import initial_guess
+    return zip(*(initial_guess(np.array(a), np.array(b), obs, 0.05, K) for a, b in game))
+
+
+def _disc_stacks(disc, n, m):
+    K1 = disc.shape[0]
+    o = np.cumsum([0, n * n, n * m, n * m, n, n])
+    return (disc[:, o[0]:o[1]].reshape(K1, n, n).transpose(0, 2, 1), disc[:, o[1]:o[2]].reshape(K1, m, n).transpose(0, 2, 1),
+            disc[:, o[2]:o[3]].reshape(K1, m, n).transpose(0, 2, 1), disc[:, o[3]:o[4]].copy(), disc[:, o[4]:o[5]].copy())
+
+
+def _check_against_oracle(p, X, U, nu, sigma, obj_kernel, w_u2):
+    """X (K,n) etc. node-major; returns the oracle solution."""
+    from oracle import nash_ref, scp_dense as sd
+    ref = nash_ref.best_response(p)
+    assert ref["status"] in ("optimal", "optimal_inaccurate"), ref["status"]
+    obj = sd.scp_objective(p, X, U, nu, sigma)
+    assert abs(obj - ref["obj"]) <= 1e-6 * abs(ref["obj"]), (obj, ref["obj"])
+    assert abs(obj_kernel - obj) <= 1e-7 * abs(obj), (obj_kernel, obj)        # kernel-reported objective
+    assert sd.scp_violation(p, X, U, nu, sigma) < 1e-7
+    gap = abs(obj - ref["obj"]) + 1e-7 * abs(ref["obj"])
+    assert np.linalg.norm(U - ref["U"]) <= np.sqrt(gap / w_u2) + 1e-6
+    return ref
+
+
+def test_slab_update_matches_reference_normals(cuda):
+    import torch
+    import scvx_hip
+    from oracle import nash_ref
+    rng = np.random.default_rng(0)
+    N, J, K, n = 4, 3, 37, 3
+    for pd in (2, 3):
+        p = rng.standard_normal((N, K, n))
+        P = rng.standard_normal((N, J, K, pd))
+        P[1, 2, 5] = p[1, 5, :pd]                    # coincident -> z = 0 (game_model.py:64)
+        P[2, 0, 7] = p[2, 7, :pd] + 1e-8             # |d| < 1e-6 -> z = 0
+        z = scvx_hip.slab_update(torch.tensor(p, device=cuda), torch.tensor(P, device=cuda), pd).cpu().numpy()
+        for a in range(N):
+            for j in range(J):
+                np.testing.assert_allclose(z[a, j], nash_ref.slab_normals(p[a, :, :pd], P[a, j]), rtol=0, atol=1e-15)
+        assert not z[1, 2, 5].any() and not z[2, 0, 7].any()
+
+
+@pytest.mark.parametrize("agent", [0, 1, 2])
+def test_best_response_matches_reference_formulation(cuda, agent):
+    from oracle import nash_ref, scp_problems as sp_
+    from SCvx.global_parameters import K
+    from SCvx.optimization.agent_best_response import AgentBestResponse
+    mam = _mam()
+    X0, U0 = _warm(K)
+    br = AgentBestResponse(agent, mam)
+    mats = [a.copy() for a in br.foh.calculate_discretization(X0[agent], U0[agent], 1.0)]
+    refs = {j: X0[j] for j in range(3) if j != agent}
+    br.setup(X0[agent], U0[agent], 1.0, mats, refs, X0[agent], refs)
+    X, U, nu, slack, p_i = br.solve()
+    assert X.shape == (3, K) and U.shape == (2, K) and p_i.shape == (2, K) and slack == 0.0
+    assert br.scp.prob.status in ("optimal", "optimal_inaccurate")
+    assert br.scp.get_variable("sigma") == 1.0
+    n, m = 3, 2
+    disc = np.hstack([a.T for a in mats])
+    cons = sp_.model_constraints("unicycle", GAME[agent][0], GAME[agent][1], obstacles=OBS_G)
+    nbr = [j for j in range(3) if j != agent]
+    slabs = [(nash_ref.slab_normals(X0[agent].T[:, :2], X0[j].T[:, :2]), X0[j].T[:, :2]) for j in nbr]
+    p = nash_ref.game_problem("unicycle", X0[agent].T, U0[agent].T, 1.0, cons, WTS, X0[agent].T, slabs, 0.5,
+                              disc=_disc_stacks(disc, n, m))
+    _check_against_oracle(p, X.T, U.T, nu.T, 1.0, br.scp.prob.value, WTS["control_weight"])
+    # the model's slab normals are the setup() dual update (update_slabs from X_prev)
+    for s, j in enumerate(nbr):
+        np.testing.assert_allclose(np.stack([z.value for z in mam.models[agent].z_params[s]]), slabs[s][0], atol=1e-15)
+
+
+def test_best_response_inertia_and_slabs_single_integrator(cuda):
+    """The SI kernel instantiation with every game term the template supports (inertia, rate,
+    slabs) on a direct SCPSolver.solve_game call, against the oracle."""
+    import torch
+    import scvx_hip
+    from oracle import nash_ref, scp_problems as sp_
+    K = 30
+    p0 = sp_.scp_instance("si", K=K, sigma_ref=20.0, x_init=[-4.0, 0.0, 0.0], x_final=[4.0, 0.0, 0.0],
+                          obstacles=SI_OBS)
+    rng = np.random.default_rng(2)
+    Xprev = p0["Xref"] + 0.3 * rng.standard_normal((K, 3))
+    Xprev[0], Xprev[-1] = p0["x_init"], p0["x_final"]
+    nbrP = [sp_.straight([0.0, -4.0, 0.0], [0.0, 4.0, 0.0], K), sp_.straight([0.0, 0.0, -4.0], [0.0, 0.0, 4.0], K)]
+    slabs = [(nash_ref.slab_normals(Xprev, P), P) for P in nbrP]
+    wts = dict(control_weight=5.0, control_rate_weight=5.0, inertia_weight=2.0)
+    p = nash_ref.game_problem("si", p0["Xref"], p0["Uref"], 20.0, sp_.model_constraints("si", p0["x_init"], p0["x_final"],
+                              obstacles=SI_OBS), wts, Xprev, slabs, 1.0, disc=None)
+    c = sp_.model_constraints("si", p0["x_init"], p0["x_final"], obstacles=SI_OBS)
+    spec = scvx_hip.SCPSpec(model="si", K=K, pos_dim=3, u_bounds=c["u_bounds"], u_soc=c["u_soc"], x_bounds=c["x_bounds"],
+                            obs=c["obs"], w_nu=p["w_nu"], w_slack=p["w_slack"], w_sigma=p["w_sigma"], game=True,
+                            sigma_fixed=True, w_u2=5.0, w_du=5.0, theta_idx=-1, w_in=2.0, n_slab=2, r_slab=1.0)
+    T = lambda a: torch.tensor(np.ascontiguousarray(a), dtype=torch.float64, device=cuda)  # noqa: E731
+    disc = np.hstack([a.T for a in sp_.foh_oracle.foh("si", p0["Xref"].T.copy(), p0["Uref"].T.copy(), 20.0, nsub=16)])
+    out = scvx_hip.SCPSolver(spec, 1, device=cuda).solve_game(
+        T(disc[None]), T(p0["Xref"][None]), T(p0["Uref"][None]), T([20.0]), T([p0["tr"]]), T(p0["x_init"][None]),
+        T(p0["x_final"][None]), X_prev=T(Xprev[None]), slab_z=T(np.stack([s[0] for s in slabs])[None]),
+        slab_P=T(np.stack([s[1] for s in slabs])[None]))
+    g = {k: v.cpu().numpy()[0] for k, v in out.items()}
+    assert g["status"] in (0, 1), g["status"]
+    assert g["sigma"] == 20.0
+    p["disc"] = disc
+    _check_against_oracle(p, g["X"], g["U"], g["nu"], 20.0, float(g["obj"]), 5.0)
+
+
+def test_si_best_response_follows_reference_constraint_replacement(cuda):
+    """SI_AgentBestResponse: update_intersample_constraints replaces the slab rows (game_si_model.py:150-151),
+    so the solve has no slab rows -- same value as the oracle without slabs."""
+    from oracle import nash_ref, scp_problems as sp_
+    from SCvx.global_parameters import K
+    from SCvx.models.game_si_model import GameSIModel, IntersampleConstraint
+    from SCvx.models.SI_multi_agent_model import SI_MultiAgentModel
+    from SCvx.optimization.si_agent_best_response import SI_AgentBestResponse
+    params = [dict(r_init=np.array(a), r_final=np.array(b), obstacles=SI_OBS) for a, b in SI_GAME]
+    mam = SI_MultiAgentModel(params)
+    for i, p in enumerate(params):
+        mam.models[i] = GameSIModel(r_init=p["r_init"], r_final=p["r_final"], obstacles=SI_OBS, robot_radius=0.5,
+                                    control_weight=5.0, collision_weight=200.0, collision_radius=1.0,
+                                    control_rate_weight=5.0, curvature_weight=100.0)
+    X0 = [sp_.straight(a, b, K).T for a, b in SI_GAME]
+    U0 = [np.zeros((3, K)) for _ in SI_GAME]
+    br = SI_AgentBestResponse(0, mam)
+    mats = [a.copy() for a in br.foh.calculate_discretization(X0[0], U0[0], 12.0)]
+    refs = {1: X0[1], 2: X0[2]}
+    br.setup(X0[0], U0[0], 12.0, mats, refs, X0[0], refs)
+    assert all(isinstance(c, IntersampleConstraint) for c in mam.models[0].extra_constraints)
+    assert br.spec().n_slab == 0
+    X, U, nu, _, _ = br.solve()
+    cons = sp_.model_constraints("si", SI_GAME[0][0], SI_GAME[0][1], obstacles=SI_OBS)
+    p = nash_ref.game_problem("si", X0[0].T, U0[0].T, 12.0, cons, SI_WTS, X0[0].T, [], 1.0,
+                              disc=_disc_stacks(np.hstack([a.T for a in mats]), 3, 3))
+    _check_against_oracle(p, X.T, U.T, nu.T, 12.0, br.scp.prob.value, 5.0)
+
+
+def test_nash_solver_gauss_seidel_trace_matches_reference_iteration(cuda):
+    """Two outer iterations of NashSolver on the default game (K = global K), replayed step by step."""
+    from oracle import nash_ref, scp_problems as sp_
+    from SCvx.global_parameters import K
+    from SCvx.optimization.nash_solver import NashSolver
+    mam = _mam()
+    X0, U0 = (list(v) for v in _warm(K))
+    ns = NashSolver(mam, max_iter=2, tol=1e-3, max_acs_iters=3)
+    ns.trace = []
+    X, U, hist = ns.solve(X0, U0, sigma_ref=1.0)
+    tr = ns.trace
+    assert len(hist) == 2 and all(np.isfinite(hist))
+    cons = [sp_.model_constraints("unicycle", a, b, obstacles=OBS_G) for a, b in GAME]
+    cur = [x.T.copy() for x in X0]                       # X_curr (node-major)
+    checked = 0
+    for it in range(2):
+        prev = [x.copy() for x in cur]                    # X_prev_all
+        deltas = []
+        for i in range(3):
+            steps = [e for e in tr if e["it"] == it and e["agent"] == i]
+            nbr = [j for j in range(3) if j != i]
+            assert 1 <= len(steps) <= 3
+            for e in steps:
+                np.testing.assert_array_equal(e["Xref"], cur[i])
+                np.testing.assert_array_equal(e["X_prev"], prev[i])
+                np.testing.assert_array_equal(e["P"], np.stack([cur[j][:, :2] for j in nbr]))   # Gauss-Seidel
+                if e["acs"] == 0:
+                    want = [nash_ref.slab_normals(prev[i][:, :2], prev[j][:, :2]) for j in nbr]
+                else:
+                    last = steps[e["acs"] - 1]["X"]
+                    want = [nash_ref.slab_normals(last[:, :2], cur[j][:, :2]) for j in nbr]
+                np.testing.assert_allclose(e["z"], np.stack(want), rtol=0, atol=1e-15)
+                assert e["status"] in (0, 1)
+                if e["acs"] < 2 or it == 0:           # the oracle replay of every solve costs ~1 s each
+                    p = nash_ref.game_problem("unicycle", cur[i], e["Uref"], 1.0, cons[i], WTS, prev[i],
+                                              list(zip(e["z"], e["P"])), 0.5,
+                                              disc=_disc_stacks(e["disc"], 3, 2))
+                    _check_against_oracle(p, e["X"], e["U"], e["nu"], 1.0, float(e["obj"]), WTS["control_weight"])
+                    checked += 1
+            # ACS stopping rule: stop at the first ||X_new - X_curr[i]|| < acs_tol, else after max_acs_iters
+            d = [np.linalg.norm(e["X"] - cur[i]) for e in steps]
+            assert all(v >= ns.acs_tol for v in d[:-1]) and (len(steps) == 3 or d[-1] < ns.acs_tol)
+            deltas.append(d[-1])
+            cur[i] = steps[-1]["X"].copy()
+        assert abs(hist[it] - max(deltas)) < 1e-9
+    for i in range(3):
+        np.testing.assert_array_equal(X[i], cur[i].T)
+    assert checked >= 9
+    # host-visible state (agent_best_response.py / game_model.py attributes)
+    br = ns.br_solvers[2]
+    assert br.scp.prob.status in ("optimal", "optimal_inaccurate")
+    np.testing.assert_array_equal(br.scp.get_variable("X"), X[2])
+
+
+def test_nash_solver_jacobi_mode_runs(cuda):
+    from SCvx.global_parameters import K
+    from SCvx.optimization.nash_solver import NashSolver
+    mam = _mam()
+    X0, U0 = (list(v) for v in _warm(K))
+    X, U, hist = NashSolver(mam, max_iter=2, mode="jacobi").solve(X0, U0, sigma_ref=1.0)
+    assert len(hist) == 2 and all(np.isfinite(hist))
+    assert all(np.allclose(x[:, 0], np.array(GAME[i][0])) and np.allclose(x[:, -1], np.array(GAME[i][1]))
+               for i, x in enumerate(X))
