@@ -13,10 +13,16 @@ binds them at import).
              (SCvx/docs/documentation_mutli_agent_game.md:465), with the metrics of
              compare_admm_vs_nash.py:44-49 and SCvx/utils/analysis.py:10-30.
 
-usage: python tests/ref_pins.py unicycle|admm  -> one JSON line on stdout"""
+  nash       run_nash of compare_admm_vs_nash.py:81-98: the same warm start, GameUnicycleModel agents of
+             SCvx/config/default_game.py (two obstacles, control 5, rate 5, curvature 100, radius 0.5),
+             NashSolver(max_iter=20, tol=1e-3); the document reports 6 iterations, min-sep 0.5665,
+             effort 2.9906, length 9.6735 (documentation_mutli_agent_game.md:466).
+
+usage: python tests/ref_pins.py unicycle|admm|nash  -> one JSON line on stdout"""
 import json
 import os
 import sys
+import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "dynamic-programming-multiagent-trajectory-optimiziation_amd"))
@@ -59,13 +65,45 @@ def admm():
     X0, U0 = zip(*(initial_guess(p["r_init"], p["r_final"], p["obstacles"], CLEARANCE, DOC_ERA["K"]) for p in params))
     mam = MultiAgentModel(params, d_min=D_MIN)
     coord = ADMMCoordinator(mam, rho_admm=1.0, max_iter=20)
+    t0 = time.time()
     X, U, sigma, pr, du = coord.solve(list(X0), list(U0), 1.0, verbose=False)
+    secs = time.time() - t0
     effort = float(sum((u ** 2).sum() for u in U))
     length = float(sum(np.linalg.norm(np.diff(x[:2], axis=1), axis=0).sum() for x in X))
     d = [np.linalg.norm(X[i][0:3] - X[j][0:3], axis=0).min() for i in range(3) for j in range(i + 1, 3)]
     return {"min_sep": float(min(d)), "effort": effort, "length": length, "rounds": len(pr),
-            "primal": [float(v) for v in pr], "dual": [float(v) for v in du]}
+            "primal": [float(v) for v in pr], "dual": [float(v) for v in du], "seconds": secs}
+
+
+GAME_OBS = [([1.0, 1.0], 0.25), ([1.0, -0.3], 0.02)]                     # SCvx/config/default_game.py:14-17
+GAME = [((0.0, -1.0, 0.0), (2.0, 3.0, 0.0)), ((2.0, -1.0, 0.0), (0.0, 3.0, 0.0)), ((1.0, -1.5, 0.0), (1.0, 3.0, 0.0))]
+
+
+def nash():
+    import numpy as np
+    _doc_era()
+    from SCvx.models.game_model import GameUnicycleModel
+    from SCvx.models.multi_agent_model import MultiAgentModel
+    from SCvx.optimization.nash_solver import NashSolver
+    from SCvx.utils.initial_guess import initial_guess
+    X0, U0 = zip(*(initial_guess(np.array(a), np.array(b), [OBSTACLE], CLEARANCE, DOC_ERA["K"]) for a, b in SCENARIO))
+    params = [{"r_init": np.array(a), "r_final": np.array(b), "obstacles": GAME_OBS} for a, b in GAME]
+    mam = MultiAgentModel(params)
+    for i, p in enumerate(params):
+        mam.models[i] = GameUnicycleModel(r_init=p["r_init"], r_final=p["r_final"], obstacles=GAME_OBS,
+                                          control_weight=5.0, collision_weight=10.0, collision_radius=0.5,
+                                          control_rate_weight=5.0, curvature_weight=100.0)
+    solver = NashSolver(mam, max_iter=20, tol=1e-3)
+    t0 = time.time()
+    X, U, hist = solver.solve(list(X0), list(U0), 1.0, verbose=False)
+    secs = time.time() - t0
+    effort = float(sum((u ** 2).sum() for u in U))
+    length = float(sum(np.linalg.norm(np.diff(x[:2], axis=1), axis=0).sum() for x in X))
+    d = [np.linalg.norm(X[i][0:3] - X[j][0:3], axis=0).min() for i in range(3) for j in range(i + 1, 3)]
+    slab = min(float(np.linalg.norm(X[i][:2] - X[j][:2], axis=0).min()) for i in range(3) for j in range(i + 1, 3))
+    return {"iters": len(hist), "min_sep": float(min(d)), "min_sep_xy": slab, "effort": effort, "length": length,
+            "hist": [float(v) for v in hist], "seconds": secs}
 
 
 if __name__ == "__main__":
-    print(json.dumps({"unicycle": unicycle, "admm": admm}[sys.argv[1]]()))
+    print(json.dumps({"unicycle": unicycle, "admm": admm, "nash": nash}[sys.argv[1]]()))
