@@ -7,7 +7,10 @@ max_iter, cost_list), descete_f (:9-28), x_traj_opt (:31-118), x_initial (:122-1
   * every robot solves against the PREVIOUS iterate of the others (Jacobi) and X_traj is updated only
     after all solves (:113-118);
   * per-robot subproblem exactly as :59-107 (see include/scvx_hip.h), collision normals without epsilon;
-  * the unused control row w[T-1] (:63) is pinned to 0, so X_traj[T-1, n:] is left unchanged.
+  * the unused control row w[T-1] (:63) is pinned to 0, so X_traj[T-1, n:] is left unchanged: in the
+    reference s_i[T-1, n:] appears in no constraint and no objective term, so every value is optimal
+    and Clarabel's regularised KKT system returns 0 for it (same update);
+  * a failed robot subproblem aborts the iteration with RuntimeError, as the reference aborts.
 Plotting (:141-196) is optional (matplotlib, only when run as a script with --plot).
 """
 import numpy as np
@@ -57,9 +60,12 @@ def x_traj_opt(X_traj, trust_region):
     Xn, Un = out["X"].cpu().numpy(), out["U"].cpu().numpy()
     status = out["status"].cpu().numpy()
     print("update X")
+    bad = [nm for a, nm in enumerate(names) if status[a] == 2]
+    if bad:
+        # the reference aborts here: cvxpy raises SolverError, or an infeasible solve leaves
+        # s_i.value = None and `s_val[name].all()` (:115) raises AttributeError
+        raise RuntimeError(f"x_traj_opt: subproblem of {bad} failed (solver_error)")
     for a, nm in enumerate(names):
-        if status[a] == 2:  # the reference skips robots whose solve returned no value (:115)
-            continue
         X_traj[nm][0:T, 0:n] += Xn[a] - Xr[a]
         X_traj[nm][0:T, n:n + m] += Un[a] - Ur[a]
     return X_traj

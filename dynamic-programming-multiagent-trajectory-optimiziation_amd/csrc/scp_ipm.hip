@@ -1044,11 +1044,6 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
         near_ok = pres < fmax(1e-4, T.tol) * pscale && dres < fmax(1e-4, T.tol) * dscale &&
                   gap < fmax(5e-5, T.tol) * fmax(1.0, fabs(pobj));  // ECOS reduced tolerances
         const double mu = gap / deg;
-#ifdef SCP_DEBUG
-        if (agent == 0 && lane == 0)
-            printf("SCP_DEBUG it=%d pres=%.3e/%.3e dres=%.3e/%.3e gap=%.3e pobj=%.9e near=%d\n", it, pres, pscale, dres,
-                   dscale, gap, pobj, (int)near_ok);
-#endif
         if (lane < NX) sMisc[lane] = nb(0)[Ly.o_z + lane] - xinit[lane];  // r_init
         // ---- scaling and node Hessians
         for (int t = lane; t < K; t += WAVE) {
@@ -1295,19 +1290,11 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             if (t < K - 1)
                 #pragma unroll
                 for (int i = 0; i < NXA; ++i) acc += B[Ly.o_yp + i];
-            if (!(fabs(acc) < INFINITY)) {
-                badl = 1.0;
-#ifdef SCP_DEBUG
-                if (agent == 0) printf("SCP_DEBUG breakdown at node %d (it=%d al=%.3e)\n", t, it, al);
-#endif
-            }
+            if (!(fabs(acc) < INFINITY)) badl = 1.0;
         }
         #pragma unroll
         for (int i = 0; i < NX; ++i)
             if (!(fabs(sMisc[8 + i]) < INFINITY)) badl = 1.0;
-#ifdef SCP_DEBUG
-        if (agent == 0 && lane == 0) printf("SCP_DEBUG aa=%.3e sigma=%.3e al=%.3e\n", aa, sg, al);
-#endif
         if (wave_max(badl) > 0.0) {
             if (regv < 1e-5) { regv *= 100.0; __syncthreads(); continue; }   // retry, stiffer
             status = near_ok ? 1 : 2;

@@ -10,14 +10,10 @@ namespace scvx {
 
 constexpr int WAVE = 64;
 
-// Phase boundary inside a one-wave workgroup: a compiler-level LDS fence.  With
-// SCVX_WSYNC_WAIT the LDS counter is drained as well (debug aid; not needed for correctness
-// because DS instructions of one wave are processed in order).
+// Phase boundary inside a one-wave workgroup: a compiler-level LDS fence (the LDS counter need
+// not be drained: DS instructions of one wave are processed in order).
 __device__ __forceinline__ void wsync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-#ifdef SCVX_WSYNC_WAIT
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only
-#endif
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }

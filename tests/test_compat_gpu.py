@@ -103,3 +103,13 @@ def test_dist_scvx_3d_outer_loop_runs(cuda):
         np.testing.assert_allclose(X[nm][-1, 0:6], d.x_des[nm][0:6], atol=1e-7)
         np.testing.assert_allclose(X[nm][0, 0:6], d.x_ini[nm][0:6], atol=1e-12)
     assert all(np.isfinite(costs))
+
+
+def test_dist_scvx_3d_failed_subproblem_aborts(cuda):
+    """An infeasible sweep (trust region 1e-6 cannot absorb the straight-line start's dynamics defects)
+    aborts, as the reference does (cvxpy SolverError, or `None.all()` at dist_scvx_3d.py:115)."""
+    import pytest
+    from Distributed_opt import dist_scvx_3d as d
+    X0 = d.x_initial(d.x_ini, d.x_des)
+    with pytest.raises(RuntimeError, match="solver_error"):
+        d.x_traj_opt({k: v.copy() for k, v in X0.items()}, 1e-6)

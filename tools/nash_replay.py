@@ -1,6 +1,6 @@
 """Diagnostic: re-solve one recorded NashSolver step (dbg/nash_trace.npz from tools/nash_trace_dump.py)
-with SCPSolver.solve_game -- run with SCVX_HIP_LIB=dbg/scpdbg/libscvx_hip.so for the kernel's
-SCP_DEBUG iteration log -- and compare with the oracle.
+with SCPSolver.solve_game and compare with the oracle (an instrumented build can be loaded with
+SCVX_HIP_LIB=..., see tools/build_variant.sh).
 usage: python tools/nash_replay.py <step> [max_iter] [tol]"""
 import os
 import sys
