@@ -33,7 +33,7 @@
 //                     pass the chain xi_{t+1} = Acl_t xi_t + f_t: g_t, f_t and every output off
 //                     the chain (feed-forward k0, inputs, multipliers) are computed lane-parallel
 //                     before/after the chain, and each chain step is one n-term dot product per
-//                     lane with the previous vector broadcast through readlane.
+//                     lane with the previous vector broadcast by DPP row_newbcast (NX <= 16).
 // Factor outputs other than Acl go to stage-minor workspace columns (ws[col * 64 + t]) that the
 // lane-parallel passes read coalesced.
 #pragma once
@@ -102,6 +102,7 @@ struct QPCfg {
                          P_A = P_E + NX, P_BT = P_A + NX * NX, P_BTR = P_BT + NX * NU, P_C = P_BTR + NX * NU,
                          PKT = P_C + NX * NU;
     static_assert(PKT == qp_pkt(NX, NU), "packet size");
+    static_assert(NX <= 16, "the solve chains broadcast within one 16-lane row");
     // factor outputs: stage-major blocks [t][FBS] (coalesced stores from the element-parallel
     // factor; each lane-parallel pass reads its own stage's block)
     static constexpr int B_K = 0;                  // K      NU x NX
@@ -164,6 +165,8 @@ typedef unsigned int qp_u2 __attribute__((ext_vector_type(2)));
 // compiler's vmcnt accounting fall back to vmcnt(0), which drains the packet prefetches issued
 // stages ahead (measured: most of the factor's per-stage time).
 constexpr int QP_SINK_DOUBLES = 64;
+// solve-chain prefetch depth (stages of Acl / offsets held in registers ahead of the chain)
+constexpr int QP_CPF = 4;
 struct QPBuf {
     __amdgpu_buffer_rsrc_t rs;
     __device__ __forceinline__ double ld(int voff, int soff) const {
@@ -725,7 +728,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         wsync();
         stamp(4);
         // ---- backward chain p_t = Acl_t' p_{t+1} + g_t (lane i: element i); p_{t+1} broadcast
-        // from lanes 0..NX-1 through readlane, the Acl column / g of the next stage read ahead
+        // from lanes 0..NX-1 by a DPP row broadcast (NX <= 16), the Acl column / g of the next stage read ahead
         if (lane < NX) {
             // lane i needs column i of Acl_t (stage block, B_ACL + k*NX + i)
             const int va = (C::B_ACL + lane) * 8;
@@ -739,36 +742,35 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 double v0 = g, v1 = 0.0;
 #pragma unroll
                 for (int k = 0; k < NX; ++k) {
-                    const double pkv = readlane_d(p, k);
+                    const double pkv = row_bcast_d(p, k);
                     if (k & 1) v1 = fma(ac[k], pkv, v1); else v0 = fma(ac[k], pkv, v0);
                 }
                 return v0 + v1;
             };
             double p = lds[V_G + (K - 1) * NX + lane];
             lds[V_CH + (K - 1) * NX + lane] = p;
-            // four register buffers: operands loaded four stages ahead
-            double ab[4][NX], gb[4];
+            // QP_CPF register buffers: operands loaded QP_CPF stages ahead (a global load under
+            // full-chip load takes ~2,000 cycles; 8 stages measured no faster than 4 and spilled more)
+            double ab[QP_CPF][NX], gb[QP_CPF];
 #pragma unroll
-            for (int b = 0; b < 4; ++b) ldA(K - 2 - b, ab[b], gb[b]);
+            for (int b = 0; b < QP_CPF; ++b) ldA(K - 2 - b, ab[b], gb[b]);
             int ts = K - 2;
             auto step = [&](double* a, double& g) __attribute__((always_inline)) {
                 p = chain(p, a, g);
                 lds[V_CH + ts * NX + lane] = p;
-                ldA(ts - 4, a, g);
+                ldA(ts - QP_CPF, a, g);
                 --ts;
             };
-            // groups of four steps with no exit inside the loop body (a mid-body exit makes the
+            // groups of QP_CPF steps with no exit inside the loop body (a mid-body exit makes the
             // compiler's vmcnt tracking fall back to vmcnt(0) and drain the prefetches), then the
-            // 0-3 remaining steps continuing the buffer rotation
-            while (ts >= 3) {
-                step(ab[0], gb[0]);
-                step(ab[1], gb[1]);
-                step(ab[2], gb[2]);
-                step(ab[3], gb[3]);
+            // remaining steps continuing the buffer rotation
+            while (ts >= QP_CPF - 1) {
+#pragma unroll
+                for (int b = 0; b < QP_CPF; ++b) step(ab[b], gb[b]);
             }
-            if (ts >= 0) step(ab[0], gb[0]);
-            if (ts >= 0) step(ab[1], gb[1]);
-            if (ts >= 0) step(ab[2], gb[2]);
+#pragma unroll
+            for (int b = 0; b < QP_CPF - 1; ++b)
+                if (ts >= 0) step(ab[b], gb[b]);
         }
         wsync();
         stamp(5);
@@ -904,32 +906,30 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 double w0 = f, w1 = 0.0;
 #pragma unroll
                 for (int k = 0; k < NX; ++k) {
-                    const double xk = readlane_d(x, k);
+                    const double xk = row_bcast_d(x, k);
                     if (k & 1) w1 = fma(ac[k], xk, w1); else w0 = fma(ac[k], xk, w0);
                 }
                 return w0 + w1;
             };
             double x = lds[V_XI0 + lane];
             lds[V_CH + lane] = x;
-            double ab[4][NX], fb[4];
+            double ab[QP_CPF][NX], fb[QP_CPF];
 #pragma unroll
-            for (int b = 0; b < 4; ++b) ldA(b, ab[b], fb[b]);
+            for (int b = 0; b < QP_CPF; ++b) ldA(b, ab[b], fb[b]);
             int ts = 0;
             auto step = [&](double* a, double& f) __attribute__((always_inline)) {
                 x = chain(x, a, f);
                 lds[V_CH + (ts + 1) * NX + lane] = x;
-                ldA(ts + 4, a, f);
+                ldA(ts + QP_CPF, a, f);
                 ++ts;
             };
-            while (ts <= K - 5) {  // four steps per trip, no exit inside (see the backward chain)
-                step(ab[0], fb[0]);
-                step(ab[1], fb[1]);
-                step(ab[2], fb[2]);
-                step(ab[3], fb[3]);
+            while (ts <= K - 1 - QP_CPF) {  // QP_CPF steps per trip, no exit inside (see the backward chain)
+#pragma unroll
+                for (int b = 0; b < QP_CPF; ++b) step(ab[b], fb[b]);
             }
-            if (ts < K - 1) step(ab[0], fb[0]);
-            if (ts < K - 1) step(ab[1], fb[1]);
-            if (ts < K - 1) step(ab[2], fb[2]);
+#pragma unroll
+            for (int b = 0; b < QP_CPF - 1; ++b)
+                if (ts < K - 1) step(ab[b], fb[b]);
         }
         wsync();
         stamp(8);

@@ -31,6 +31,34 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     return __hiloint2double(hi, lo);
 }
 
+// Lane l (< 16) of this lane's 16-lane row, broadcast by a 64-bit DPP move (row_newbcast, gfx90a+):
+// one VALU op with no SGPR round trip.  l must fold to a constant (unrolled loops).
+template <int L>
+__device__ __forceinline__ double row_bcast_c(double v) {
+    static_assert(L >= 0 && L < 16, "row lane");
+    return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + L, 0xF, 0xF, false);
+}
+__device__ __forceinline__ double row_bcast_d(double v, int l) {
+    switch (l) {
+        case 0: return row_bcast_c<0>(v);
+        case 1: return row_bcast_c<1>(v);
+        case 2: return row_bcast_c<2>(v);
+        case 3: return row_bcast_c<3>(v);
+        case 4: return row_bcast_c<4>(v);
+        case 5: return row_bcast_c<5>(v);
+        case 6: return row_bcast_c<6>(v);
+        case 7: return row_bcast_c<7>(v);
+        case 8: return row_bcast_c<8>(v);
+        case 9: return row_bcast_c<9>(v);
+        case 10: return row_bcast_c<10>(v);
+        case 11: return row_bcast_c<11>(v);
+        case 12: return row_bcast_c<12>(v);
+        case 13: return row_bcast_c<13>(v);
+        case 14: return row_bcast_c<14>(v);
+        default: return row_bcast_c<15>(v);
+    }
+}
+
 // Reductions over the 64 lanes (result uniform): DPP inside each 16-lane row (quad xor 1, quad
 // xor 2, half-row mirror, row mirror), then the four row results through readlane.
 #define SCVX_WAVE_REDUCE(NAME, OP)                                     \
