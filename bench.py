@@ -314,6 +314,105 @@ def bench_scproblem(args, world, rank, device):
         "cpu_baseline": cpu}), flush=True)
 
 
+def bench_nash(args, world, rank, device):
+    """--config nash: the Nash best-response path (SCvx/optimization/nash_solver.py + agent_best_response.py).
+    (1) NashSolver, Gauss-Seidel (the reference's order), on the default 3-agent game (SCvx/config/
+    default_game.py agents, K = global K = 100, warm start SCvx/utils/initial_guess.py): `steps` outer
+    iterations (tol < 0, so exactly that many), each = 3 agents x max_acs_iters ACS solves; one agent per
+    launch, so this is the latency-bound sequential path.  (2) The game kernel's throughput: N = 1024
+    best responses (the three agents' first problems, neighbour positions jittered) in one
+    scvx_scp_game_solve_batched launch, timed with HIP events on the launch stream."""
+    import torch
+    sys.path.insert(0, os.path.join(REPO, "dynamic-programming-multiagent-trajectory-optimiziation_amd"))
+    from SCvx.config import default_game as G
+    from SCvx.global_parameters import K as KG
+    from SCvx.models.game_model import GameUnicycleModel
+    from SCvx.models.multi_agent_model import MultiAgentModel
+    from SCvx.optimization.nash_solver import NashSolver
+    from SCvx.optimization.sc_problem import _solver
+    from SCvx.utils.initial_guess import initial_guess
+    X0, U0 = (list(v) for v in zip(*(initial_guess(p["r_init"], p["r_final"], G.OBSTACLES, G.CLEARANCE, KG)
+                                     for p in G.AGENT_PARAMS)))
+    mam = MultiAgentModel(G.AGENT_PARAMS)
+    for i, p in enumerate(G.AGENT_PARAMS):       # compare_admm_vs_nash.py:84-95
+        mam.models[i] = GameUnicycleModel(**{k: p[k] for k in ("r_init", "r_final", "obstacles", "control_weight",
+                                                               "collision_weight", "collision_radius",
+                                                               "control_rate_weight", "curvature_weight")})
+    ns = NashSolver(mam, max_iter=max(args.warmup, 1), tol=-1.0)
+    ns.solve(X0, U0, 1.0)
+    torch.cuda.synchronize()
+    ns.max_iter = args.steps
+    t0 = time.perf_counter()
+    ns.solve(X0, U0, 1.0)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    solves = ns.solves
+    # (2) batched throughput on the game kernel
+    br = ns.br_solvers
+    N = args.agents
+    rng = np.random.default_rng(5 + rank)
+    T = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float64, device=device)  # noqa: E731
+    ins = [b.scp.host_inputs() for b in br]
+    pick = [a % len(br) for a in range(N)]
+    args_b = {k: T(np.stack([ins[i][k] for i in pick]) if np.ndim(ins[0][k]) else [ins[i][k] for i in pick])
+              for k in ins[0]}
+    spec = br[0].spec()
+    X_prev = T(np.stack([np.asarray(br[i].X_prev_param.require(), float).T for i in pick]))
+    P = np.stack([np.stack([np.asarray(br[i].Y_params[j].require(), float).T for j in sorted(br[i].Y_params)])
+                  for i in pick])
+    P = T(P + rng.uniform(-0.05, 0.05, P.shape))
+    z = scvx_hip.slab_update(X_prev, P, spec.pos_dim)
+    solver = _solver(spec, N, device)
+    for _ in range(2):
+        solver.solve_game(X_prev=X_prev, slab_z=z, slab_P=P, **args_b)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    reps = 5
+    ev[0].record()
+    for _ in range(reps):
+        out = solver.solve_game(X_prev=X_prev, slab_z=z, slab_P=P, **args_b)
+    ev[1].record()
+    torch.cuda.synchronize()
+    launch_ms = ev[0].elapsed_time(ev[1]) / reps
+    st = out["status"].cpu().numpy()
+    it = out["iters"].cpu().numpy()
+    cpu = None
+    if not args.no_cpu:
+        from oracle import nash_ref, scp_problems as sp_
+        b0 = br[0]
+        i0 = b0.scp.host_inputs()
+        p0 = G.AGENT_PARAMS[0]
+        cons = sp_.model_constraints("unicycle", p0["r_init"], p0["r_final"], obstacles=G.OBSTACLES)
+        wts = {k: p0[k] for k in ("control_weight", "control_rate_weight", "curvature_weight")}
+        slabs = [(np.stack([zz.require() for zz in row]), np.asarray(b0.Y_params[j].require(), float).T)
+                 for row, j in zip(b0.model.z_params, sorted(b0.Y_params))]
+        pr = nash_ref.game_problem("unicycle", i0["Xref"], i0["Uref"], 1.0, cons, wts,
+                                   np.asarray(b0.X_prev_param.require(), float).T, slabs, p0["collision_radius"],
+                                   disc=nash_ref.disc_stacks(i0["disc"], 3, 2))
+        t1, done = time.perf_counter(), 0
+        while time.perf_counter() - t1 < 10.0:
+            nash_ref.best_response(pr)
+            done += 1
+        cel = time.perf_counter() - t1
+        cpu = dict(value=done / cel, unit="best-responses/s", cores=1, kind="port",
+                   sample=f"{done} solves of agent 0's best response (oracle/nash_ref.py: the reference formulation, "
+                          f"sparse conic IPM in numpy/scipy, 1 thread), {cel:.1f} s")
+    if rank != 0:
+        return
+    print(json.dumps({
+        "metric": "Nash best responses/sec (default 3-agent game, K=100), Gauss-Seidel IBR + ACS",
+        "value": solves / el, "unit": "best-responses/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": 1e3 * el / args.steps, "ms_per_best_response": 1e3 * el / max(solves, 1),
+        "higher_is_better": True, "scaling": "replicas only", "vs_baseline": None, "dtype": "f64",
+        "data": "SCvx/config/default_game.py agents, initial_guess warm start",
+        "config": {"workload": f"nash: NashSolver GS, 3 agents, K={KG}, max_acs_iters=5; an outer iteration = "
+                               "3 x 5 best responses", "agents_per_gpu": 3, "K": KG, "parallelism": "none (GS order)"},
+        "batched_game_kernel": {"agents": N, "launch_ms": launch_ms, "best_responses_per_s": N / (launch_ms * 1e-3),
+                                "ipm_iters_mean": float(it.mean()), "ipm_iters_max": int(it.max()),
+                                "status_counts": {str(k): int((st == k).sum()) for k in (0, 1, 2)}},
+        "cpu_baseline": cpu}), flush=True)
+
+
 def _free_port():
     import socket
     with socket.socket() as so:
@@ -369,7 +468,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", choices=("c3", "c4", "c5", "is", "scp"), default="c3")
+    ap.add_argument("--config", choices=("c3", "c4", "c5", "is", "scp", "nash"), default="c3")
     ap.add_argument("--agents", type=int, default=N_AGENTS, help="c3: agents per GPU")
     ap.add_argument("--cpu-sample", type=int, default=1024)
     ap.add_argument("--no-cpu", action="store_true")
@@ -402,6 +501,8 @@ def main():
         return bench_intersample(args, world, rank, device)
     if args.config == "scp":
         return bench_scproblem(args, world, rank, device)
+    if args.config == "nash":
+        return bench_nash(args, world, rank, device)
     if args.config == "c3":
         N = args.agents
         sc, w = make_workload(N, seed=1 + rank, device=device)

@@ -17,12 +17,11 @@ from typing import List, Optional, Tuple
 
 import numpy as np
 
+from ..config.SI_default_game import AGT_COLL_RAD
 from ..global_parameters import K as GLOBAL_K
 from ..optimization.variables import Parameter, Variable
 from .game_model import GameCost, SlabConstraint, slab_normals
 from .single_integrator_model import SingleIntegratorModel
-
-AGT_COLL_RAD = 1.0   # SCvx/config/SI_default_game.py:22: 2 * ROBOT_RADIUS + MARGIN_AGT
 
 
 class IntersampleConstraint:

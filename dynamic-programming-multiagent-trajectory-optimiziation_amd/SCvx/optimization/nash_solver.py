@@ -53,6 +53,7 @@ class NashSolver:
         self.acs_tol = acs_tol
         self.mode = mode
         self.trace = None    # set to a list to record every best-response solve (host copies; tests)
+        self.solves = 0      # best-response solves of the last solve() (agents x ACS steps)
 
     # ---------------------------------------------------------------------------------------------
     def _specs(self, X_h, U_h, sigma_ref):
@@ -92,6 +93,7 @@ class NashSolver:
         last = [None] * N
         slabs = [None] * N
         t0 = time.time()
+        self.solves = 0
         for it in range(self.max_iter):
             if verbose:
                 print(f"\n--- Outer iteration {it} ---")
@@ -136,6 +138,7 @@ class NashSolver:
             zin = z.clone()
             out = solver.solve_game(disc[s_], Xr, Ur, sig[s_], tr[s_], x_init[s_], x_final[s_], X_prev=Xp[s_].contiguous(),
                                     slab_z=zin, slab_P=P)
+            self.solves += 1
             if self.trace is not None:
                 self.trace.append(dict(it=self._it, agent=i, acs=acs, disc=disc[i].cpu().numpy(), Xref=Xr[0].cpu().numpy(),
                                        Uref=Ur[0].cpu().numpy(), X_prev=Xp[i].cpu().numpy(), z=zin[0].cpu().numpy(),
@@ -169,6 +172,7 @@ class NashSolver:
         for _ in range(self.max_acs_iters):
             out = solver.solve_game(disc, X.clone(), U.clone(), sig, tr, x_init, x_final, X_prev=Xp, slab_z=z.clone(),
                                     slab_P=P)
+            self.solves += int(active.sum())
             if bool((out["status"][active] >= 2).any()):
                 i = int((active & (out["status"] >= 2)).nonzero()[0, 0])
                 raise self.br_solvers[i]._failed()

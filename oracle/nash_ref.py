@@ -54,6 +54,14 @@ def game_problem(model, Xref, Uref, sigma_ref, cons, weights, X_prev, slabs, r_s
     return p
 
 
+def disc_stacks(disc, n, m):
+    """Kernel disc rows (K-1, n(n+2m+2): F-order A | B | C | S | z per node) -> node-major stacks."""
+    K1 = disc.shape[0]
+    o = np.cumsum([0, n * n, n * m, n * m, n, n])
+    return (disc[:, o[0]:o[1]].reshape(K1, n, n).transpose(0, 2, 1), disc[:, o[1]:o[2]].reshape(K1, m, n).transpose(0, 2, 1),
+            disc[:, o[2]:o[3]].reshape(K1, m, n).transpose(0, 2, 1), disc[:, o[3]:o[4]].copy(), disc[:, o[4]:o[5]].copy())
+
+
 def best_response(p, tol=1e-10, maxit=300):
     return scp_dense.solve_scproblem(p, tol=tol, maxit=maxit)
 

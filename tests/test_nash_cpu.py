@@ -4,7 +4,7 @@ kernel template it derives (agent_best_response.py:46-98)."""
 import numpy as np
 import pytest
 
-from tests.test_nash_gpu import GAME, OBS_G, _mam
+from tests.test_nash_gpu import GAME, OBS_G, SI_GAME, SI_OBS, _cfg, _mam
 
 
 def test_game_model_surface_and_records():
@@ -83,3 +83,11 @@ def test_game_si_model_records():
     np.testing.assert_allclose(m.z_params[0][0].value, -np.ones(3) / np.sqrt(3))
     m.update_intersample_constraints(None, None, np.zeros((3, K)), np.zeros((3, K)), None, 1.0)
     assert m.extra_constraints == [] and m.inter_slacks == []   # replaced (no obstacles -> no rows)
+
+
+def test_config_modules_hold_the_reference_scenarios():
+    """SCvx/config data against the reference's default_game.py / SI_default_game.py values."""
+    g, sg = _cfg()
+    assert [(tuple(p["r_init"]), tuple(p["r_final"])) for p in g.AGENT_PARAMS] == GAME and g.OBSTACLES == OBS_G
+    assert [(tuple(p["r_init"]), tuple(p["r_final"])) for p in sg.AGENT_PARAMS] == SI_GAME and sg.OBSTACLES == SI_OBS
+    assert sg.AGT_COLL_RAD == 1.0 and g.COLL_RAD == 0.5

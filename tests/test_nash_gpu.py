@@ -16,7 +16,12 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-OBS_G = [([1.0, 1.0], 0.25), ([1.0, -0.3], 0.02)]                # SCvx/config/default_game.py:14-17
+def _cfg():
+    from SCvx.config import SI_default_game as sg, default_game as g
+    return g, sg
+
+
+OBS_G = [([1.0, 1.0], 0.25), ([1.0, -0.3], 0.02)]                # SCvx/config/default_game.py (reference :14-17)
 GAME = [((0.0, -1.0, 0.0), (2.0, 3.0, 0.0)), ((2.0, -1.0, 0.0), (0.0, 3.0, 0.0)), ((1.0, -1.5, 0.0), (1.0, 3.0, 0.0))]
 WTS = dict(control_weight=5.0, control_rate_weight=5.0, curvature_weight=100.0)   # :21-26
 SI_OBS = [([0.0, 0.0, 0.0], 0.8)]                                   # SCvx/config/SI_default_game.py:16-18
@@ -25,14 +30,18 @@ SI_WTS = dict(control_weight=5.0, control_rate_weight=5.0)
 
 
 def _mam():
+    """The reference's run_nash (compare_admm_vs_nash.py:84-95): MultiAgentModel of the default game with
+    every agent replaced by a GameUnicycleModel carrying its weights."""
     from SCvx.models.game_model import GameUnicycleModel
     from SCvx.models.multi_agent_model import MultiAgentModel
-    params = [dict(r_init=np.array(a), r_final=np.array(b), obstacles=OBS_G) for a, b in GAME]
-    mam = MultiAgentModel(params)
-    for i, p in enumerate(params):     # SCvx/examples/compare_admm_vs_nash.py:84-95
-        mam.models[i] = GameUnicycleModel(r_init=p["r_init"], r_final=p["r_final"], obstacles=OBS_G,
-                                          control_weight=5.0, collision_weight=10.0, collision_radius=0.5,
-                                          control_rate_weight=5.0, curvature_weight=100.0)
+    g, _ = _cfg()
+    mam = MultiAgentModel(g.AGENT_PARAMS)
+    for i, p in enumerate(g.AGENT_PARAMS):
+        mam.models[i] = GameUnicycleModel(r_init=p["r_init"], r_final=p["r_final"], obstacles=p["obstacles"],
+                                          control_weight=p["control_weight"], collision_weight=p["collision_weight"],
+                                          collision_radius=p["collision_radius"],
+                                          control_rate_weight=p["control_rate_weight"],
+                                          curvature_weight=p["curvature_weight"])
     return mam
 
 
@@ -42,10 +51,8 @@ def _warm(K, game=GAME, obs=OBS_G):
 
 
 def _disc_stacks(disc, n, m):
-    K1 = disc.shape[0]
-    o = np.cumsum([0, n * n, n * m, n * m, n, n])
-    return (disc[:, o[0]:o[1]].reshape(K1, n, n).transpose(0, 2, 1), disc[:, o[1]:o[2]].reshape(K1, m, n).transpose(0, 2, 1),
-            disc[:, o[2]:o[3]].reshape(K1, m, n).transpose(0, 2, 1), disc[:, o[3]:o[4]].copy(), disc[:, o[4]:o[5]].copy())
+    from oracle import nash_ref
+    return nash_ref.disc_stacks(disc, n, m)
 
 
 def _check_against_oracle(p, X, U, nu, sigma, obj_kernel, w_u2):
