@@ -323,6 +323,7 @@ def bench_nash(args, world, rank, device):
     best responses (the three agents' first problems, neighbour positions jittered) in one
     scvx_scp_game_solve_batched launch, timed with HIP events on the launch stream."""
     import torch
+    import scvx_hip
     sys.path.insert(0, os.path.join(REPO, "dynamic-programming-multiagent-trajectory-optimiziation_amd"))
     from SCvx.config import default_game as G
     from SCvx.global_parameters import K as KG

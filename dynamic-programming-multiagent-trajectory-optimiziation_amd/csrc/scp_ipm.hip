@@ -934,6 +934,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
     // primal regularisation of the iteration's Newton systems: raised x100 to retry an iteration whose
     // direction broke down (Riccati overflow in the end-game), relaxed x0.01 after every taken step
     double regv = T.reg;
+    double pres_best = INFINITY, dres_best = INFINITY;
 #ifdef SCP_TRACE
     long long tr_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     long long tr_last = __builtin_amdgcn_s_memtime();
@@ -1043,6 +1044,15 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
         // if the iteration cap or a numerical breakdown ends the solve before full accuracy
         near_ok = pres < fmax(1e-4, T.tol) * pscale && dres < fmax(1e-4, T.tol) * dscale &&
                   gap < fmax(5e-5, T.tol) * fmax(1.0, fabs(pobj));  // ECOS reduced tolerances
+        // insufficient progress (ECOS's end-game exit): once the reduced tolerances hold, a residual
+        // that jumps 100x above its best (the Newton systems' accuracy floor, barrier ratios ~1e16) ends
+        // the solve as optimal_inaccurate instead of letting the iterate drift away
+        if (near_ok && (pres > fmax(100.0 * pres_best, T.tol * pscale) || dres > fmax(100.0 * dres_best, T.tol * dscale))) {
+            status = 1;
+            break;
+        }
+        pres_best = fmin(pres_best, pres);
+        dres_best = fmin(dres_best, dres);
         const double mu = gap / deg;
         if (lane < NX) sMisc[lane] = nb(0)[Ly.o_z + lane] - xinit[lane];  // r_init
         // ---- scaling and node Hessians

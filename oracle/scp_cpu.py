@@ -313,6 +313,7 @@ class SCPSolver:
                                                                      default=0.0))
         pscale, dscale = 1.0 + hmax, 1.0 + qmax
         status, it, near_ok = "max_iter", 0, False
+        pres_best = dres_best = np.inf
         self.trace = []
         self._regv = self.reg     # kernel: regv (x100 retry after a breakdown, x0.01 after a step)
         for it in range(self.max_iter):
@@ -355,6 +356,12 @@ class SCPSolver:
             # reduced (ECOS-style "inaccurate") tolerances, used if the solve ends early (kernel: near_ok)
             near_ok = (pres < max(1e-4, self.tol) * pscale and dres < max(1e-4, self.tol) * dscale
                        and gap < max(5e-5, self.tol) * max(1.0, abs(pobj)))   # ECOS reduced tolerances
+            # insufficient progress (kernel: pres_best / dres_best): a residual jumping 100x above its best
+            if near_ok and (pres > max(100.0 * pres_best, self.tol * pscale)
+                            or dres > max(100.0 * dres_best, self.tol * dscale)):
+                status = "inaccurate"
+                break
+            pres_best, dres_best = min(pres_best, pres), min(dres_best, dres)
             # scaling
             Wn = [self._nt(nd, s[k], lam[k]) for k, nd in enumerate(nodes)]
             lt = [self._Wmul(nd, Wn[k], lam[k], 0) for k, nd in enumerate(nodes)]   # lambda~ = W lam

@@ -1,0 +1,31 @@
+"""Diagnostic: re-solve the instance tools/nash_batch_diag.py saved (dbg/nash_fail.npz) once with the
+game kernel (load an instrumented build with SCVX_HIP_LIB=...)."""
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "dynamic-programming-multiagent-trajectory-optimiziation_amd"))
+import torch  # noqa: E402
+
+import scvx_hip  # noqa: E402
+from SCvx.config import default_game as G  # noqa: E402
+from SCvx.models.game_model import GameUnicycleModel  # noqa: E402
+
+d = np.load(os.path.join(REPO, "dbg", "nash_fail.npz"))
+p = G.AGENT_PARAMS[2]
+m = GameUnicycleModel(**{k: p[k] for k in ("r_init", "r_final", "obstacles", "control_weight", "collision_weight",
+                                           "collision_radius", "control_rate_weight", "curvature_weight")})
+c = m.scp_constraints()
+K = d["Xref"].shape[0]
+tol = float(sys.argv[1]) if len(sys.argv) > 1 else 1e-9
+spec = scvx_hip.SCPSpec(model="unicycle", K=K, pos_dim=2, u_bounds=c["u_bounds"], x_bounds=c["x_bounds"], obs=c["obs"],
+                        w_nu=1e4, w_slack=1e6, w_sigma=100.0, max_iter=100, tol=tol, game=True, sigma_fixed=True,
+                        w_u2=5.0, w_du=5.0, w_dth=100.0, theta_idx=2, n_slab=2, r_slab=0.5)
+T = lambda a: torch.tensor(np.ascontiguousarray(a), dtype=torch.float64, device="cuda")  # noqa: E731
+out = scvx_hip.SCPSolver(spec, 1).solve_game(T(d["disc"][None]), T(d["Xref"][None]), T(d["Uref"][None]), T([1.0]),
+                                              T([100.0]), T(c["x_init"][None]), T(c["x_final"][None]),
+                                              X_prev=T(d["X_prev"][None]), slab_z=T(d["z"][None]), slab_P=T(d["P"][None]))
+torch.cuda.synchronize()
+print("status", int(out["status"][0]), "iters", int(out["iters"][0]), "obj", float(out["obj"][0]))
