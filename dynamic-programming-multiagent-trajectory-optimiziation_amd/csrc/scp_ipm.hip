@@ -109,6 +109,7 @@ __host__ __device__ inline SCPLay scp_layout(const scvx_scp_template& T) {
     L.o_LD = take(NUA * NUA);
     L.o_nh = take(1);
     L.stride = (o + 7) & ~7;
+    if (L.stride < 64) L.stride = 64;  // the junk block after the K node blocks holds one slot per lane
     return L;
 }
 
@@ -227,6 +228,10 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
     const int RH = Ly.RH, NS = Ly.NS, Q = Ly.Q, RL = Ly.RL, NLP = RH + 2 * NS;
     double* ws = ws_all + agent * a.ws_agent;
     auto nb = [&](int t) -> double* { return ws + (long long)t * Ly.stride; };
+    // per-lane junk slot after the K node blocks: lanes without an output of their own store there, so
+    // every global store of the sweeps is unconditional (a store under a divergent branch makes the
+    // compiler's vmcnt accounting fall back to vmcnt(0), draining the next stage's prefetched packet)
+    double* const jnk = ws + (long long)K * Ly.stride + lane;
     const double* disc = disc_all + agent * (long long)(K - 1) * (NX * (NX + 2 * NU + 2));
     constexpr int DSTR = NX * (NX + 2 * NU + 2);
     const double trv = a.tr[agent], sref = a.sigma_ref[agent];
@@ -638,27 +643,34 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             #pragma unroll
             for (int e = 0; e < NUA * NUA; ++e) Lm[e] = sQuu[e];
             ldl_factor<NUA>(Lm, NUA);
-            if (lane < NXA) {
+            {  // every lane solves (lanes >= NXA on a copy of column 0, stored to the junk slot)
+                const bool kl = lane < NXA;
+                const int c = kl ? lane : 0;
                 double x[NUA];
                 #pragma unroll
-                for (int i = 0; i < NUA; ++i) x[i] = -sQux[i * NXA + lane];
+                for (int i = 0; i < NUA; ++i) x[i] = -sQux[i * NXA + c];
                 ldl_solve<NUA>(Lm, NUA, x);
                 #pragma unroll
                 for (int i = 0; i < NUA; ++i) {
-                    sK[i * NXA + lane] = x[i];
-                    nb(t)[Ly.o_K + i * NXA + lane] = x[i];
+                    if (kl) sK[i * NXA + lane] = x[i];
+                    *(kl ? nb(t) + Ly.o_K + i * NXA + lane : jnk) = x[i];
                 }
-            }
-            if (lane == 0)
+                double lv = 0.0;  // element `lane` of the factor (select chain: no dynamic register index)
                 #pragma unroll
-                for (int e = 0; e < NUA * NUA; ++e) nb(t)[Ly.o_LD + e] = Lm[e];
+                for (int e = 0; e < NUA * NUA; ++e) lv = (e == lane) ? Lm[e] : lv;
+                *(lane < NUA * NUA ? nb(t) + Ly.o_LD + lane : jnk) = lv;
+            }
             wsync();
-            for (int e = lane; e < NXA * NXA; e += WAVE) {
-                const int i = e / NXA, j = e % NXA, p = i < j ? i : j, q = i < j ? j : i;
+            #pragma unroll
+            for (int rep = 0; rep < (NXA * NXA + WAVE - 1) / WAVE; ++rep) {
+                const int e = lane + rep * WAVE;
+                const bool ok = e < NXA * NXA;
+                const int ee = ok ? e : 0;
+                const int i = ee / NXA, j = ee % NXA, p = i < j ? i : j, q = i < j ? j : i;
                 double v = sQxx[p * NXA + q];
                 for (int k = 0; k < NUA; ++k) v += sQux[k * NXA + p] * sK[k * NXA + q];
-                sP[e] = v;
-                nb(t)[Ly.o_Pr + e] = v;
+                if (ok) sP[e] = v;
+                *(ok ? nb(t) + Ly.o_Pr + e : jnk) = v;
             }
             park(slot ^ 1);
             wsync();
@@ -713,19 +725,18 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
                     #pragma unroll
                     for (int i = 0; i < NUA; ++i) x[i] = -sQ[NXA + i];
                     ldl_solve<NUA>(Lm, NUA, x);
-                    if (lane < NUA) {
-                        // (select x[lane] without dynamic register indexing)
-                        double xv = 0.0;
-                        #pragma unroll
-                        for (int i = 0; i < NUA; ++i) xv = (i == lane) ? x[i] : xv;
-                        nb(t)[Ly.o_kv + lane] = xv;
-                    }
+                    // (select x[lane] without dynamic register indexing)
+                    double xv = 0.0;
+                    #pragma unroll
+                    for (int i = 0; i < NUA; ++i) xv = (i == lane) ? x[i] : xv;
+                    *(lane < NUA ? nb(t) + Ly.o_kv + lane : jnk) = xv;
                 }
-                double pn = 0.0;
-                if (lane < NXA) {
-                    pn = sQ[lane];
-                    for (int k = 0; k < NUA; ++k) pn += pk[B_K + k * NXA + lane] * sQ[NXA + k];
-                    nb(t)[Ly.o_pv + lane] = pn;
+                double pn;
+                {
+                    const int li = lane < NXA ? lane : 0;
+                    pn = sQ[li];
+                    for (int k = 0; k < NUA; ++k) pn += pk[B_K + k * NXA + li] * sQ[NXA + k];
+                    *(lane < NXA ? nb(t) + Ly.o_pv + lane : jnk) = pn;
                 }
                 wsync();
                 if (lane < NXA) sPv[lane] = pn;
@@ -779,13 +790,14 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
                 gather(t + 1, dn, off, len, 7);
                 const double* pk = sRing[slot];
                 double* B = nb(t);
-                if (lane < NUA) {
-                    double v = pk[W_KV + lane];
-                    for (int k = 0; k < NXA; ++k) v += pk[W_K + lane * NXA + k] * sXi[cur][k];
-                    sU[lane] = v;
-                    B[Ly.o_dz + NXA + lane] = v;
+                {
+                    const int lu = lane < NUA ? lane : 0;
+                    double v = pk[W_KV + lu];
+                    for (int k = 0; k < NXA; ++k) v += pk[W_K + lu * NXA + k] * sXi[cur][k];
+                    if (lane < NUA) sU[lane] = v;
+                    *(lane < NUA ? B + Ly.o_dz + NXA + lane : jnk) = v;
                 }
-                if (lane < NXA) B[Ly.o_dz + lane] = sXi[cur][lane];
+                *(lane < NXA ? B + Ly.o_dz + lane : jnk) = sXi[cur][lane < NXA ? lane : 0];
                 wsync();
                 if (t < K - 1) {
                     if (lane < NXA) {
@@ -796,10 +808,11 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
                     }
                     wsync();
                     cur ^= 1;
-                    if (lane < NXA) {
-                        double v = pk[W_PV1 + lane];
-                        for (int k = 0; k < NXA; ++k) v += pk[W_PR1 + lane * NXA + k] * sXi[cur][k];
-                        B[Ly.o_yp + lane] = v;
+                    {
+                        const int li = lane < NXA ? lane : 0;
+                        double v = pk[W_PV1 + li];
+                        for (int k = 0; k < NXA; ++k) v += pk[W_PR1 + li * NXA + k] * sXi[cur][k];
+                        *(lane < NXA ? B + Ly.o_yp + lane : jnk) = v;
                     }
                 }
                 park(slot ^ 1);
@@ -1444,7 +1457,7 @@ using namespace scvx;
 extern "C" size_t scvx_scp_workspace_bytes(const scvx_scp_template* T, int N) {
     if (!T || N < 0) return 0;
     const SCPLay L = scp_layout(*T);
-    return sizeof(double) * (size_t)N * (size_t)L.stride * (size_t)T->K;
+    return sizeof(double) * (size_t)N * (size_t)L.stride * (size_t)(T->K + 1);  // + the per-lane junk block
 }
 
 static int scp_launch(const scvx_scp_template* T, int N, const double* disc, const double* Xref, const double* Uref,
@@ -1489,7 +1502,7 @@ static int scp_launch(const scvx_scp_template* T, int N, const double* disc, con
     a.X = X; a.U = U; a.nu = nu; a.sigma = sigma; a.s_obs = s_obs; a.s_nbr = s_nbr; a.obj = obj;
     a.status = status; a.iters = iters;
     a.ws = (double*)workspace;
-    a.ws_agent = (long long)scp_layout(*T).stride * T->K;
+    a.ws_agent = (long long)scp_layout(*T).stride * (T->K + 1);
     hipStream_t st = (hipStream_t)stream;
     const int ne = scp_ne(*T);
     if (T->model_id == SCVX_MODEL_UNICYCLE && T->n_x == 3 && T->n_u == 2) {
