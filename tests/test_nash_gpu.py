@@ -241,3 +241,42 @@ def test_nash_solver_jacobi_mode_runs(cuda):
     assert len(hist) == 2 and all(np.isfinite(hist))
     assert all(np.allclose(x[:, 0], np.array(GAME[i][0])) and np.allclose(x[:, -1], np.array(GAME[i][1]))
                for i, x in enumerate(X))
+
+
+def test_si_nash_solver_trace_matches_reference_iteration(cuda):
+    """SI_NashSolver (si_nash_solver.py:43-124) on the SI default game, one outer iteration replayed:
+    each best response (no slab rows: the reference's update_intersample_constraints replaced them)
+    against the oracle on the same data, the Gauss-Seidel neighbour positions, the ACS stopping rule."""
+    from oracle import nash_ref, scp_problems as sp_
+    from SCvx.global_parameters import K
+    from SCvx.models.SI_multi_agent_model import SI_MultiAgentModel
+    from SCvx.models.game_si_model import GameSIModel
+    from SCvx.optimization.si_nash_solver import SI_NashSolver
+    _, sg = _cfg()
+    mam = SI_MultiAgentModel(sg.AGENT_PARAMS)
+    for i, p in enumerate(sg.AGENT_PARAMS):
+        mam.models[i] = GameSIModel(**{k: p[k] for k in ("r_init", "r_final", "obstacles", "robot_radius",
+                                                         "control_weight", "collision_weight", "collision_radius",
+                                                         "control_rate_weight", "curvature_weight")})
+    X0 = [sp_.straight(p["r_init"], p["r_final"], K).T for p in sg.AGENT_PARAMS]
+    U0 = [np.zeros((3, K)) for _ in sg.AGENT_PARAMS]
+    ns = SI_NashSolver(mam, max_iter=1, max_acs_iters=2)
+    ns.trace = []
+    X, U, hist = ns.solve(X0, U0, sigma_ref=12.0, show_progress=False)
+    assert len(hist) == 1 and np.isfinite(hist[0])
+    cur = [x.T.copy() for x in X0]
+    for i in range(3):
+        steps = [e for e in ns.trace if e["agent"] == i]
+        nbr = [j for j in range(3) if j != i]
+        assert 1 <= len(steps) <= 2
+        for e in steps:
+            np.testing.assert_array_equal(e["P"], np.stack([cur[j] for j in nbr]))
+            assert e["status"] in (0, 1)
+            cons = sp_.model_constraints("si", sg.AGENT_PARAMS[i]["r_init"], sg.AGENT_PARAMS[i]["r_final"],
+                                         obstacles=SI_OBS)
+            p = nash_ref.game_problem("si", e["Xref"], e["Uref"], 12.0, cons, SI_WTS, e["X_prev"], [], 1.0,
+                                      disc=_disc_stacks(e["disc"], 3, 3))
+            _check_against_oracle(p, e["X"], e["U"], e["nu"], 12.0, float(e["obj"]), SI_WTS["control_weight"])
+        cur[i] = steps[-1]["X"].copy()
+    for i in range(3):
+        np.testing.assert_array_equal(X[i], cur[i].T)
