@@ -64,10 +64,10 @@ int qp_check(const scvx_qp_template* T, int N, const ModelTable*& mt, int& cls) 
     return SCVX_OK;
 }
 
-size_t ws_bytes(const ModelTable& mt, int cls, int N) {
+size_t ws_bytes(const ModelTable& mt, int cls, int N, int K) {
     const int nb = mt.caps[3 * cls], no = mt.caps[3 * cls + 1], nc = mt.caps[3 * cls + 2];
     const int ns = no + nc, ng = no + (nc > 0 ? 1 : 0);
-    return sizeof(double) * (size_t)N * (size_t)qp_ws_doubles(mt.nx, mt.nu, nb, ns, ng);
+    return sizeof(double) * (size_t)N * (size_t)qp_ws_doubles(mt.nx, mt.nu, nb, ns, ng, K);
 }
 }  // namespace
 
@@ -86,7 +86,7 @@ extern "C" size_t scvx_qp_workspace_bytes(const scvx_qp_template* tpl, int N) {
     const ModelTable* mt = nullptr;
     int cls = -1;
     if (N <= 0 || qp_check(tpl, N, mt, cls) != SCVX_OK) return 0;
-    return ws_bytes(*mt, cls, N);
+    return ws_bytes(*mt, cls, N, tpl->K);
 }
 
 extern "C" int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const double* disc, const double* sigma,
@@ -104,7 +104,7 @@ extern "C" int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const d
         return set_error(SCVX_EINVAL, "qp: null buffer");
     if (tpl->has_final && !x_final) return set_error(SCVX_EINVAL, "qp: x_final required");
     if (tpl->j_max > 0 && (!coll_rows || !coll_count)) return set_error(SCVX_EINVAL, "qp: collision rows required");
-    const size_t need = ws_bytes(*mt, cls, N);
+    const size_t need = ws_bytes(*mt, cls, N, tpl->K);
     if (!workspace || workspace_bytes < need) return set_error(SCVX_EWORKSPACE, "qp: workspace too small");
     QPArgs a{};
     a.T = *tpl;

@@ -72,8 +72,11 @@ struct QPArgs {
 // ---- sizes shared by host (workspace / LDS bytes) and device
 constexpr int qp_dstr(int nx, int nu) { return nx * (nx + 2 * nu + 2); }
 constexpr int qp_pkt(int nx, int nu) { return 2 * nx * nx + 4 * nx * nu + nu * nu + nx; }
+// global (compact) packet: Q as its diagonal + the 3 off-diagonals of the position block, S, R upper
+// packed, e, A, Bt (column-major), C_{t-1} -- expanded to the LDS packet layout by the factor's prefetch
+constexpr int qp_gpk(int nx, int nu) { return (nx + 3) + nx * nu + nu * (nu + 1) / 2 + nx + nx * nx + 2 * nx * nu; }
 constexpr int qp_even(int x) { return (x + 1) & ~1; }
-// workspace columns (doubles x 64) of a capacity class
+// workspace columns (K doubles each: one per node) of a capacity class
 constexpr int qp_ncol(int nx, int nu, int nb, int ns, int ng) {
     // disc^T | Bt | soft rows | groups | rd | r1a | cP | ub | node state | SOC
     return qp_dstr(nx, nu) + nx * nu + 4 * ns + 4 * ng + (nx + nu) + ng + ((1 << nu) + 2 * nb + ns + ng) + nu +
@@ -82,9 +85,14 @@ constexpr int qp_ncol(int nx, int nu, int nb, int ns, int ng) {
 // factor outputs per stage (stage-major block): K, kappa, LD, W2, P, Pi, u, Acl, one junk slot (the
 // global store of lanes without an output of their own)
 constexpr int qp_fbs(int nx, int nu) { return 3 * nu * nx + nu * nu + 3 * nx * nx + nx + 1; }
-constexpr long long qp_ws_doubles(int nx, int nu, int nb, int ns, int ng) {
-    return (long long)qp_ncol(nx, nu, nb, ns, ng) * 64 + 64LL * qp_pkt(nx, nu) + 64LL * qp_fbs(nx, nu) + 64;
+// per agent: columns [c][K], packets [K][GPK], factor blocks [K][FBS] -- only the K nodes: lanes >= K
+// address past the end of the buffer (loads read 0, stores are dropped), so the agent's footprint is
+// what its nodes touch (C3: 1024 agents x 199 KB stay inside the 256 MB Infinity Cache)
+constexpr long long qp_ws_doubles(int nx, int nu, int nb, int ns, int ng, int K) {
+    return (long long)K * (qp_ncol(nx, nu, nb, ns, ng) + qp_gpk(nx, nu) + qp_fbs(nx, nu));
 }
+// byte offset of every access of a lane without a node (t >= K): beyond num_records of any workspace
+constexpr int QP_OOB = 0x40000000;
 
 template <int NX_, int NU_, int NB_, int NO_, int NC_>
 struct QPCfg {
@@ -102,6 +110,35 @@ struct QPCfg {
                          P_A = P_E + NX, P_BT = P_A + NX * NX, P_BTR = P_BT + NX * NU, P_C = P_BTR + NX * NU,
                          PKT = P_C + NX * NU;
     static_assert(PKT == qp_pkt(NX, NU), "packet size");
+    // global packet (compact; qp_gpk): Q diagonal | Q position-block off-diagonals (0,1) (0,2) (1,2) |
+    // S | R upper packed | e | A (column-major) | Bt (column-major) | C_{t-1} (column-major)
+    static constexpr int G_QD = 0, G_QO = G_QD + NX, G_S = G_QO + 3, G_R = G_S + NX * NU,
+                         G_E = G_R + NU * (NU + 1) / 2, G_A = G_E + NX, G_BT = G_A + NX * NX, G_C = G_BT + NX * NU,
+                         GPK = G_C + NX * NU;
+    static_assert(GPK == qp_gpk(NX, NU), "global packet size");
+    static_assert(NX >= 3, "the position block is 3 x 3");
+    // global packet element of LDS packet element e (-1: a structural zero)
+    static constexpr int gsrc(int e) {
+        if (e < P_S) {
+            const int i = e / NX, j = e % NX;
+            if (i == j) return G_QD + i;
+            if (i < 3 && j < 3) return G_QO + i + j - 1;  // (0,1) -> 0, (0,2) -> 1, (1,2) -> 2
+            return -1;
+        }
+        if (e < P_R) return G_S + (e - P_S);
+        if (e < P_E) {
+            const int i = (e - P_R) / NU, j = (e - P_R) % NU, p = i < j ? i : j, q = i < j ? j : i;
+            return G_R + p * NU - p * (p - 1) / 2 + (q - p);
+        }
+        if (e < P_A) return G_E + (e - P_E);
+        if (e < P_BT) return G_A + (e - P_A);
+        if (e < P_BTR) return G_BT + (e - P_BT);
+        if (e < P_C) {
+            const int i = (e - P_BTR) / NU, j = (e - P_BTR) % NU;
+            return G_BT + j * NX + i;
+        }
+        return G_C + (e - P_C);
+    }
     static_assert(NX <= 16, "the solve chains broadcast within one 16-lane row");
     // factor outputs: stage-major blocks [t][FBS] (coalesced stores from the element-parallel
     // factor; each lane-parallel pass reads its own stage's block)
@@ -159,12 +196,11 @@ __host__ __device__ constexpr int qp_dpk(int off, int) { return off; }
 // VGPR (voffset) and the column part as a (rematerialisable) SGPR constant (soffset), so no
 // per-column 64-bit address is ever materialised in vector registers.
 typedef unsigned int qp_u2 __attribute__((ext_vector_type(2)));
-// Every memory op of the factor sweep is unconditional: lanes with nothing to store write to a
-// per-lane sink block at the end of the agent's own workspace, and prefetch loads of padding
-// elements read a clamped in-bounds element.  A load or store under a divergent branch makes the
+// Every memory op of the factor sweep is unconditional: lanes with nothing to store write to the
+// junk slot of the stage block, and prefetch loads of padding / structurally zero packet elements
+// read past the end of the workspace (0).  A load or store under a divergent branch makes the
 // compiler's vmcnt accounting fall back to vmcnt(0), which drains the packet prefetches issued
 // stages ahead (measured: most of the factor's per-stage time).
-constexpr int QP_SINK_DOUBLES = 64;
 // solve-chain prefetch depth (stages of Acl / offsets held in registers ahead of the chain)
 constexpr int QP_CPF = 4;
 struct QPBuf {
@@ -278,19 +314,28 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     const double* disc = a.disc + agent * (long long)(K - 1) * C::DSTR;
     double* ws = a.ws + agent * a.ws_agent;
     QPBuf wb;
-    wb.rs = __builtin_amdgcn_make_buffer_rsrc(ws, (short)0, 0x7fffffff, 0x00020000);
-    const int vt = t * 8;  // this lane's element of a stage-minor column
-    constexpr int PKB = C::NCOL * WAVE * 8;  // byte offset of the packets [t][PKT]
-    constexpr int FBB = PKB + WAVE * PKT * 8;  // byte offset of the factor output blocks [t][FBS]
-    const int vpk = t * PKT * 8;
-    const int vfb = t * C::FBS * 8;
-    // Loads go through `vcur`, this lane's offset re-derived (opaquely) at the start of every
-    // phase: a load in one phase is then never merged with the same load of an earlier phase,
-    // which would keep the value live in registers across the sweeps in between.
-    int vcur = vt;
-    auto fresh = [&]() __attribute__((always_inline)) { vcur = qp_opaque(vt); };
-    auto cld = [&](int c) __attribute__((always_inline)) -> double { return wb.ld(vcur, c * WAVE * 8); };
-    auto cst = [&](int c, double v) __attribute__((always_inline)) { wb.st(vt, c * WAVE * 8, v); };
+    // num_records = the agent's workspace: the lanes without a node address QP_OOB (reads 0, stores dropped)
+    wb.rs = __builtin_amdgcn_make_buffer_rsrc(ws, (short)0, (int)(a.ws_agent * 8), 0x00020000);
+    const int colb = K * 8;      // bytes per workspace column (one double per node)
+    const int vt = act ? t * 8 : QP_OOB;  // this lane's element of a stage-minor column
+    const int PKB = C::NCOL * colb;       // byte offset of the packets [t][GPK]
+    const int FBB = PKB + K * C::GPK * 8;  // byte offset of the factor output blocks [t][FBS]
+    const int vpk = act ? t * C::GPK * 8 : QP_OOB;
+    const int vfb = act ? t * C::FBS * 8 : QP_OOB;
+    // Loads go through `vcur` / `vpcur`, this lane's offsets re-derived (opaquely) at the start of every
+    // phase: a load in one phase is then never merged with the same load of an earlier phase, which
+    // would keep the value live in registers across the sweeps in between.  The lane-parallel passes
+    // read columns (one coalesced line set per load); a lane's packet / factor block is contiguous per
+    // lane (64 lines per load), so those passes read them only where no column copy exists.
+    int vcur = vt, vpcur = vpk;
+    auto fresh = [&]() __attribute__((always_inline)) {
+        vcur = qp_opaque(vt);
+        vpcur = qp_opaque(vpk);
+    };
+    auto cld = [&](int c) __attribute__((always_inline)) -> double { return wb.ld(vcur, c * colb); };
+    auto cst = [&](int c, double v) __attribute__((always_inline)) { wb.st(vt, c * colb, v); };
+    // element g of this lane's (global) packet
+    auto pld = [&](int g) __attribute__((always_inline)) -> double { return wb.ld(vpcur, PKB + g * 8); };
     // Batched loads: ldn issues the loads of n consecutive columns, hold pins values in registers.
     // Issue every load of a phase first and hold them before the first use, so the phase pays one
     // memory round trip (the scheduler otherwise serialises load -> wait -> use under pressure).
@@ -348,13 +393,12 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                     for (int k = 0; k < NX; ++k) v = fma(Ad[k * NX + i], Cp[j * NX + k], v);
                     cst(C::C_BT + i * NU + j, v);
-                    pst(C::P_BT + j * NX + i, v);
-                    pst(C::P_BTR + i * NU + j, v);
+                    pst(C::G_BT + j * NX + i, v);
                 }
 #pragma unroll
-            for (int e = 0; e < NX * NX; ++e) pst(C::P_A + e, Ad[e]);
+            for (int e = 0; e < NX * NX; ++e) pst(C::G_A + e, Ad[e]);
 #pragma unroll
-            for (int e = 0; e < NX * NU; ++e) pst(C::P_C + e, Cp[e]);
+            for (int e = 0; e < NX * NU; ++e) pst(C::G_C + e, Cp[e]);
         }
         // soft rows: obstacle linearisations (single_integrator_model.py:113-126) from Xref, then
         // the caller's collision rows (dist_scvx_3d.py:93-107)
@@ -411,10 +455,10 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         if (lane < NX) { lds[V_YI + lane] = 0.0; lds[V_YF + lane] = 0.0; }
         if (lane < 16) lds[V_ST + lane] = 0.0;
     }
-    // C_{t-1} (column-major as disc) of this node, from the transposed disc at stage t-1
+    // C_{t-1} (column-major as disc) of this node, from the transposed disc of node t-1 (the lane below)
     auto load_cp = [&](double* Cp) __attribute__((always_inline)) {
 #pragma unroll
-        for (int e = 0; e < NX * NU; ++e) Cp[e] = wb.ld(vcur - 8, (C::C_DT + NX * NX + NX * NU + e) * WAVE * 8);
+        for (int e = 0; e < NX * NU; ++e) Cp[e] = wb.ld(vcur - 8, (C::C_DT + NX * NX + NX * NU + e) * colb);
         hold(Cp, NX * NU);
 #pragma unroll
         for (int e = 0; e < NX * NU; ++e) Cp[e] = (t > 0) ? Cp[e] : 0.0;
@@ -515,12 +559,17 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         // last read), loads issued 3 stages ahead (register buffers pf[0..2], so the stage loop is
         // unrolled by 3 to keep their indices static)
         double pf[3][PFN];
+        // lane's global packet element per prefetch slot (structural zeros read past the end: 0)
+        int pfo[PFN];
+#pragma unroll
+        for (int k = 0; k < PFN; ++k) {
+            const int e = qp_opaque(lane) + WAVE * k;
+            const int g = e < PKT ? C::gsrc(e) : -1;  // padding lanes read 0 (stored to the sink)
+            pfo[k] = g >= 0 ? g * 8 : QP_OOB;
+        }
         auto pf_load = [&](int ts, double* b) __attribute__((always_inline)) {
 #pragma unroll
-            for (int k = 0; k < PFN; ++k) {
-                const int e = lane + WAVE * k;
-                b[k] = wb.ld((e < PKT ? e : PKT - 1) * 8, PKB + (ts > 0 ? ts : 0) * PKT * 8);  // in bounds
-            }
+            for (int k = 0; k < PFN; ++k) b[k] = wb.ld(pfo[k], PKB + (ts > 0 ? ts : 0) * C::GPK * 8);
         };
         auto pf_store = [&](int ts, const double* b) __attribute__((always_inline)) {
 #pragma unroll
@@ -540,7 +589,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         auto stage = [&](int ts, double* nb, const double* cb) __attribute__((always_inline)) {
             const bool last = ts == K - 1;
             const double blast = last ? 1.0 : 0.0;
-            const int fbo = FBB + ts * C::FBS * 8;  // byte offset of this stage's output block
+            const int fbo = FBB + ts * C::FBS * 8;  // byte offset of this stage's output block (uniform)
             pf_load(ts - 3, nb);  // unconditional: stage K-1 re-issues K-4, ts-3 < 0 reads zeros
             // ---- phase 1: T1 = P'A, T2 = P'Bt, W1 = A'Pi', W2 = Bt'Pi', u = P'e, xe += Pi''e
             qp_phase<NX, R1>(lds, q1, blast, wb, fbo, a1);
@@ -870,7 +919,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             ldb(Pi, C::B_PI, NX * NX);
             ldn(Bt, C::C_BT, NX * NU);
 #pragma unroll
-            for (int i = 0; i < NX; ++i) ev[i] = wb.ld(vpk, PKB + (C::P_E + i) * 8);
+            for (int i = 0; i < NX; ++i) ev[i] = pld(C::G_E + i);
             hold(kap, NU * NX); hold(Pi, NX * NX); hold(Bt, NX * NU); hold(ev, NX);
 #pragma unroll
             for (int i = 0; i < NU; ++i)
@@ -1156,7 +1205,10 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 double v = (i == j) ? dbox[i] : 0.0;
                 if (i < 3 && j < 3) v += Hpp[i < 3 ? i : 0][j < 3 ? j : 0];
                 Q[i * NX + j] = v;
-                pst(C::P_Q + i * NX + j, v);
+                // global packet: the diagonal and the position block's upper off-diagonals (the factor
+                // reads the upper triangle; every other element is a structural zero)
+                if (i == j) pst(C::G_QD + i, v);
+                else if (i < j && j < 3) pst(C::G_QO + i + j - 1, v);
             }
         double Sx[NX * NU];
 #pragma unroll
@@ -1167,19 +1219,19 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                 for (int k = 0; k < NX; ++k) v = fma(Q[i * NX + k], Cp[j * NX + k], v);
                 Sx[i * NU + j] = v;
-                pst(C::P_S + i * NU + j, v);
+                pst(C::G_S + i * NU + j, v);
             }
 #pragma unroll
         for (int i = 0; i < NU; ++i)
 #pragma unroll
-            for (int j = 0; j < NU; ++j) {
+            for (int j = i; j < NU; ++j) {  // upper triangle, packed by rows
                 double v = Huu[i * NU + j];
 #pragma unroll
                 for (int k = 0; k < NX; ++k) v = fma(Cp[i * NX + k], Sx[k * NU + j], v);
-                pst(C::P_R + i * NU + j, v);
+                pst(C::G_R + i * NU - i * (i - 1) / 2 + (j - i), v);
             }
 #pragma unroll
-        for (int i = 0; i < NX; ++i) pst(C::P_E + i, (t < K - 1) ? -rp[i] : 0.0);
+        for (int i = 0; i < NX; ++i) pst(C::G_E + i, (t < K - 1) ? -rp[i] : 0.0);
     };
     // eliminate the group part of a Newton rhs (stores it for recover_aux): r1_p -= Hpa/Haa r1a;
     // returns the (xi, u) linear terms q, r of the node

@@ -1,0 +1,47 @@
+"""Diagnostic (CPU only): the C3 bench's SCvx steps (bench.py constants, per-agent trust-region rule)
+through the CPU restatements (oracle/foh_ref.c + oracle/scvx_cpu.cpp, the kernel's twin), printing the
+IPM-iteration histogram of every step.  Used to try IPM algorithm changes on the CPU twin before they
+go into qp_ipm.hpp (the kernel time is the slowest agent's iteration count x the per-iteration latency).
+usage: python tools/ipm_tail_cpu.py [steps] [N] [threads]"""
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "dynamic-programming-multiagent-trajectory-optimiziation_amd"))
+import bench  # noqa: E402
+from oracle import foh_oracle, qp_cpu  # noqa: E402
+from scvx_hip import workloads  # noqa: E402
+
+steps = int(sys.argv[1]) if len(sys.argv) > 1 else 6
+N = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+threads = int(sys.argv[3]) if len(sys.argv) > 3 else (os.cpu_count() or 1)
+K = bench.K
+sc = workloads.synthetic_di(N, K=K, seed=1, sigma=bench.SIGMA, obstacles=bench.N_OBS)
+tpl = qp_cpu.make_template(6, 3, K, box=bench.BOX, obs=sc["obs"], w_obs=1e6, u_max=bench.U_MAX, tol=1e-8, max_iter=60)
+X, U = sc["X"].copy(), sc["U"].copy()
+tr = np.full(N, bench.TR0)
+prev = np.full(N, np.inf)
+tot = []
+tot_cost = []
+for s in range(steps):
+    t0 = time.time()
+    disc = np.stack([np.hstack([o.T for o in foh_oracle.foh("di", X[a].T, U[a].T, sc["sigma"][a])]) for a in range(N)])
+    o = qp_cpu.solve_batched(tpl, disc, sc["sigma"], X, U, sc["x_init"], sc["x_final"], tr, nthreads=threads)
+    it, st = o["iters"] % 100, o["status"]
+    gz = o["iters"] // 100
+    cost = it + float(os.environ.get("GZ_COST", "0.25")) * gz
+    tot_cost.append(cost.max())
+    tot.append(it.max())
+    h = np.bincount(it)
+    print(f"step {s}: iters mean {it.mean():.2f} max {it.max()} hist(from 8) {h[8:].tolist()} "
+          f"status {np.bincount(st, minlength=3).tolist()} corr {gz.sum()} maxcost {cost.max():.2f} ({time.time() - t0:.1f} s)", flush=True)
+    ok = (st != 2)[:, None, None]
+    X, U = np.where(ok, o["X"], X), np.where(ok, o["U"], U)
+    cost = (U[:, :-1] ** 2).sum(axis=(1, 2))
+    tr = tr * np.where(cost > prev, 0.5, 1.0) * np.where(st == 2, 0.5, 1.0)
+    prev = cost
+print(f"sum of per-step max iterations: {sum(tot)} (mean {np.mean(tot):.2f}); mean max cost {np.mean(tot_cost):.2f}")
