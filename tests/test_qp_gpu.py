@@ -76,8 +76,8 @@ def test_c3_family_matches_cpu_and_dense(cuda, umax, nobs):
     cpu = qp_cpu.solve_batched(tpl, dn, sc["sigma"], sc["X"], sc["U"], sc["x_init"], sc["x_final"], tr)
     st = out["status"].cpu().numpy()
     ok = cpu["status"] == 0
-    assert ok.sum() >= N // 2
-    assert (st[ok] == 0).all()
+    assert ok.all(), cpu["status"]  # every agent of the family solves (tests/test_qp_twin_cpu.py: twin == dense)
+    assert (st == 0).all(), st
     Xg, Ug, og = out["X"].cpu().numpy(), out["U"].cpu().numpy(), out["obj"].cpu().numpy()
     for a in np.nonzero(ok)[0]:
         assert abs(og[a] - cpu["obj"][a]) <= 1e-8 * max(1.0, abs(cpu["obj"][a]))
