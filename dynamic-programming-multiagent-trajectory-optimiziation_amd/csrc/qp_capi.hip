@@ -102,7 +102,9 @@ extern "C" int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const d
     if (N == 0) return SCVX_OK;
     if (!disc || !sigma || !Xref || !Uref || !x_init || !tr || !X || !U || !slack_coll || !obj || !status || !iters)
         return set_error(SCVX_EINVAL, "qp: null buffer");
-    if (tpl->has_final && !x_final) return set_error(SCVX_EINVAL, "qp: x_final required");
+    if ((tpl->has_final || tpl->w_final > 0.0) && !x_final) return set_error(SCVX_EINVAL, "qp: x_final required");
+    if (tpl->w_final < 0.0 || (tpl->w_final > 0.0 && tpl->has_final))
+        return set_error(SCVX_EINVAL, "qp: w_final > 0 (soft terminal) needs has_final = 0");
     if (tpl->j_max > 0 && (!coll_rows || !coll_count)) return set_error(SCVX_EINVAL, "qp: collision rows required");
     const size_t need = ws_bytes(*mt, cls, N, tpl->K);
     if (!workspace || workspace_bytes < need) return set_error(SCVX_EWORKSPACE, "qp: workspace too small");

@@ -308,9 +308,17 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     double qnorm = 0.0;  // ||q||_inf: the linear objective weights of the slack groups
     if (nobs > 0) qnorm = fmax(qnorm, T.w_obs);
     if (has_coll) qnorm = fmax(qnorm, T.w_coll);
+    // soft terminal state (has_final = 0, w_final > 0): + w_final ||x_{K-1} - x_final||^2, linear term
+    // -2 w_final x_final at node K-1 (a build-side option for nonlinear models, no reference row)
+    const bool soft_fin = !fin && T.w_final > 0.0;
+    if (soft_fin) {
+        for (int i = 0; i < NX; ++i) qnorm = fmax(qnorm, 2.0 * T.w_final * fabs(a.x_final[agent * NX + i]));
+    }
     const double osc = fmax(1.0, qnorm), iosc = 1.0 / osc;
     const double wu = ((t < K - 1) ? 1.0 : T.w_last) * iosc;
     const bool fixed_u = act && (t == K - 1) && T.fix_last_input;
+    const bool tsoft = soft_fin && act && (t == K - 1);
+    const double wfs = tsoft ? T.w_final * iosc : 0.0;
     const double* disc = a.disc + agent * (long long)(K - 1) * C::DSTR;
     double* ws = a.ws + agent * a.ws_agent;
     QPBuf wb;
@@ -1147,7 +1155,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     auto assemble = [&](bool unit, const double* Wi2uu, const double* rp) __attribute__((always_inline)) {
         double dbox[NX], Hpp[3][3], Huu[NU * NU];
 #pragma unroll
-        for (int i = 0; i < NX; ++i) dbox[i] = 0.0;
+        for (int i = 0; i < NX; ++i) dbox[i] = 2.0 * wfs;
 #pragma unroll
         for (int i = 0; i < 3; ++i) Hpp[i][0] = Hpp[i][1] = Hpp[i][2] = 0.0;
 #pragma unroll
@@ -1372,7 +1380,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         assemble(true, Wu, rp);
         double r1[NZ], r1a[NGA];
 #pragma unroll
-        for (int i = 0; i < NX; ++i) r1[i] = 0.0;
+        for (int i = 0; i < NX; ++i) r1[i] = tsoft ? -2.0 * wfs * (z[i] - a.x_final[agent * NX + i]) : 0.0;
 #pragma unroll
         for (int j = 0; j < NU; ++j) r1[NX + j] = -2.0 * wu * z[NX + j] - (soc ? z[NX + j] : 0.0);
 #pragma unroll
@@ -1489,7 +1497,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             }
         }
 #pragma unroll
-        for (int i = 0; i < NX; ++i) rd[i] = 0.0;
+        for (int i = 0; i < NX; ++i) rd[i] = tsoft ? 2.0 * wfs * (z[i] - a.x_final[agent * NX + i]) : 0.0;
 #pragma unroll
         for (int j = 0; j < NU; ++j) rd[NX + j] = 2.0 * wu * z[NX + j];
 #pragma unroll
@@ -1568,6 +1576,10 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 }
 #pragma unroll
                 for (int j = 0; j < NU; ++j) pobj += wu * z[NX + j] * z[NX + j];
+                if (tsoft) {  // the objective without its constant w_final ||x_final||^2 (Clarabel's)
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) pobj += wfs * z[i] * (z[i] - 2.0 * a.x_final[agent * NX + i]);
+                }
             }
         }
         pres = wave_max(pres); dres = wave_max(dres);
@@ -1904,6 +1916,13 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         for (int j = 0; j < NU; ++j) { a.U[(agent * K + t) * NU + j] = z[NX + j]; pobj += wu * z[NX + j] * z[NX + j]; }
 #pragma unroll
         for (int g = 0; g < NG; ++g) pobj += grp_on(g) ? gweight(g) * av[g] : 0.0;
+        if (tsoft) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                const double e = z[i] - a.x_final[agent * NX + i];
+                pobj += wfs * e * e;
+            }
+        }
         a.slack_coll[agent * K + t] = (has_coll && ineq) ? av[NG > 0 ? NG - 1 : 0] : 0.0;
     }
     pobj = wave_sum(pobj);

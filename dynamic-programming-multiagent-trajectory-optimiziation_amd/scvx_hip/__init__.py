@@ -173,9 +173,15 @@ class QPSpec:
     # relative stopping tolerance (primal / dual residual and gap); 1e-8 is Clarabel's default
     # (tol_feas = tol_gap_rel = tol_gap_abs = 1e-8), the solver dist_scvx_3d.py:110 calls
     tol: float = 1e-8
+    # soft terminal state (build-side option for nonlinear models; the reference's subproblem has the
+    # hard row d_{T-1} + x_{T-1} == x_des): with has_final=False and w_final > 0 the objective gains
+    # w_final ||x_{K-1} - x_final||^2, so the subproblem stays feasible whatever the linearisation
+    w_final: float = 0.0
 
     def to_c(self):
         n, m = MODEL_DIMS[self.model]
+        if self.w_final < 0 or (self.w_final > 0 and self.has_final):
+            raise ValueError("QPSpec: w_final > 0 (soft terminal) needs has_final=False")
         t = QPTemplate()
         t.model_id, t.n_x, t.n_u, t.K, t.pos_dim = MODEL_IDS[self.model], n, m, self.K, self.pos_dim
         t.has_final, t.fix_last_input, t.ineq_last = int(self.has_final), int(self.fix_last_input), int(self.ineq_last)
@@ -194,6 +200,7 @@ class QPSpec:
         t.has_soc = int(self.u_max is not None)
         t.u_max = 0.0 if self.u_max is None else float(self.u_max)
         t.max_iter, t.tol = int(self.max_iter), float(self.tol)
+        t.w_final = float(self.w_final)
         return t
 
 
@@ -226,7 +233,7 @@ class QPSolver:
         want = {"disc": (disc, (N, K - 1, disc_stride(spec.model))), "sigma": (sigma, (N,)),
                 "Xref": (Xref, (N, K, n)), "Uref": (Uref, (N, K, m)), "x_init": (x_init, (N, n)),
                 "tr": (tr, (N,))}
-        if spec.has_final:
+        if spec.has_final or spec.w_final > 0:
             if x_final is None:
                 raise ValueError("QPSolver.solve: the template has a terminal condition; x_final is required")
             want["x_final"] = (x_final, (N, n))

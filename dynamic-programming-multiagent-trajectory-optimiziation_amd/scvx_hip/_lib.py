@@ -38,7 +38,7 @@ class QPTemplate(ctypes.Structure):
         ("obs_center", (ctypes.c_double * 3) * SCVX_MAX_OBS), ("obs_radius", ctypes.c_double * SCVX_MAX_OBS),
         ("w_obs", ctypes.c_double), ("j_max", ctypes.c_int32), ("w_coll", ctypes.c_double),
         ("has_soc", ctypes.c_int32), ("u_max", ctypes.c_double), ("max_iter", ctypes.c_int32),
-        ("tol", ctypes.c_double),
+        ("tol", ctypes.c_double), ("w_final", ctypes.c_double),
     ]
 
 

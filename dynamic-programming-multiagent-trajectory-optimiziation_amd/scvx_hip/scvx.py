@@ -52,13 +52,17 @@ class CouplingSpec:
 class JacobiSCvx:
     """Device-resident Jacobi SCvx for this rank's agents [i0, i0 + N_local) of N_total.
 
+    on_fail: what a failed subproblem (status 2) does to its agent's trust radius -- "halve" (the
+             default) or "grow" (x2, at most tr_max, default tr0: an infeasible trust-region subproblem is the trust
+             region being too small to reach x_final, the usual SCP remedy; for nonlinear models).
     tr_rule: "global" -- one trust region for all agents, halved when the total cost rises
              (dist_scvx_3d.py:248-252); "per_agent" -- the same rule applied to each agent's own
              cost (independent agents, configs C2/C3).
     """
 
     def __init__(self, spec: QPSpec, x_init, x_final, sigma, tr0: float, coupling: Optional[CouplingSpec] = None,
-                 tr_rule: str = "per_agent", group=None, nsub: Optional[int] = None, backend=None):
+                 tr_rule: str = "per_agent", group=None, nsub: Optional[int] = None, backend=None,
+                 on_fail: str = "halve", tr_max: Optional[float] = None):
         import torch
         self.torch = torch
         self.backend = backend or HipBackend()
@@ -68,6 +72,9 @@ class JacobiSCvx:
         self.x_init, self.x_final, self.sigma = x_init, x_final, sigma
         self.coupling = coupling
         self.tr_rule = tr_rule
+        if on_fail not in ("halve", "grow"):
+            raise ValueError(f"on_fail must be 'halve' or 'grow', not {on_fail!r}")
+        self.on_fail, self.tr_max = on_fail, float(tr0 if tr_max is None else tr_max)
         self.group = group
         self.nsub = nsub or DEFAULT_NSUB[spec.model]
         self.solver = self.backend.qp_solver(spec, self.N, self.device)
@@ -182,6 +189,9 @@ class JacobiSCvx:
             shrink = (cost > self.prev_cost).to(torch.float64)
             self.tr.mul_(1.0 - 0.5 * shrink)
             self.prev_cost.copy_(cost)
-        self.tr.mul_(1.0 - 0.5 * failed.to(torch.float64))
+        if self.on_fail == "grow":
+            self.tr.mul_(1.0 + failed.to(torch.float64)).clamp_(max=self.tr_max)
+        else:
+            self.tr.mul_(1.0 - 0.5 * failed.to(torch.float64))
         self._mark(marks, "update")
         return Xn, Un, out

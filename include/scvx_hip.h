@@ -111,12 +111,13 @@ typedef struct scvx_qp_template {
     double u_max;
     int32_t max_iter;
     double tol;
+    double w_final;         /* has_final = 0 and w_final > 0: soft terminal w_final ||x_{K-1} - x_final||^2 */
 } scvx_qp_template;
 
 /*
  * Inputs (device, agent-major):
  *   disc [N][K-1][n(n+2m+2)], sigma [N], Xref [N][K][n], Uref [N][K][m], x_init [N][n],
- *   x_final [N][n] (ignored unless has_final), tr [N],
+ *   x_final [N][n] (ignored unless has_final or w_final > 0), tr [N],
  *   coll_rows [N][K][j_max][pos_dim+1] rows (g, b), coll_count [N][K] (both ignored if j_max=0)
  * Outputs (device):
  *   X [N][K][n], U [N][K][m], slack_coll [N][K] (S_t, zeros if j_max = 0), obj [N],

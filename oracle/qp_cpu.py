@@ -20,13 +20,13 @@ class QPTemplate(ctypes.Structure):
         ("obs_center", (ctypes.c_double * 3) * MAX_OBS), ("obs_radius", ctypes.c_double * MAX_OBS),
         ("w_obs", ctypes.c_double), ("j_max", ctypes.c_int32), ("w_coll", ctypes.c_double),
         ("has_soc", ctypes.c_int32), ("u_max", ctypes.c_double), ("max_iter", ctypes.c_int32),
-        ("tol", ctypes.c_double),
+        ("tol", ctypes.c_double), ("w_final", ctypes.c_double),
     ]
 
 
 def make_template(n, m, K, pos_dim=3, has_final=True, fix_last_input=True, ineq_last=False, w_last=0.0,
                   box=(), obs=(), w_obs=1e6, j_max=0, w_coll=1e4, u_max=None, max_iter=60, tol=1e-9,
-                  model_id=0):
+                  model_id=0, w_final=0.0):
     t = QPTemplate()
     t.model_id, t.n_x, t.n_u, t.K, t.pos_dim = model_id, n, m, K, pos_dim
     t.has_final, t.fix_last_input, t.ineq_last, t.w_last = int(has_final), int(fix_last_input), int(ineq_last), w_last
@@ -42,6 +42,7 @@ def make_template(n, m, K, pos_dim=3, has_final=True, fix_last_input=True, ineq_
     t.has_soc = int(u_max is not None)
     t.u_max = 0.0 if u_max is None else u_max
     t.max_iter, t.tol = max_iter, tol
+    t.w_final = w_final
     return t
 
 

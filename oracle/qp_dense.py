@@ -232,6 +232,8 @@ def build_agent_problem(prob):
            a_t = (pbar_t - c)/(||pbar_t - c|| + 1e-6)  (single_integrator_model.py:113-126)
       umax or None                       -- ||u_t + w_t||_2 <= umax  (single_integrator_model.py:103-104)
       w_last                             -- weight on ||u_{T-1}+w_{T-1}||^2 (0 in dist_scvx_3d: unused row)
+      w_final                            -- > 0: soft terminal w_final ||x_{T-1} + d_{T-1} - x_final||^2 in
+                                            place of the row (:74) (build-side option, QPSpec.w_final)
       fix_last_input (bool)              -- pin w_{T-1} = 0 (dist_scvx_3d leaves it free & unused)
       pos_dim (3)
     Returns (P, q, A, b, G, h, dims, index dict).
@@ -278,6 +280,11 @@ def build_agent_problem(prob):
         for j in range(m):
             P[vw(t, j), vw(t, j)] += 2.0 * wt
             q[vw(t, j)] += 2.0 * wt * Ur[t, j]
+    w_final = prob.get("w_final", 0.0)
+    if w_final > 0:
+        for i in range(n):
+            P[vd(K - 1, i), vd(K - 1, i)] += 2.0 * w_final
+            q[vd(K - 1, i)] += 2.0 * w_final * (Xr[K - 1, i] - prob["x_final"][i])
     if has_coll:
         q[idx["S"][0]:idx["S"][1]] = prob["w_coll"]
     if obs:
@@ -292,7 +299,7 @@ def build_agent_problem(prob):
 
     for i in range(n):                       # d_0 == 0            (:73)
         r = eqrow(); r[vd(0, i)] = 1.0; beq.append(0.0)
-    if prob.get("x_final") is not None:      # d_{T-1} + x_{T-1} == x_des   (:74)
+    if prob.get("x_final") is not None and not w_final > 0:   # d_{T-1} + x_{T-1} == x_des   (:74)
         for i in range(n):
             r = eqrow(); r[vd(K - 1, i)] = 1.0; beq.append(prob["x_final"][i] - Xr[K - 1, i])
     for t in range(K - 1):                   # x_{t+1}+d_{t+1} == A(x_t+d_t) + B(u_t+w_t) [+C(..)+c]  (:80-83)
@@ -380,6 +387,8 @@ def solve_agent(prob, **kw):
     Ur = prob["Uref"]
     w_last = prob.get("w_last", 0.0)
     obj += np.sum(Ur[:-1] ** 2) + w_last * np.sum(Ur[-1] ** 2)
+    if prob.get("w_final", 0.0) > 0:
+        obj += prob["w_final"] * np.sum((prob["Xref"][-1] - prob["x_final"]) ** 2)
     info = dict(status=sol["status"], iters=sol["iters"], cert=kkt_certificate(P, q, A, b, G, h, dims, sol))
     if "S" in idx:
         info["S"] = x[idx["S"][0]:idx["S"][1]]
@@ -396,7 +405,7 @@ def constraint_violation(prob, X, U, S=None):
     d, w = X - Xr, U - Ur
     viol = {}
     viol["init"] = np.abs(d[0]).max()
-    if prob.get("x_final") is not None:
+    if prob.get("x_final") is not None and not prob.get("w_final", 0.0) > 0:
         viol["final"] = np.abs(X[K - 1] - prob["x_final"]).max()
     dyn = 0.0
     for t in range(K - 1):

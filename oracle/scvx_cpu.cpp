@@ -254,7 +254,7 @@ static void setup_agent(Agent& ag, const scvx_qp_template* T, const double* disc
     }
     ag.x_init.assign(x_init, x_init + n);
     ag.x_final.assign(n, 0.0);
-    if (T->has_final) ag.x_final.assign(x_final, x_final + n);
+    if (T->has_final || T->w_final > 0.0) ag.x_final.assign(x_final, x_final + n);
     ag.nd.assign(K, Node());
     const bool coll = T->j_max > 0;
     for (int t = 0; t < K; ++t) {
@@ -266,6 +266,9 @@ static void setup_agent(Agent& ag, const scvx_qp_template* T, const double* disc
         N.pdiag.assign(N.nv, 0.0);
         double wu = (t < K - 1) ? 1.0 : T->w_last;
         for (int j = 0; j < m; ++j) N.pdiag[n + j] = 2.0 * wu;
+        if (t == K - 1 && !T->has_final && T->w_final > 0.0) {  // soft terminal (kernel: tsoft)
+            for (int i = 0; i < n; ++i) { N.pdiag[i] = 2.0 * T->w_final; N.q[i] = -2.0 * T->w_final * ag.x_final[i]; }
+        }
         N.fixed_u = (t == K - 1) && T->fix_last_input;
         std::vector<Vec> rows;
         Vec hs;
@@ -1022,6 +1025,8 @@ done:
             pobj += 0.5 * ag.nd[t].pdiag[j] * zj * zj + ag.nd[t].q[j] * zj;
         }
     obj_out = pobj * osc;
+    if (!ag.T->has_final && ag.T->w_final > 0.0)  // the soft terminal's constant w_final ||x_final||^2
+        for (int i = 0; i < n; ++i) obj_out += ag.T->w_final * ag.x_final[i] * ag.x_final[i];
     iters_out = it;
     return status;
 }
@@ -1042,7 +1047,7 @@ extern "C" int oracle_qp_solve_batched(const scvx_qp_template* tpl, int N, const
         const double* cr = tpl->j_max > 0 ? coll_rows + (size_t)a * K * tpl->j_max * (pd + 1) : nullptr;
         const int32_t* cc = tpl->j_max > 0 ? coll_count + (size_t)a * K : nullptr;
         setup_agent(ag, tpl, disc + a * stride, sigma[a], Xref + (size_t)a * K * n, Uref + (size_t)a * K * m,
-                    x_init + (size_t)a * n, tpl->has_final ? x_final + (size_t)a * n : nullptr, tr[a], cr, cc);
+                    x_init + (size_t)a * n, (tpl->has_final || tpl->w_final > 0.0) ? x_final + (size_t)a * n : nullptr, tr[a], cr, cc);
         int it = 0;
         double ob = 0.0;
         status[a] = solve_agent(ag, it, ob);

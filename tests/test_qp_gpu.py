@@ -211,3 +211,40 @@ def test_unicycle_and_si_classes_match_cpu_and_dense(cuda, model):
     assert info["status"] == "optimal"
     assert abs(og[i] - objd) <= 1e-7 * max(1.0, abs(objd))
     assert max(qd.constraint_violation(prob, Xg[i], out["U"].cpu().numpy()[i]).values()) < 1e-7
+
+
+def test_soft_terminal_matches_twin_and_dense(cuda):
+    """QPSpec.w_final (soft terminal, has_final=False): the kernel equals the CPU twin on every agent of
+    a 64-agent C3-family batch and the dense reference form (x_final row replaced by the penalty) on a
+    sample; tolerances as above."""
+    N, K, wf = 64, 50, 50.0
+    sc = pb.synthetic_di(N, K=K, seed=4, obstacles=8)
+    box = [(0, -12, 12), (1, -12, 12)]
+    import torch
+    X, U, sig = _t(sc["X"], cuda), _t(sc["U"], cuda), _t(sc["sigma"], cuda)
+    disc = scvx_hip.foh_batched("di", X, U, sig)
+    tr = np.full(N, 0.25)
+    spec = scvx_hip.QPSpec(model="di", K=K, box=box, obs=sc["obs"], w_obs=1e6, u_max=1.0, has_final=False,
+                           w_final=wf, tol=1e-10, max_iter=80)
+    out = scvx_hip.qp_solve_batched(spec, disc, sig, X, U, _t(sc["x_init"], cuda), _t(sc["x_final"], cuda),
+                                    _t(tr, cuda))
+    st = out["status"].cpu().numpy()
+    assert (st == 0).all(), np.bincount(st, minlength=3)
+    dn = disc.cpu().numpy()
+    tpl = qp_cpu.make_template(6, 3, K, has_final=False, w_final=wf, box=box, obs=sc["obs"], w_obs=1e6, u_max=1.0,
+                               tol=1e-10, max_iter=80)
+    cpu = qp_cpu.solve_batched(tpl, dn, sc["sigma"], sc["X"], sc["U"], sc["x_init"], sc["x_final"], tr, nthreads=8)
+    assert (cpu["status"] == 0).all()
+    Xg, Ug = out["X"].cpu().numpy(), out["U"].cpu().numpy()
+    assert np.abs(Xg - cpu["X"]).max() < 1e-6
+    assert np.abs(Ug[:, :-1] - cpu["U"][:, :-1]).max() < 1e-6
+    for a in (0, 17):
+        A, B, C, S, z = pb.unpack_disc(dn[a], 6, 3)
+        prob = dict(A=A, B=B, C=C, c=S * sc["sigma"][a] + z, Xref=sc["X"][a], Uref=sc["U"][a],
+                    x_final=sc["x_final"][a], w_final=wf, tr=0.25, box=box, obs=sc["obs"], w_obs=1e6, umax=1.0,
+                    fix_last_input=True)
+        with np.errstate(all="ignore"):
+            Xd, Ud, objd, info = qd.solve_agent(prob, tol=1e-11, maxit=150)
+        assert info["status"] == "optimal"
+        assert np.abs(Xg[a] - Xd).max() < 1e-6 and np.abs(Ug[a][:-1] - Ud[:-1]).max() < 1e-6
+        assert abs(out["obj"][a].item() - objd) <= 1e-6 * max(1.0, abs(objd))

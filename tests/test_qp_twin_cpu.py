@@ -50,3 +50,26 @@ def test_twin_matches_dense_oracle_on_every_c3_agent(umax, nobs, agents):
                     x_final=sc["x_final"][a], tr=0.25, box=BOX, obs=sc["obs"], w_obs=1e6, umax=umax,
                     fix_last_input=True)
         _check_agent(prob, cpu, a)
+
+
+def test_twin_soft_terminal_matches_dense_oracle():
+    """QPSpec.w_final (soft terminal, the build's option for nonlinear models): has_final = 0 and
+    w_final ||x_{K-1} - x_final||^2 in the objective, on the twin and on the dense form (no x_final
+    row there either); the objective includes the constant w_final ||x_final||^2 in both."""
+    N, K, wf = 3, 50, 50.0
+    sc = pb.synthetic_di(N, K=K, seed=4, obstacles=8)
+    disc = _disc(sc, "di", N)
+    tr = np.full(N, 0.25)
+    tpl = qp_cpu.make_template(6, 3, K, has_final=False, w_final=wf, box=BOX, obs=sc["obs"], w_obs=1e6, u_max=1.0,
+                               tol=1e-12, max_iter=80)   # 1e-12: the 1e6-weighted obstacle slacks move the
+    #                                                         objective by ~1e-7 at 1e-10 (agent 1)
+    cpu = qp_cpu.solve_batched(tpl, disc, sc["sigma"], sc["X"], sc["U"], sc["x_init"], sc["x_final"], tr)
+    assert (cpu["status"] == 0).all(), cpu["status"]
+    for a in range(N):
+        A, B, C, S, z = pb.unpack_disc(disc[a], 6, 3)
+        prob = dict(A=A, B=B, C=C, c=S * sc["sigma"][a] + z, Xref=sc["X"][a], Uref=sc["U"][a],
+                    x_final=sc["x_final"][a], w_final=wf, tr=0.25, box=BOX, obs=sc["obs"], w_obs=1e6, umax=1.0,
+                    fix_last_input=True)
+        _check_agent(prob, cpu, a)
+        # the terminal state is pulled towards x_final but not pinned to it
+        assert np.abs(cpu["X"][a][-1] - sc["x_final"][a]).max() > 1e-6

@@ -87,10 +87,14 @@ def run(cfg="c5", iters=7):
     sc, w, cfgd = bench.make_coupled(cfg, 1, 0, dev)
     model = cfgd["model"]
     n, m = scvx_hip.MODEL_DIMS[model]
+    wf = float(os.environ.get("WF", 0))
     spec = scvx_hip.QPSpec(model=model, K=bench.K, box=cfgd["box"], obs=cfgd["obs"], w_obs=1e6,
-                           j_max=cfgd["j_max"], w_coll=1e4, max_iter=60)
-    drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], bench.TR0, coupling=CouplingSpec(R=cfgd["R"]),
-                     tr_rule="global")
+                           j_max=cfgd["j_max"], w_coll=1e4, max_iter=60, has_final=wf <= 0, w_final=wf)
+    drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], bench.TR0,
+                     coupling=CouplingSpec(R=cfgd["R"], check=os.environ.get("CHECK", "1") == "1",
+                                           j_max_hi=int(os.environ.get("JHI", 32))),
+                     tr_rule="global", on_fail=os.environ.get("ONFAIL", "halve"),
+                     tr_max=float(os.environ.get("TRMAX", bench.TR0)))
     X, U = w["X"].clone(), w["U"].clone()
     codes = torch.zeros(X.shape[0], dtype=torch.float64, device=dev)
     for it in range(int(iters)):
@@ -103,7 +107,8 @@ def run(cfg="c5", iters=7):
         cd = codes.cpu().numpy().astype(int)
         print(f"iter {it}: tr {trp.min().item():.4g}..{trp.max().item():.4g} status {np.bincount(st, minlength=3)} exit codes "
               f"{dict(zip(*np.unique(cd[st == 2], return_counts=True)))} iters mean {o['iters'].float().mean().item():.1f} "
-              f"check {drv.last_check}", flush=True)
+              f"check {drv.last_check} terminal err max {(Xn[:, -1] - w['x_final']).abs().max().item():.3e} "
+              f"cost {(Un[:, :-1] ** 2).sum().item():.6e}", flush=True)
         bad = np.nonzero(st == 2)[0]
         if it == int(iters) - 1 and bad.size:
             a = int(bad[0])
