@@ -14,7 +14,8 @@ xi, xf = torch.tensor(sc["x_init"], device=d), torch.tensor(sc["x_final"], devic
 tr = torch.full((N,), 0.25, dtype=torch.float64, device=d)
 spec = scvx_hip.QPSpec(model="di", K=K, box=[(0,-12,12),(1,-12,12)], obs=sc["obs"] if NOBS else (), u_max=1.0 if os.environ.get("SOC", "1") == "1" else None, max_iter=60)
 solver = scvx_hip.QPSolver(spec, N)
-for rep in range(3):
+qp_ms = []
+for rep in range(int(os.environ.get("REPS", "3"))):
     torch.cuda.synchronize(); t0 = time.time()
     disc = scvx_hip.foh_batched("di", X, U, sig)
     torch.cuda.synchronize(); t1 = time.time()
@@ -22,6 +23,9 @@ for rep in range(3):
     torch.cuda.synchronize(); t2 = time.time()
     st = out["status"].cpu().numpy(); it = out["iters"].cpu().numpy()
     print(f"N={N} foh {1e3*(t1-t0):.3f} ms  qp {1e3*(t2-t1):.3f} ms  status {np.bincount(st, minlength=3)}  iters mean {it.mean():.1f} max {it.max()}", flush=True)
+    qp_ms.append(1e3 * (t2 - t1))
+if len(qp_ms) > 3:
+    print(f"qp median {np.median(qp_ms[1:]):.3f} ms  min {min(qp_ms[1:]):.3f} ms over {len(qp_ms) - 1} reps", flush=True)
 if os.environ.get("TRACE"):
     import ctypes
     buf = torch.zeros(8 * 80 + 20, dtype=torch.float64, device=d)
