@@ -31,6 +31,14 @@
 namespace scvx {
 
 constexpr int COLL_TJ = 512;  // neighbours staged per LDS tile
+constexpr int COLL_CH = 8;    // neighbours per branch-free chunk of the scans
+
+// |p_i - p_j|^2 summed in coordinate order (d0^2 + d1^2) + d2^2, the rounding of the sequential
+// scan the selection and the check were pinned with
+__device__ __forceinline__ double coll_d2(const double* pi, const double* pj, int pd) {
+    const double d0 = pi[0] - pj[0], d1 = pd > 1 ? pi[1] - pj[1] : 0.0, d2 = pd > 2 ? pi[2] - pj[2] : 0.0;
+    return fma(d2, d2, fma(d1, d1, d0 * d0));
+}
 
 template <int JM>
 __global__ __launch_bounds__(64) void collision_rows_kernel(int K, int pd, int nx, int N_total, int N_local,
@@ -68,30 +76,39 @@ __global__ __launch_bounds__(64) void collision_rows_kernel(int K, int pd, int n
         }
         __syncthreads();
         if (!live) continue;
-#pragma unroll 4
-        for (int jj = 0; jj < nt; ++jj) {
-            const long long j = j0 + jj;
-            double d2 = 0.0;
-            for (int d = 0; d < pd; ++d) {
-                const double df = pi[d] - tile[jj * 3 + d];
-                d2 += df * df;
-            }
-            if (j == gi || (cull2 > 0 && !(d2 < cull2))) continue;
-            int slot;
-            if (n < j_max) {
-                slot = n++;
-            } else {
-                if (!(d2 < worst_d2)) continue;
-                slot = worst;
-            }
+        for (int jb = 0; jb < nt; jb += COLL_CH) {
+            // squared distances of a chunk of neighbours, branch-free (independent LDS broadcasts and
+            // FMAs); the sequential insertion below runs only if some lane of the wave may keep one
+            double d2v[COLL_CH];
+            bool need = n < j_max;
 #pragma unroll
-            for (int k = 0; k < JM; ++k)
-                if (k == slot) { kd[k] = d2; kj[k] = (int)j; }
-            if (n == j_max) {  // recompute the eviction candidate (first maximum, as a sequential scan)
-                worst_d2 = -1.0;
+            for (int c = 0; c < COLL_CH; ++c) {
+                const int jj = min(jb + c, nt - 1);
+                d2v[c] = coll_d2(pi, tile + jj * 3, pd);
+                need |= (jb + c < nt) && d2v[c] < worst_d2;
+            }
+            if (!__builtin_amdgcn_ballot_w64(need)) continue;
+#pragma unroll
+            for (int c = 0; c < COLL_CH; ++c) {
+                const long long j = j0 + jb + c;
+                const double d2 = d2v[c];
+                if (jb + c >= nt || j == gi || (cull2 > 0 && !(d2 < cull2))) continue;
+                int slot;
+                if (n < j_max) {
+                    slot = n++;
+                } else {
+                    if (!(d2 < worst_d2)) continue;
+                    slot = worst;
+                }
 #pragma unroll
                 for (int k = 0; k < JM; ++k)
-                    if (k < j_max && kd[k] > worst_d2) { worst_d2 = kd[k]; worst = k; }
+                    if (k == slot) { kd[k] = d2; kj[k] = (int)j; }
+                if (n == j_max) {  // recompute the eviction candidate (first maximum, as a sequential scan)
+                    worst_d2 = -1.0;
+#pragma unroll
+                    for (int k = 0; k < JM; ++k)
+                        if (k < j_max && kd[k] > worst_d2) { worst_d2 = kd[k]; worst = k; }
+                }
             }
         }
     }
@@ -124,6 +141,10 @@ __global__ __launch_bounds__(64) void collision_rows_kernel(int K, int pd, int n
 // position of local agent i and S_t its solved shared slack.  Same mapping as collision_rows_kernel
 // (workgroup = (node t, 64 local agents), neighbour positions staged in LDS).  Per (agent, node):
 // the number of rows violated by more than tol and the largest violation.
+// Bound skip: by Cauchy-Schwarz |g'dp| <= |dp|, so a row's value is at most 2R + |dp| - S - ||pbar_i -
+// pbar_j||.  A neighbour whose squared distance is at least (2R + |dp| - S - m)^2, m = min(largest value
+// so far, tol), can neither be counted nor raise the maximum, and its sqrt / division are skipped
+// (both outputs stay exact; coincident agents still give NaN).
 __global__ __launch_bounds__(64) void collision_check_kernel(int K, int pd, int nx, int N_total, int N_local,
                                                              const double* __restrict__ X_all, int i0, double R,
                                                              const double* __restrict__ X_new,
@@ -150,6 +171,8 @@ __global__ __launch_bounds__(64) void collision_check_kernel(int K, int pd, int 
     int nv = 0;
     double worst = -1e300;
     const double rr = 2.0 * R;
+    const double ndp = sqrt(dp[0] * dp[0] + dp[1] * dp[1] + dp[2] * dp[2]);
+    double skip2 = 1e300;  // skip the exact row when d2 >= skip2 (none before the first row)
     for (int j0 = 0; j0 < N_total; j0 += COLL_TJ) {
         const int nt = min(COLL_TJ, N_total - j0);
         __syncthreads();
@@ -159,19 +182,30 @@ __global__ __launch_bounds__(64) void collision_check_kernel(int K, int pd, int 
         }
         __syncthreads();
         if (!live) continue;
-#pragma unroll 4
-        for (int jj = 0; jj < nt; ++jj) {
-            if (j0 + jj == gi) continue;
-            double d2 = 0.0, gd = 0.0;
-            for (int d = 0; d < pd; ++d) {
-                const double df = pi[d] - tile[jj * 3 + d];
-                d2 += df * df;
-                gd += df * dp[d];
+        for (int jb = 0; jb < nt; jb += COLL_CH) {
+            double d2v[COLL_CH];
+            bool need = false;
+#pragma unroll
+            for (int c = 0; c < COLL_CH; ++c) {
+                const int jj = min(jb + c, nt - 1);
+                d2v[c] = coll_d2(pi, tile + jj * 3, pd);
+                need |= (jb + c < nt) && d2v[c] < skip2;
             }
-            const double nr = sqrt(d2);
-            const double v = (rr - nr) - gd / nr - S;  // NaN for coincident agents, as the reference's 0/0
-            worst = (v > worst || v != v) ? v : worst;
-            nv += (v > tol || v != v) ? 1 : 0;
+            if (!__builtin_amdgcn_ballot_w64(need)) continue;
+#pragma unroll
+            for (int c = 0; c < COLL_CH; ++c) {
+                const int jj = jb + c;
+                if (jj >= nt || j0 + jj == gi || !(d2v[c] < skip2)) continue;
+                double gd = 0.0;
+                for (int d = 0; d < pd; ++d) gd += (pi[d] - tile[jj * 3 + d]) * dp[d];
+                const double nr = sqrt(d2v[c]);
+                const double v = (rr - nr) - gd / nr - S;  // NaN for coincident agents, as the reference's 0/0
+                worst = (v > worst || v != v) ? v : worst;
+                nv += (v > tol || v != v) ? 1 : 0;
+                // fmin ignores a NaN maximum: the count threshold tol still bounds the skip
+                const double cb = (rr + ndp - S - fmin(worst, tol)) * (1.0 + 1e-12) + 1e-12;
+                skip2 = cb > 0.0 ? cb * cb : 1e-300;  // cb <= 0: every row but a coincident one (d2 = 0) skips
+            }
         }
     }
     if (!live) return;

@@ -232,3 +232,32 @@ def test_iteration_cap_far_from_optimum_is_a_failure(cuda):
     full = scvx_hip.qp_solve_batched(scvx_hip.QPSpec(model="di", K=K, box=box, obs=sc["obs"], u_max=1.0,
                                                      max_iter=60), *args)
     assert (full["status"].cpu().numpy() == 0).all()
+
+
+def test_collision_check_kernel_exact_on_every_row(cuda):
+    """scvx_collision_check_batched against numpy on every (agent, node): the violation count and the
+    largest row value, with clustered agents (rows near the threshold), far agents (skipped by the
+    kernel's distance bound) and one coincident pair (NaN, as the reference's 0/0)."""
+    import torch
+    rng = np.random.default_rng(7)
+    N, K, R, tol = 300, 8, 0.5, 1e-7
+    X_all = np.zeros((N, K, 6))
+    X_all[:, :, :3] = rng.normal(scale=3.0, size=(N, K, 3))
+    X_all[:40, :, :3] = rng.normal(scale=0.4, size=(40, K, 3))   # a dense cluster
+    X_all[41, 3, :3] = X_all[40, 3, :3]                          # coincident at node 3
+    X_new = X_all + rng.normal(scale=0.2, size=X_all.shape)
+    S = np.abs(rng.normal(scale=0.3, size=(N, K)))
+    viol, vmax = scvx_hip.collision_check(_t(X_all, cuda), 0, _t(X_new, cuda), _t(S, cuda), R, tol=tol)
+    viol, vmax = viol.cpu().numpy(), vmax.cpu().numpy()
+    with np.errstate(all="ignore"):
+        for a in range(N):
+            for t in range(K - 1):
+                diff = X_all[a, t, :3] - np.delete(X_all[:, t, :3], a, axis=0)
+                nr = np.linalg.norm(diff, axis=1)
+                v = (2 * R - nr) - diff @ (X_new[a, t, :3] - X_all[a, t, :3]) / nr - S[a, t]
+                assert viol[a, t] == int(np.sum((v > tol) | np.isnan(v))), (a, t)
+                if np.isnan(v).any():
+                    assert np.isnan(vmax[a, t]), (a, t)
+                else:
+                    assert abs(vmax[a, t] - v.max()) <= 1e-12 * max(1.0, abs(v.max())), (a, t, vmax[a, t], v.max())
+            assert viol[a, K - 1] == 0
