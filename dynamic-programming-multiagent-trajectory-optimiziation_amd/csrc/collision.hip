@@ -67,6 +67,31 @@ __global__ __launch_bounds__(64) void collision_rows_kernel(int K, int pd, int n
     int n = 0, worst = 0;
     double worst_d2 = -1.0;  // largest |d|^2 among kept rows (the one to evict)
     const double cull2 = cull > 0 ? cull * cull : -1.0;
+    // A first bound tau on the j_max-th smallest |d|^2: the j_max-th smallest over this wave's other
+    // agents (their positions are the lanes' pi).  Every kept row has |d|^2 <= tau, so the scan below
+    // considers only those: the kept set is unchanged (rows are stored in insertion order), and the
+    // insertion code runs for a few dozen neighbours instead of whenever one lane's list changes.
+    __shared__ double blk[64 * 3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) blk[lane * 3 + d] = pi[d];
+    __syncthreads();
+    double tau = 1e300;
+    if (live) {
+        double sv[JM];  // ascending
+#pragma unroll
+        for (int k = 0; k < JM; ++k) sv[k] = 1e300;
+        const long long b0 = (long long)blockIdx.x * 64;
+        for (int l = 0; l < 64; ++l) {
+            if (l == lane || b0 + l >= N_local) continue;
+            const double d2 = coll_d2(pi, blk + l * 3, pd);
+            if (cull2 > 0 && !(d2 < cull2)) continue;
+#pragma unroll
+            for (int k = JM - 1; k > 0; --k) sv[k] = d2 < sv[k - 1] ? sv[k - 1] : fmin(sv[k], d2);
+            sv[0] = fmin(sv[0], d2);
+        }
+#pragma unroll
+        for (int k = 0; k < JM; ++k) tau = (k == j_max - 1) ? sv[k] : tau;
+    }
     for (int j0 = 0; j0 < N_total; j0 += COLL_TJ) {
         const int nt = min(COLL_TJ, N_total - j0);
         __syncthreads();
@@ -80,19 +105,19 @@ __global__ __launch_bounds__(64) void collision_rows_kernel(int K, int pd, int n
             // squared distances of a chunk of neighbours, branch-free (independent LDS broadcasts and
             // FMAs); the sequential insertion below runs only if some lane of the wave may keep one
             double d2v[COLL_CH];
-            bool need = n < j_max;
+            bool need = false;
 #pragma unroll
             for (int c = 0; c < COLL_CH; ++c) {
                 const int jj = min(jb + c, nt - 1);
                 d2v[c] = coll_d2(pi, tile + jj * 3, pd);
-                need |= (jb + c < nt) && d2v[c] < worst_d2;
+                need |= (jb + c < nt) && d2v[c] <= tau && (n < j_max || d2v[c] < worst_d2);
             }
             if (!__builtin_amdgcn_ballot_w64(need)) continue;
 #pragma unroll
             for (int c = 0; c < COLL_CH; ++c) {
                 const long long j = j0 + jb + c;
                 const double d2 = d2v[c];
-                if (jb + c >= nt || j == gi || (cull2 > 0 && !(d2 < cull2))) continue;
+                if (jb + c >= nt || j == gi || !(d2 <= tau) || (cull2 > 0 && !(d2 < cull2))) continue;
                 int slot;
                 if (n < j_max) {
                     slot = n++;
@@ -173,6 +198,31 @@ __global__ __launch_bounds__(64) void collision_check_kernel(int K, int pd, int 
     const double rr = 2.0 * R;
     const double ndp = sqrt(dp[0] * dp[0] + dp[1] * dp[1] + dp[2] * dp[2]);
     double skip2 = 1e300;  // skip the exact row when d2 >= skip2 (none before the first row)
+    // the rows of this wave's other agents first (their positions are the lanes' pi, usually the
+    // nearest ones): the bound then skips most of the scan below, which leaves those agents out
+    __shared__ double blk[64 * 3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) blk[lane * 3 + d] = pi[d];
+    __syncthreads();
+    const long long b0 = (long long)blockIdx.x * 64;
+    const long long blo = i0 + b0, bhi = i0 + min(b0 + 64, (long long)N_local);  // global [blo, bhi)
+    auto row = [&](const double* pj) __attribute__((always_inline)) {
+        double gd = 0.0;
+        for (int d = 0; d < pd; ++d) gd += (pi[d] - pj[d]) * dp[d];
+        const double d2 = coll_d2(pi, pj, pd);
+        if (!(d2 < skip2)) return;
+        const double nr = sqrt(d2);
+        const double v = (rr - nr) - gd / nr - S;  // NaN for coincident agents, as the reference's 0/0
+        worst = (v > worst || v != v) ? v : worst;
+        nv += (v > tol || v != v) ? 1 : 0;
+        // fmin ignores a NaN maximum: the count threshold tol still bounds the skip
+        const double cb = (rr + ndp - S - fmin(worst, tol)) * (1.0 + 1e-12) + 1e-12;
+        skip2 = cb > 0.0 ? cb * cb : 1e-300;  // cb <= 0: every row but a coincident one (d2 = 0) skips
+    };
+    if (live) {
+        for (int l = 0; l < 64; ++l)
+            if (l != lane && b0 + l < N_local) row(blk + l * 3);
+    }
     for (int j0 = 0; j0 < N_total; j0 += COLL_TJ) {
         const int nt = min(COLL_TJ, N_total - j0);
         __syncthreads();
@@ -189,22 +239,16 @@ __global__ __launch_bounds__(64) void collision_check_kernel(int K, int pd, int 
             for (int c = 0; c < COLL_CH; ++c) {
                 const int jj = min(jb + c, nt - 1);
                 d2v[c] = coll_d2(pi, tile + jj * 3, pd);
-                need |= (jb + c < nt) && d2v[c] < skip2;
+                const long long j = j0 + jb + c;
+                need |= (jb + c < nt) && d2v[c] < skip2 && (j < blo || j >= bhi);
             }
             if (!__builtin_amdgcn_ballot_w64(need)) continue;
 #pragma unroll
             for (int c = 0; c < COLL_CH; ++c) {
                 const int jj = jb + c;
-                if (jj >= nt || j0 + jj == gi || !(d2v[c] < skip2)) continue;
-                double gd = 0.0;
-                for (int d = 0; d < pd; ++d) gd += (pi[d] - tile[jj * 3 + d]) * dp[d];
-                const double nr = sqrt(d2v[c]);
-                const double v = (rr - nr) - gd / nr - S;  // NaN for coincident agents, as the reference's 0/0
-                worst = (v > worst || v != v) ? v : worst;
-                nv += (v > tol || v != v) ? 1 : 0;
-                // fmin ignores a NaN maximum: the count threshold tol still bounds the skip
-                const double cb = (rr + ndp - S - fmin(worst, tol)) * (1.0 + 1e-12) + 1e-12;
-                skip2 = cb > 0.0 ? cb * cb : 1e-300;  // cb <= 0: every row but a coincident one (d2 = 0) skips
+                const long long j = j0 + jj;
+                if (jj >= nt || (j >= blo && j < bhi) || !(d2v[c] < skip2)) continue;
+                row(tile + jj * 3);
             }
         }
     }

@@ -261,3 +261,31 @@ def test_collision_check_kernel_exact_on_every_row(cuda):
                 else:
                     assert abs(vmax[a, t] - v.max()) <= 1e-12 * max(1.0, abs(v.max())), (a, t, vmax[a, t], v.max())
             assert viol[a, K - 1] == 0
+
+
+@pytest.mark.parametrize("j_max", [8, 16])
+def test_collision_rows_keep_the_nearest_neighbours(cuda, j_max):
+    """scvx_collision_rows_batched's culled selection against numpy on every (agent, node): the j_max
+    rows of the nearest neighbours (dist_scvx_3d.py:93-107 rows, compared as sets), for 200 local
+    agents of 300 (a dense cluster and a sparse cloud, so the wave-local bound is tight for some
+    waves and loose for others)."""
+    rng = np.random.default_rng(11)
+    N, K, R, i0, n_loc = 300, 6, 0.5, 50, 200
+    X_all = np.zeros((N, K, 6))
+    X_all[:, :, :3] = rng.normal(scale=4.0, size=(N, K, 3))
+    X_all[60:140, :, :3] = rng.normal(scale=0.5, size=(80, K, 3))
+    rows, cnt = scvx_hip.collision_rows(_t(X_all, cuda), i0, n_loc, R, j_max=j_max)
+    rows, cnt = rows.cpu().numpy(), cnt.cpu().numpy()
+    for a in range(n_loc):
+        gi = i0 + a
+        for t in range(K - 1):
+            assert cnt[a, t] == j_max
+            diff = X_all[gi, t, :3] - X_all[:, t, :3]
+            nr = np.linalg.norm(diff, axis=1)
+            nr[gi] = np.inf
+            near = np.argsort(nr, kind="stable")[:j_max]
+            g = diff[near] / nr[near, None]
+            ref = np.hstack([g, (2 * R - nr[near] + g @ X_all[gi, t, :3])[:, None]])
+            got = rows[a, t, :j_max]
+            np.testing.assert_allclose(got[np.lexsort(got.T)], ref[np.lexsort(ref.T)], rtol=1e-12, atol=1e-12)
+        assert cnt[a, K - 1] == 0
