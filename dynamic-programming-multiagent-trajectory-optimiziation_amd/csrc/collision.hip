@@ -34,10 +34,23 @@ constexpr int COLL_TJ = 512;  // neighbours staged per LDS tile
 constexpr int COLL_CH = 8;    // neighbours per branch-free chunk of the scans
 
 // |p_i - p_j|^2 summed in coordinate order (d0^2 + d1^2) + d2^2, the rounding of the sequential
-// scan the selection and the check were pinned with
-__device__ __forceinline__ double coll_d2(const double* pi, const double* pj, int pd) {
-    const double d0 = pi[0] - pj[0], d1 = pd > 1 ? pi[1] - pj[1] : 0.0, d2 = pd > 2 ? pi[2] - pj[2] : 0.0;
+// scan the selection and the check were pinned with.  Positions past pos_dim are 0 in both operands
+// (tile and lane registers), so the unused terms add exact zeros.
+__device__ __forceinline__ double coll_d2(const double* pi, const double* pj, int) {
+    const double d0 = pi[0] - pj[0], d1 = pi[1] - pj[1], d2 = pi[2] - pj[2];
     return fma(d2, d2, fma(d1, d1, d0 * d0));
+}
+
+// Stage node t's positions of neighbours [j0, j0 + nt) in LDS as [jj][3] (zeros past pos_dim), and
+// pad the tile to a whole chunk with far-away positions (|d|^2 = inf: never kept, never checked), so
+// the chunk loops need no bounds tests.
+__device__ __forceinline__ void coll_stage(double* tile, const double* __restrict__ X_all, int j0, int nt, int K,
+                                           int t, int nx, int pd, int lane) {
+    const int ntp = (nt + COLL_CH - 1) / COLL_CH * COLL_CH;
+    for (int e = lane; e < ntp * 3; e += 64) {
+        const int jj = e / 3, d = e - jj * 3;
+        tile[e] = jj >= nt ? 1e200 : (d < pd ? X_all[((long long)(j0 + jj) * K + t) * nx + d] : 0.0);
+    }
 }
 
 template <int JM>
@@ -95,23 +108,20 @@ __global__ __launch_bounds__(64) void collision_rows_kernel(int K, int pd, int n
     for (int j0 = 0; j0 < N_total; j0 += COLL_TJ) {
         const int nt = min(COLL_TJ, N_total - j0);
         __syncthreads();
-        for (int e = lane; e < nt * pd; e += 64) {
-            const int jj = e / pd, d = e - jj * pd;
-            tile[jj * 3 + d] = X_all[((long long)(j0 + jj) * K + t) * nx + d];
-        }
+        coll_stage(tile, X_all, j0, nt, K, t, nx, pd, lane);
         __syncthreads();
         if (!live) continue;
         for (int jb = 0; jb < nt; jb += COLL_CH) {
             // squared distances of a chunk of neighbours, branch-free (independent LDS broadcasts and
             // FMAs); the sequential insertion below runs only if some lane of the wave may keep one
-            double d2v[COLL_CH];
-            bool need = false;
+            double d2v[COLL_CH], m = 1e300;
 #pragma unroll
             for (int c = 0; c < COLL_CH; ++c) {
-                const int jj = min(jb + c, nt - 1);
-                d2v[c] = coll_d2(pi, tile + jj * 3, pd);
-                need |= (jb + c < nt) && d2v[c] <= tau && (n < j_max || d2v[c] < worst_d2);
+                d2v[c] = coll_d2(pi, tile + (jb + c) * 3, pd);
+                m = fmin(m, d2v[c]);
             }
+            // some element of the chunk may enter the list iff its smallest |d|^2 may
+            const bool need = m <= tau && (n < j_max || m < worst_d2);
             if (!__builtin_amdgcn_ballot_w64(need)) continue;
 #pragma unroll
             for (int c = 0; c < COLL_CH; ++c) {
@@ -226,22 +236,17 @@ __global__ __launch_bounds__(64) void collision_check_kernel(int K, int pd, int 
     for (int j0 = 0; j0 < N_total; j0 += COLL_TJ) {
         const int nt = min(COLL_TJ, N_total - j0);
         __syncthreads();
-        for (int e = lane; e < nt * pd; e += 64) {
-            const int jj = e / pd, d = e - jj * pd;
-            tile[jj * 3 + d] = X_all[((long long)(j0 + jj) * K + t) * nx + d];
-        }
+        coll_stage(tile, X_all, j0, nt, K, t, nx, pd, lane);
         __syncthreads();
         if (!live) continue;
         for (int jb = 0; jb < nt; jb += COLL_CH) {
-            double d2v[COLL_CH];
-            bool need = false;
+            double d2v[COLL_CH], m = 1e300;
 #pragma unroll
             for (int c = 0; c < COLL_CH; ++c) {
-                const int jj = min(jb + c, nt - 1);
-                d2v[c] = coll_d2(pi, tile + jj * 3, pd);
-                const long long j = j0 + jb + c;
-                need |= (jb + c < nt) && d2v[c] < skip2 && (j < blo || j >= bhi);
+                d2v[c] = coll_d2(pi, tile + (jb + c) * 3, pd);
+                m = fmin(m, d2v[c]);
             }
+            const bool need = m < skip2;  // (block-mates, done above, are skipped below)
             if (!__builtin_amdgcn_ballot_w64(need)) continue;
 #pragma unroll
             for (int c = 0; c < COLL_CH; ++c) {
