@@ -521,16 +521,14 @@ def main():
                                tol=args.tol, max_iter=60)
         drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, coupling=CouplingSpec(R=cfg["R"]),
                          tr_rule="global")
-    X, U = w["X"].clone(), w["U"].clone()
+    it_state = [w["X"].clone(), w["U"].clone()]   # the current iterate (X, U), rebound every step
 
-    def step(X, U, marks=None):
-        Xn, Un, out = drv.step(X, U, marks=marks)
-        X.copy_(Xn)
-        U.copy_(Un)
+    def step(marks=None):
+        it_state[0], it_state[1], out = drv.step(it_state[0], it_state[1], marks=marks)
         return out
 
     for _ in range(args.warmup):
-        step(X, U)
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -541,7 +539,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         mk = []
-        out = step(X, U, mk)
+        out = step(mk)
         marks.append(mk)
         iters.append(out["iters"].sum())
         if drv.last_check is not None:

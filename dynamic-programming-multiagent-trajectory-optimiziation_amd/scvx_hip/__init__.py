@@ -467,6 +467,32 @@ def admm_consensus(X_new, nbr, rho, Y, Lam, pos_dim, primal=None, dual=None, str
     return primal, dual
 
 
+def jacobi_update(status, X_sol, U_sol, X, U, tr, prev_cost, grow=False, tr_max=float("inf"), X_out=None, U_out=None,
+                  stream=None):
+    """Fused bookkeeping of one Jacobi SCvx iteration, per-agent trust-region rule
+    (scvx_jacobi_update_batched): failed agents (status 2) keep (X, U), the others take (X_sol, U_sol);
+    tr halves where sum_{t<K-1} ||u_t||^2 rose above prev_cost, then a failed agent's radius halves
+    (or doubles up to tr_max with grow=True); prev_cost <- the new cost.  tr / prev_cost are updated in
+    place; returns (X_out, U_out) (fresh tensors unless given)."""
+    torch = _torch()
+    N, K, n = X.shape
+    m = U.shape[2]
+    if (tuple(X_sol.shape) != (N, K, n) or tuple(U.shape) != (N, K, m) or tuple(U_sol.shape) != (N, K, m)
+            or tuple(status.shape) != (N,) or tuple(tr.shape) != (N,) or tuple(prev_cost.shape) != (N,)):
+        raise ValueError("jacobi_update: X / X_sol (N,K,n), U / U_sol (N,K,m), status / tr / prev_cost (N,)")
+    X_out = torch.empty_like(X) if X_out is None else X_out
+    U_out = torch.empty_like(U) if U_out is None else U_out
+    if tuple(X_out.shape) != (N, K, n) or tuple(U_out.shape) != (N, K, m):
+        raise ValueError("jacobi_update: X_out / U_out shapes")
+    rc = lib().scvx_jacobi_update_batched(N, K, n, m, _dev(status, torch.int32, "status"), _dev(X_sol, name="X_sol"),
+                                          _dev(U_sol, name="U_sol"), _dev(X, name="X"), _dev(U, name="U"),
+                                          _dev(X_out, name="X_out"), _dev(U_out, name="U_out"), _dev(tr, name="tr"),
+                                          _dev(prev_cost, name="prev_cost"), int(bool(grow)), float(tr_max),
+                                          _stream(stream))
+    check(rc, "scvx_jacobi_update_batched")
+    return X_out, U_out
+
+
 def intersample_batched(model, X, U, sigma, obstacles, proj=None, dt=1.0, seg_dt=None, num_samples=100, eps=1e-4,
                         tol=1e-6, max_crit=8, nsub=None, params=None, stream=None):
     """Inter-sample obstacle minima for every (agent, segment, obstacle) (scvx_intersample_batched;

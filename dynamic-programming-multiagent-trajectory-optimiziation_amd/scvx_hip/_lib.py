@@ -20,7 +20,7 @@ EXPORTS = ("scvx_version", "scvx_last_error", "scvx_foh_batched", "scvx_integrat
            "scvx_qp_solve_batched", "scvx_qp_workspace_bytes", "scvx_qp_set_trace",
            "scvx_collision_rows_batched", "scvx_collision_check_batched", "scvx_scp_solve_batched", "scvx_scp_workspace_bytes",
            "scvx_intersample_batched", "scvx_admm_consensus_batched", "scvx_scp_game_solve_batched",
-           "scvx_slab_update_batched")
+           "scvx_slab_update_batched", "scvx_jacobi_update_batched")
 
 
 class ScvxError(RuntimeError):
@@ -103,6 +103,7 @@ def lib():
         L.scvx_admm_consensus_batched.argtypes = [i32, i32, i32, i32, i32, vp, vp, dbl, vp, vp, vp, vp, vp]
         L.scvx_scp_game_solve_batched.argtypes = [ctypes.POINTER(SCPTemplate), i32] + [vp] * 18 + [vp, sz, vp]
         L.scvx_slab_update_batched.argtypes = [i32, i32, i32, i32, i32, vp, vp, vp, vp]
+        L.scvx_jacobi_update_batched.argtypes = [i32, i32, i32, i32] + [vp] * 9 + [i32, dbl, vp]
         sized = ("scvx_last_error", "scvx_qp_workspace_bytes", "scvx_scp_workspace_bytes")
         for fn in EXPORTS:
             getattr(L, fn).restype = getattr(L, fn).restype if fn in sized else i32

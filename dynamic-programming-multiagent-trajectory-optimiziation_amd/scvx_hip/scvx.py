@@ -15,7 +15,8 @@ import dataclasses
 from dataclasses import dataclass
 from typing import Optional
 
-from . import (DEFAULT_NSUB, MODEL_DIMS, QPSolver, QPSpec, collision_check, collision_rows, foh_batched)
+from . import (DEFAULT_NSUB, MODEL_DIMS, QPSolver, QPSpec, collision_check, collision_rows, foh_batched,
+               jacobi_update)
 
 
 class HipBackend:
@@ -32,6 +33,9 @@ class HipBackend:
 
     def qp_solver(self, spec, N, device):
         return QPSolver(spec, N, device=device)
+
+    def jacobi_update(self, status, X_sol, U_sol, X, U, tr, prev_cost, grow, tr_max):
+        return jacobi_update(status, X_sol, U_sol, X, U, tr, prev_cost, grow=grow, tr_max=tr_max)
 
 
 @dataclass
@@ -173,6 +177,13 @@ class JacobiSCvx:
         # iterate (its output may be non-finite and would otherwise reach every other agent through
         # the collision all-gather) and halves its own trust radius so the next subproblem differs.
         # The reference aborts the whole run instead (cvxpy raises SolverError, dist_scvx_3d.py:110).
+        fused = getattr(self.backend, "jacobi_update", None)
+        if self.tr_rule == "per_agent" and fused is not None:
+            # one launch for the update, the cost rule and the failure rule (csrc/jacobi.hip)
+            Xn, Un = fused(out["status"], out["X"], out["U"], X, U, self.tr, self.prev_cost, self.on_fail == "grow",
+                           self.tr_max)
+            self._mark(marks, "update")
+            return Xn, Un, out
         failed = out["status"] == 2
         ok = (~failed)[:, None, None]
         Xn, Un = torch.where(ok, out["X"], X), torch.where(ok, out["U"], U)

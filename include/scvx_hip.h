@@ -323,6 +323,20 @@ int scvx_admm_consensus_batched(int N, int n_nbr, int K, int pos_dim, int n_x, c
                                 const int32_t* nbr, double rho, double* Y, double* Lam, double* primal,
                                 double* dual, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Bookkeeping of one Jacobi SCvx iteration with the per-agent trust-region rule (the tensor ops of
+ * scvx_hip/scvx.py JacobiSCvx.step, fused): per agent i, (X_out[i], U_out[i]) = (X_sol[i], U_sol[i]) if
+ * status[i] != 2, else (X[i], U[i]) (Distributed_opt/dist_scvx_3d.py:113-118; X_out may alias X);
+ * cost = sum_{t<K-1} ||U_out[i][t]||^2
+ * (cost_fcn, :131-138); tr[i] *= 0.5 if cost > prev_cost[i] (:248-252, per agent); a failed agent's
+ * radius then halves (grow = 0) or doubles up to tr_max (grow = 1); prev_cost[i] = cost.
+ * Device buffers: status [N] int32, X_sol / X / X_out [N][K][n_x], U_sol / U / U_out [N][K][n_u],
+ * tr / prev_cost [N] (updated in place).
+ */
+int scvx_jacobi_update_batched(int N, int K, int n_x, int n_u, const int32_t* status, const double* X_sol,
+                               const double* U_sol, const double* X, const double* U, double* X_out, double* U_out,
+                               double* tr, double* prev_cost, int grow, double tr_max, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
