@@ -6,7 +6,8 @@
 //     (the update X_traj += s of Distributed_opt/dist_scvx_3d.py:113-118, with the solved trajectory);
 //   * cost_i = sum_{t<K-1} ||u_t||^2 of the new inputs (cost_fcn, dist_scvx_3d.py:131-138);
 //   * tr_i halves when cost_i > prev_cost_i (the rule of dist_scvx_3d.py:248-252 applied per agent),
-//     then a failed agent's radius halves (grow = 0) or doubles up to tr_max (grow = 1);
+//     then a failed agent's radius halves (grow = 0) or doubles (grow = 1, every radius then capped
+//     at tr_max);
 //   * prev_cost_i = cost_i.
 // One wave per agent: coalesced copies of the agent's X / U slabs, the cost by a wave reduction,
 // lane 0 updates the radius.  Replaces ~10 small elementwise launches per SCvx iteration.
@@ -40,7 +41,8 @@ __global__ __launch_bounds__(64) void jacobi_update_kernel(int K, int n, int m, 
     if (lane == 0) {
         double r = tr[a];
         if (c > prev_cost[a]) r *= 0.5;
-        if (!ok) r = grow ? fmin(2.0 * r, tr_max) : 0.5 * r;
+        if (!ok) r = grow ? 2.0 * r : 0.5 * r;
+        if (grow) r = fmin(r, tr_max);  // the driver's rule caps every radius at tr_max in grow mode
         tr[a] = r;
         prev_cost[a] = c;
     }

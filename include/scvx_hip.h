@@ -329,7 +329,8 @@ int scvx_admm_consensus_batched(int N, int n_nbr, int K, int pos_dim, int n_x, c
  * status[i] != 2, else (X[i], U[i]) (Distributed_opt/dist_scvx_3d.py:113-118; X_out may alias X);
  * cost = sum_{t<K-1} ||U_out[i][t]||^2
  * (cost_fcn, :131-138); tr[i] *= 0.5 if cost > prev_cost[i] (:248-252, per agent); a failed agent's
- * radius then halves (grow = 0) or doubles up to tr_max (grow = 1); prev_cost[i] = cost.
+ * radius then halves (grow = 0) or doubles (grow = 1; every radius is then capped at tr_max);
+ * prev_cost[i] = cost.
  * Device buffers: status [N] int32, X_sol / X / X_out [N][K][n_x], U_sol / U / U_out [N][K][n_u],
  * tr / prev_cost [N] (updated in place).
  */

@@ -48,8 +48,12 @@ def test_fused_update_matches_tensor_rule(cuda, grow):
 
 
 def test_driver_fused_and_tensor_paths_agree(cuda):
-    """Three C3-family SCvx iterations through JacobiSCvx with the fused update and with the tensor
-    path (a backend without jacobi_update): identical iterates, radii and statuses."""
+    """Two C3-family SCvx iterations through JacobiSCvx with the fused update and with the tensor path
+    (a backend without jacobi_update): identical iterates and statuses, identical radii after the
+    first.  (This family converges in one step, so the second step's costs equal the first's to
+    rounding, and the halving test `cost > prev_cost` is decided by summation order -- in the
+    reference's cost_fcn as well; `tools/jac_diag.py` prints those agents.  The radii are therefore
+    compared after the first step only.)"""
     import torch
     from scvx_hip import workloads
     from scvx_hip.scvx import HipBackend, JacobiSCvx
@@ -65,9 +69,10 @@ def test_driver_fused_and_tensor_paths_agree(cuda):
     for backend in (HipBackend(), TensorPath()):
         drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], 0.25, backend=backend)
         X, U = w["X"].clone(), w["U"].clone()
-        for _ in range(3):
-            X, U, out = drv.step(X, U)
-        runs.append((X, U, drv.tr.clone(), out["status"].clone()))
+        X, U, out = drv.step(X, U)
+        tr1 = drv.tr.clone()
+        X, U, out = drv.step(X, U)
+        runs.append((X, U, tr1, out["status"].clone()))
     (Xa, Ua, ta, sa), (Xb, Ub, tb, sb) = runs
     assert torch.equal(sa, sb) and torch.equal(ta, tb)
     assert torch.equal(Xa, Xb) and torch.equal(Ua, Ub)
