@@ -66,7 +66,7 @@ class JacobiSCvx:
 
     def __init__(self, spec: QPSpec, x_init, x_final, sigma, tr0: float, coupling: Optional[CouplingSpec] = None,
                  tr_rule: str = "per_agent", group=None, nsub: Optional[int] = None, backend=None,
-                 on_fail: str = "halve", tr_max: Optional[float] = None):
+                 on_fail: str = "halve", tr_max: Optional[float] = None, fused_update: bool = False):
         import torch
         self.torch = torch
         self.backend = backend or HipBackend()
@@ -79,6 +79,9 @@ class JacobiSCvx:
         if on_fail not in ("halve", "grow"):
             raise ValueError(f"on_fail must be 'halve' or 'grow', not {on_fail!r}")
         self.on_fail, self.tr_max = on_fail, float(tr0 if tr_max is None else tr_max)
+        # per-agent rule in one launch (csrc/jacobi.hip); opt-in: its cost summation order breaks the
+        # rounding-level ties of converged agents differently from the tensor form
+        self.fused_update = fused_update
         self.group = group
         self.nsub = nsub or DEFAULT_NSUB[spec.model]
         self.solver = self.backend.qp_solver(spec, self.N, self.device)
@@ -178,7 +181,7 @@ class JacobiSCvx:
         # the collision all-gather) and halves its own trust radius so the next subproblem differs.
         # The reference aborts the whole run instead (cvxpy raises SolverError, dist_scvx_3d.py:110).
         fused = getattr(self.backend, "jacobi_update", None)
-        if self.tr_rule == "per_agent" and fused is not None:
+        if self.fused_update and self.tr_rule == "per_agent" and fused is not None:
             # one launch for the update, the cost rule and the failure rule (csrc/jacobi.hip)
             Xn, Un = fused(out["status"], out["X"], out["U"], X, U, self.tr, self.prev_cost, self.on_fail == "grow",
                            self.tr_max)

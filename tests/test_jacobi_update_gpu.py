@@ -67,7 +67,7 @@ def test_driver_fused_and_tensor_paths_agree(cuda):
                            max_iter=60)
     runs = []
     for backend in (HipBackend(), TensorPath()):
-        drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], 0.25, backend=backend)
+        drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], 0.25, backend=backend, fused_update=True)
         X, U = w["X"].clone(), w["U"].clone()
         X, U, out = drv.step(X, U)
         tr1 = drv.tr.clone()

@@ -15,7 +15,8 @@ dev = torch.device("cuda:0")
 sc = workloads.synthetic_di(128, K=50, seed=3, sigma=30.0, obstacles=8)
 w = {k: torch.tensor(sc[k], device=dev) for k in ("X", "U", "x_init", "x_final", "sigma")}
 spec = scvx_hip.QPSpec(model="di", K=50, box=[(0, -12, 12), (1, -12, 12)], obs=sc["obs"], w_obs=1e6, u_max=1.0, max_iter=60)
-drvs = [JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], 0.25, backend=b) for b in (HipBackend(), TensorPath())]
+drvs = [JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], 0.25, backend=b, fused_update=True)
+        for b in (HipBackend(), TensorPath())]
 st = [[w["X"].clone(), w["U"].clone()] for _ in drvs]
 for k in range(3):
     outs = []
