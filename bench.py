@@ -23,7 +23,9 @@ Optional workloads (--config; the default c3 is the headline line the driver rec
       are sharded contiguously over ranks; one RCCL all_gather of the states per iteration feeds the
       collision linearization (strong scaling: the 4096-agent problem is fixed).
   c5  N=1024 12-state quadrotors (models.hpp) from hover, 8 obstacles, coupling as c4 with R=0.5
-      (strong scaling).
+      (strong scaling); the subproblem carries virtual control (QPSpec.w_nu = 1e4: nu_t in the dynamics
+      priced w_nu ||nu_t||_1, the SCvx form of sc_problem.py:60-68) and a proximal state term
+      (QPSpec.w_prox = 10), so it stays feasible under the Jacobi update of a nonlinear model.
 """
 import argparse
 import json
@@ -44,6 +46,7 @@ TR0 = 0.25
 U_MAX = 1.0
 N_OBS = 8
 BOX = [(0, -12.0, 12.0), (1, -12.0, 12.0)]
+C5_W_NU, C5_W_PROX = 1e4, 10.0   # c5 subproblem: virtual control weight (WEIGHT_NU, global_parameters.py) and proximal term
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) dense peak, spec
 HBM_PEAK_GBS = 8000.0
 
@@ -124,6 +127,7 @@ def make_coupled(config, world, rank, device):
     else:
         sc = workloads.synthetic_quad(1024, K=K, seed=3, sigma=SIGMA, obstacles=N_OBS)
         model, R, obs, box, j_max = "quad", 0.5, sc["obs"], workloads.QUAD_BOX, 8
+    vc = dict(w_nu=C5_W_NU, w_prox=C5_W_PROX) if config == "c5" else {}
     N_total = sc["X"].shape[0]
     if N_total % world:
         raise SystemExit(f"{config}: {N_total} agents do not shard over {world} ranks")
@@ -131,7 +135,7 @@ def make_coupled(config, world, rank, device):
     sl = slice(rank * n_loc, (rank + 1) * n_loc)
     t = {k: torch.tensor(np.ascontiguousarray(sc[k][sl]), device=device)
          for k in ("X", "U", "x_init", "x_final", "sigma")}
-    return sc, t, dict(model=model, R=R, obs=obs, box=box, j_max=j_max, N_total=N_total, n_loc=n_loc)
+    return sc, t, dict(model=model, R=R, obs=obs, box=box, j_max=j_max, N_total=N_total, n_loc=n_loc, vc=vc)
 
 
 def host_info():
@@ -518,7 +522,7 @@ def main():
         n, m = scvx_hip.MODEL_DIMS[model]
         n_obs = len(cfg["obs"])
         spec = scvx_hip.QPSpec(model=model, K=K, box=box, obs=cfg["obs"], w_obs=1e6, j_max=j_max, w_coll=1e4,
-                               tol=args.tol, max_iter=60)
+                               tol=args.tol, max_iter=60, **cfg["vc"])
         drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, coupling=CouplingSpec(R=cfg["R"]),
                          tr_rule="global")
     it_state = [w["X"].clone(), w["U"].clone()]   # the current iterate (X, U), rebound every step
@@ -535,13 +539,15 @@ def main():
     torch.cuda.synchronize()
     # timed region: exactly `steps` steps (the same code path as the warmup); every stage is bracketed
     # by HIP events on the launch stream (the QP kernel's mark pair gives its launch duration)
-    marks, iters, checks = [], [], []
+    marks, iters, checks, stats = [], [], [], []
+    status_ids = torch.arange(3, device=device, dtype=torch.int32)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         mk = []
         out = step(mk)
         marks.append(mk)
         iters.append(out["iters"].sum())
+        stats.append((out["status"][:, None] == status_ids).sum(dim=0))   # device op, no sync (bincount syncs)
         if drv.last_check is not None:
             checks.append(dict(drv.last_check))
     torch.cuda.synchronize()
@@ -596,7 +602,9 @@ def main():
             workload = (f"{args.config.upper()}: N={cfg['N_total']} agents ({N}/GPU), model {model} n={n} m={m}, "
                         f"K=50, pairwise coupling R={cfg['R']} (j_max={j_max} nearest rows per node in the solve, "
                         f"every other row checked at the solution and violators re-solved with 32), {n_obs} "
-                        f"obstacles, box |x|,|y|<={box[0][2]:g}, global trust-region rule, RCCL all_gather of states")
+                        f"obstacles, box |x|,|y|<={box[0][2]:g}, global trust-region rule, RCCL all_gather of states"
+                        + (f", virtual control w_nu={cfg['vc']['w_nu']:g} + proximal w_prox={cfg['vc']['w_prox']:g}"
+                           if cfg["vc"] else ""))
         line = {
             "metric": metric,
             "value": value,
@@ -633,6 +641,8 @@ def main():
             "ipm_iters_hist_last": {str(int(v)): int(c) for v, c in zip(*np.unique(out["iters"].cpu().numpy(),
                                                                                   return_counts=True))},
             "status_counts": {str(k): int((status == k).sum()) for k in (0, 1, 2)},
+            "status_counts_per_step": [[int(v) for v in c.tolist()[:3]] for c in stats],
+            "min_frac_status_0_1": min(float((c[0] + c[1]).item()) / N for c in stats),
             "coupling_check": checks or None,
             "cpu_baseline": cpu,
         }

@@ -36,10 +36,10 @@ struct ModelTable {
 // model table entry for the template (nullptr: unknown model / dimensions)
 const ModelTable* model_of(const scvx_qp_template& T) {
     static const ModelTable tab[] = {
-        {6, 3, kCapsDI, (int)(sizeof(kCapsDI) / sizeof(int) / 3), qp_launch_di},
-        {3, 2, kCapsUni, (int)(sizeof(kCapsUni) / sizeof(int) / 3), qp_launch_unicycle},
-        {3, 3, kCapsSI, (int)(sizeof(kCapsSI) / sizeof(int) / 3), qp_launch_si},
-        {12, 4, kCapsQuad, (int)(sizeof(kCapsQuad) / sizeof(int) / 3), qp_launch_quad},
+        {6, 3, kCapsDI, (int)(sizeof(kCapsDI) / sizeof(int) / QP_CAPS_W), qp_launch_di},
+        {3, 2, kCapsUni, (int)(sizeof(kCapsUni) / sizeof(int) / QP_CAPS_W), qp_launch_unicycle},
+        {3, 3, kCapsSI, (int)(sizeof(kCapsSI) / sizeof(int) / QP_CAPS_W), qp_launch_si},
+        {12, 4, kCapsQuad, (int)(sizeof(kCapsQuad) / sizeof(int) / QP_CAPS_W), qp_launch_quad},
     };
     const int ids[] = {SCVX_MODEL_DOUBLE_INTEGRATOR, SCVX_MODEL_UNICYCLE, SCVX_MODEL_SINGLE_INTEGRATOR, SCVX_MODEL_QUADROTOR};
     for (int i = 0; i < 4; ++i)
@@ -60,14 +60,19 @@ int qp_check(const scvx_qp_template* T, int N, const ModelTable*& mt, int& cls) 
     mt = model_of(*T);
     if (!mt) return set_error(SCVX_EUNSUPPORTED, "qp: model id / dimensions");
     cls = qp_pick_caps(mt->caps, mt->ncaps, *T);
-    if (cls < 0) return set_error(SCVX_EUNSUPPORTED, "qp: more box / obstacle / collision rows than the largest capacity class (j_max <= 32, n_obs <= 16)");
+    if (T->w_nu < 0.0 || T->w_prox < 0.0) return set_error(SCVX_EINVAL, "qp: w_nu / w_prox must be >= 0");
+    if (cls < 0)
+        return set_error(SCVX_EUNSUPPORTED, T->w_nu > 0.0
+            ? "qp: no virtual-control class for this model / row counts (w_nu > 0: quad n_box <= 4, n_obs <= 16, j_max <= 32; di n_box <= 2, n_obs <= 8, no coupling)"
+            : "qp: more box / obstacle / collision rows than the largest capacity class (j_max <= 32, n_obs <= 16)");
     return SCVX_OK;
 }
 
 size_t ws_bytes(const ModelTable& mt, int cls, int N, int K) {
-    const int nb = mt.caps[3 * cls], no = mt.caps[3 * cls + 1], nc = mt.caps[3 * cls + 2];
+    const int* c = mt.caps + QP_CAPS_W * cls;
+    const int nb = c[0], no = c[1], nc = c[2], nv = c[3] ? mt.nx : 0;
     const int ns = no + nc, ng = no + (nc > 0 ? 1 : 0);
-    return sizeof(double) * (size_t)N * (size_t)qp_ws_doubles(mt.nx, mt.nu, nb, ns, ng, K);
+    return sizeof(double) * (size_t)N * (size_t)qp_ws_doubles(mt.nx, mt.nu, nb, ns, ng, K, nv);
 }
 }  // namespace
 
@@ -93,7 +98,7 @@ extern "C" int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const d
                                      const double* Xref, const double* Uref, const double* x_init,
                                      const double* x_final, const double* tr, const double* coll_rows,
                                      const int32_t* coll_count, double* X, double* U, double* slack_coll,
-                                     double* obj, int32_t* status, int32_t* iters, void* workspace,
+                                     double* nu, double* obj, int32_t* status, int32_t* iters, void* workspace,
                                      size_t workspace_bytes, void* stream) {
     const ModelTable* mt = nullptr;
     int cls = -1;
@@ -106,6 +111,7 @@ extern "C" int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const d
     if (tpl->w_final < 0.0 || (tpl->w_final > 0.0 && tpl->has_final))
         return set_error(SCVX_EINVAL, "qp: w_final > 0 (soft terminal) needs has_final = 0");
     if (tpl->j_max > 0 && (!coll_rows || !coll_count)) return set_error(SCVX_EINVAL, "qp: collision rows required");
+    if (tpl->w_nu > 0.0 && !nu) return set_error(SCVX_EINVAL, "qp: nu output required (w_nu > 0)");
     const size_t need = ws_bytes(*mt, cls, N, tpl->K);
     if (!workspace || workspace_bytes < need) return set_error(SCVX_EWORKSPACE, "qp: workspace too small");
     QPArgs a{};
@@ -113,7 +119,7 @@ extern "C" int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const d
     a.N = N;
     a.disc = disc; a.sigma = sigma; a.Xref = Xref; a.Uref = Uref; a.x_init = x_init; a.x_final = x_final;
     a.tr = tr; a.coll_rows = coll_rows; a.coll_count = coll_count;
-    a.X = X; a.U = U; a.slack_coll = slack_coll; a.obj = obj; a.status = status; a.iters = iters;
+    a.X = X; a.U = U; a.slack_coll = slack_coll; a.nu = nu; a.obj = obj; a.status = status; a.iters = iters;
     a.ws = (double*)workspace;
     a.ws_agent = (long long)(need / sizeof(double) / (size_t)N);
     a.trace = g_trace; a.trace_agent = g_trace_agent; a.trace_cap = g_trace_cap;

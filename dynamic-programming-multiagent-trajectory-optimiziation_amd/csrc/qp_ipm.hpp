@@ -60,6 +60,7 @@ struct QPArgs {
     double* X;
     double* U;
     double* slack_coll;
+    double* nu;          // virtual control [N][K-1][n] (w_nu > 0 classes)
     double* obj;
     int32_t* status;
     int32_t* iters;
@@ -71,32 +72,40 @@ struct QPArgs {
 
 // ---- sizes shared by host (workspace / LDS bytes) and device
 constexpr int qp_dstr(int nx, int nu) { return nx * (nx + 2 * nu + 2); }
-constexpr int qp_pkt(int nx, int nu) { return 2 * nx * nx + 4 * nx * nu + nu * nu + nx; }
+constexpr int qp_pkt(int nx, int nu, int nv = 0) { return 2 * nx * nx + 4 * nx * nu + nu * nu + nx + nv; }
 // global (compact) packet: Q as its diagonal + the 3 off-diagonals of the position block, S, R upper
 // packed, e, A, Bt (column-major), C_{t-1} -- expanded to the LDS packet layout by the factor's prefetch
-constexpr int qp_gpk(int nx, int nu) { return (nx + 3) + nx * nu + nu * (nu + 1) / 2 + nx + nx * nx + 2 * nx * nu; }
+// (+ the virtual control's node curvature D, nv doubles)
+constexpr int qp_gpk(int nx, int nu, int nv = 0) {
+    return (nx + 3) + nx * nu + nu * (nu + 1) / 2 + nx + nx * nx + 2 * nx * nu + nv;
+}
 constexpr int qp_even(int x) { return (x + 1) & ~1; }
 // workspace columns (K doubles each: one per node) of a capacity class
-constexpr int qp_ncol(int nx, int nu, int nb, int ns, int ng) {
-    // disc^T | Bt | soft rows | groups | rd | r1a | cP | ub | node state | SOC
+constexpr int qp_ncol(int nx, int nu, int nb, int ns, int ng, int nv = 0) {
+    // disc^T | Bt | soft rows | groups | rd | r1a | cP | ub | node state | SOC | virtual control state
     return qp_dstr(nx, nu) + nx * nu + 4 * ns + 4 * ng + (nx + nu) + ng + ((1 << nu) + 2 * nb + ns + ng) + nu +
-           ((nx + nu) + nx + 2 * (nu + 1) + ng) + (3 * (nu + 1) + 1 + (nu + 1));
+           ((nx + nu) + nx + 2 * (nu + 1) + ng) + (3 * (nu + 1) + 1 + (nu + 1)) + 11 * nv;
 }
-// factor outputs per stage (stage-major block): K, kappa, LD, W2, P, Pi, u, Acl, one junk slot (the
-// global store of lanes without an output of their own)
-constexpr int qp_fbs(int nx, int nu) { return 3 * nu * nx + nu * nu + 3 * nx * nx + nx + 1; }
+// factor outputs per stage (stage-major block): K, kappa, LD, W2, P, Pi, u, Acl, [virtual control: G^-1 P,
+// G^-1 Pi, G^-1, Acl~], one junk slot (the global store of lanes without an output of their own)
+constexpr int qp_fbs(int nx, int nu, int nv = 0) { return 3 * nu * nx + nu * nu + 3 * nx * nx + nx + 4 * nv * nx + 1; }
 // per agent: columns [c][K], packets [K][GPK], factor blocks [K][FBS] -- only the K nodes: lanes >= K
 // address past the end of the buffer (loads read 0, stores are dropped), so the agent's footprint is
 // what its nodes touch (C3: 1024 agents x 199 KB stay inside the 256 MB Infinity Cache)
-constexpr long long qp_ws_doubles(int nx, int nu, int nb, int ns, int ng, int K) {
-    return (long long)K * (qp_ncol(nx, nu, nb, ns, ng) + qp_gpk(nx, nu) + qp_fbs(nx, nu));
+constexpr long long qp_ws_doubles(int nx, int nu, int nb, int ns, int ng, int K, int nv = 0) {
+    return (long long)K * (qp_ncol(nx, nu, nb, ns, ng, nv) + qp_gpk(nx, nu, nv) + qp_fbs(nx, nu, nv));
 }
 // byte offset of every access of a lane without a node (t >= K): beyond num_records of any workspace
 constexpr int QP_OOB = 0x40000000;
 
-template <int NX_, int NU_, int NB_, int NO_, int NC_>
+// VC_ = 1: the virtual-control class (scvx_qp_template.w_nu > 0): nu_t in every dynamics row, priced
+// w_nu ||nu_t||_1 through its epigraph -e <= nu <= e.  nu is eliminated inside each Riccati stage
+// (G = D + P_{t+1}, D = the node's nu curvature after e is eliminated), e and the 2 n rows per node
+// live in workspace columns, not in the LDS row state.
+template <int NX_, int NU_, int NB_, int NO_, int NC_, int VC_ = 0>
 struct QPCfg {
-    static constexpr int NX = NX_, NU = NU_, NB = NB_, NO = NO_, NC = NC_;
+    static constexpr int NX = NX_, NU = NU_, NB = NB_, NO = NO_, NC = NC_, VC = VC_;
+    static constexpr int NV = VC_ ? NX_ : 0, NVA = NV > 0 ? NV : 1;
     static constexpr int NZ = NX + NU, NQ = NU + 1, NTR = 1 << NU;
     static constexpr int NS = NO + NC;                // soft halfspace rows
     static constexpr int NG = NO + (NC > 0 ? 1 : 0);  // slack groups (one per obstacle, one shared)
@@ -108,14 +117,14 @@ struct QPCfg {
     // phases then reads two contiguous LDS vectors.
     static constexpr int P_Q = 0, P_S = P_Q + NX * NX, P_R = P_S + NX * NU, P_E = P_R + NU * NU,
                          P_A = P_E + NX, P_BT = P_A + NX * NX, P_BTR = P_BT + NX * NU, P_C = P_BTR + NX * NU,
-                         PKT = P_C + NX * NU;
-    static_assert(PKT == qp_pkt(NX, NU), "packet size");
+                         P_D = P_C + NX * NU, PKT = P_D + NV;
+    static_assert(PKT == qp_pkt(NX, NU, NV), "packet size");
     // global packet (compact; qp_gpk): Q diagonal | Q position-block off-diagonals (0,1) (0,2) (1,2) |
     // S | R upper packed | e | A (column-major) | Bt (column-major) | C_{t-1} (column-major)
     static constexpr int G_QD = 0, G_QO = G_QD + NX, G_S = G_QO + 3, G_R = G_S + NX * NU,
                          G_E = G_R + NU * (NU + 1) / 2, G_A = G_E + NX, G_BT = G_A + NX * NX, G_C = G_BT + NX * NU,
-                         GPK = G_C + NX * NU;
-    static_assert(GPK == qp_gpk(NX, NU), "global packet size");
+                         G_D = G_C + NX * NU, GPK = G_D + NV;
+    static_assert(GPK == qp_gpk(NX, NU, NV), "global packet size");
     static_assert(NX >= 3, "the position block is 3 x 3");
     // global packet element of LDS packet element e (-1: a structural zero)
     static constexpr int gsrc(int e) {
@@ -137,7 +146,8 @@ struct QPCfg {
             const int i = (e - P_BTR) / NU, j = (e - P_BTR) % NU;
             return G_BT + j * NX + i;
         }
-        return G_C + (e - P_C);
+        if (e < P_D) return G_C + (e - P_C);
+        return G_D + (e - P_D);
     }
     static_assert(NX <= 16, "the solve chains broadcast within one 16-lane row");
     // factor outputs: stage-major blocks [t][FBS] (coalesced stores from the element-parallel
@@ -150,9 +160,14 @@ struct QPCfg {
     static constexpr int B_PI = B_P + NX * NX;     // Pi_t
     static constexpr int B_U = B_PI + NX * NX;     // P_{t+1} e_t
     static constexpr int B_ACL = B_U + NX;         // Acl_t = A_t + Bt_t K_t (row-major)
-    static constexpr int B_JNK = B_ACL + NX * NX;  // junk slot (stores of lanes without an output)
+    // virtual control (VC): G^-1 P_{t+1}, G^-1 Pi_{t+1}, G^-1 (column-major), the chain matrix
+    // Acl~ = G^-1 D Acl (row-major)
+    static constexpr int B_YP = B_ACL + NX * NX, B_YPI = B_YP + NV * NX, B_GI = B_YPI + NV * NX,
+                         B_ACL2 = B_GI + NV * NX;
+    static constexpr int B_CH = NV > 0 ? B_ACL2 : B_ACL;  // what the solve chains read
+    static constexpr int B_JNK = B_ACL2 + NV * NX;  // junk slot (stores of lanes without an output)
     static constexpr int FBS = B_JNK + 1;
-    static_assert(FBS == qp_fbs(NX, NU), "factor block");
+    static_assert(FBS == qp_fbs(NX, NU, NV), "factor block");
     // stage-minor workspace columns
     static constexpr int C_DT = 0;                 // disc, transposed: A (col-major) | B | C | S | z
     static constexpr int C_BT = C_DT + DSTR;       // Bt_t (row-major)
@@ -168,21 +183,30 @@ struct QPCfg {
     // SOC scaling of the current iteration: w (NQ), eta, W lam (NQ), rc (NQ), rho (NQ)
     static constexpr int C_WV = C_AV + NG, C_ETA = C_WV + NQ, C_LTQ = C_ETA + 1, C_RCQ = C_LTQ + NQ,
                          C_RHO = C_RCQ + NQ;
-    static constexpr int NCOL = C_RHO + NQ;
-    static_assert(NCOL == qp_ncol(NX, NU, NB, NS, NG), "column count");
+    // virtual control state (lanes t < K-1): nu, e, slacks s1 s2 and duals l1 l2 of the rows nu - e <= 0,
+    // -nu - e <= 0, the e part of the Newton rhs, the predictor products of the two rows, the dual residual
+    // (nu, e parts)
+    static constexpr int C_VN = C_RHO + NQ, C_VE = C_VN + NV, C_VS = C_VE + NV, C_VL = C_VS + 2 * NV,
+                         C_VRE = C_VL + 2 * NV, C_VCP = C_VRE + NV, C_VRD = C_VCP + 2 * NV;
+    static constexpr int NCOL = C_VRD + 2 * NV;
+    static_assert(NCOL == qp_ncol(NX, NU, NB, NS, NG, NV), "column count");
     // LDS (doubles, compile-time offsets except the K-sized blocks at the end):
     // factor: the current stage's packet, P', Pi' (col-major), T1, T2 (col-major), W1, W2 (col-major), Qh,
     // Sh (col-major), Rh, [K | kappa] (col-major), sink
     static constexpr int F_RING = 0, F_PP = PKT, F_PIP = F_PP + NX * NX, F_T1 = F_PIP + NX * NX,
                          F_T2 = F_T1 + NX * NX, F_W1 = F_T2 + NX * NU, F_W2 = F_W1 + NX * NX,
                          F_QH = F_W2 + NU * NX, F_SH = F_QH + NX * NX, F_RH = F_SH + NU * NX,
-                         F_KK = F_RH + NU * NU, F_SINK = F_KK + 2 * NU * NX, F_END = qp_even(F_SINK + 8);
+                         F_KK = F_RH + NU * NU, F_SINK = F_KK + 2 * NU * NX,
+                         // virtual control: G^-1 P, G^-1 Pi (column-major), Z = G^-1 D (row-major), Acl (column-major)
+                         F_YP = F_SINK + (NX > 8 ? NX : 8), F_YPI = F_YP + NV * NX, F_Z = F_YPI + NV * NX,
+                         F_ACLC = F_Z + NV * NX, F_END = qp_even(F_ACLC + NV * NX);
     static constexpr int L_M = F_END, L_PI0 = L_M + NX * NX, L_XE = L_PI0 + NX * NX, L_XI0 = L_XE + NX,
                          L_R2F = L_XI0 + NX, L_YI = L_R2F + NX, L_YF = L_YI + NX, L_DYI = L_YF + NX,
                          L_DYF = L_DYI + NX, L_PIV = L_DYF + NX, L_ONE = L_PIV + NX, L_FLAG = L_ONE + 1,
                          L_ST = qp_even(L_FLAG + 4), L_S = L_ST + 16, L_L = L_S + NR * 64, L_VAR = L_L + NR * 64;
     // row slacks s / duals lambda [r][lane]; then K-sized: chain offsets g/f [K][NX], chain vectors [K+1][NX]
     static constexpr int lds_doubles(int K) { return L_VAR + K * NX + (K + 1) * NX; }
+    static_assert(4 * NV <= WAVE, "virtual control: one Gauss-Jordan column per lane");
 };
 
 // packed phase descriptors (all operands are contiguous LDS vectors; the stage packet always sits at
@@ -286,7 +310,7 @@ __device__ __forceinline__ void qp_phase(double* lds, const QPRep (&d)[NREP], do
 template <class C>
 __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     constexpr int NX = C::NX, NU = C::NU, NZ = C::NZ, NQ = C::NQ, NR = C::NR, NG = C::NG, NS = C::NS,
-                  NO = C::NO, NC = C::NC, NB = C::NB, PKT = C::PKT;
+                  NO = C::NO, NC = C::NC, NB = C::NB, PKT = C::PKT, NV = C::NV, NVA = C::NVA;
     constexpr int NGA = NG > 0 ? NG : 1, NSA = NS > 0 ? NS : 1, NBA = NB > 0 ? NB : 1;
     extern __shared__ double lds[];
     const scvx_qp_template& T = a.T;
@@ -314,7 +338,29 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     if (soft_fin) {
         for (int i = 0; i < NX; ++i) qnorm = fmax(qnorm, 2.0 * T.w_final * fabs(a.x_final[agent * NX + i]));
     }
+    // virtual control (VC classes): weight of the epigraph variables e; lanes t < K-1 carry nu_t
+    if (NV > 0) qnorm = fmax(qnorm, T.w_nu);
+    const bool vact = NV > 0 && act && t < K - 1;
+    // proximal term w_prox ||x_t - xbar_t||^2 (every node): linear term -2 w_prox xbar_t
+    const bool prox = T.w_prox > 0.0;
+    if (prox) {
+        double qp = 0.0;
+        for (int i = 0; i < NX; ++i) qp = fmax(qp, act ? 2.0 * T.w_prox * fabs(a.Xref[(agent * K + (act ? t : 0)) * NX + i]) : 0.0);
+        qnorm = fmax(qnorm, wave_max(qp));
+    }
     const double osc = fmax(1.0, qnorm), iosc = 1.0 / osc;
+    const double wnu = NV > 0 ? T.w_nu * iosc : 0.0;
+    const double wpx = (prox && act) ? T.w_prox * iosc : 0.0;
+    // the proximal term's constant w_prox sum ||xbar||^2 (scaled): the gap tests use the true objective
+    double cpx = 0.0;
+    if (prox) {
+        double v = 0.0;
+        for (int i = 0; i < NX; ++i) {
+            const double xb = act ? a.Xref[(agent * K + t) * NX + i] : 0.0;
+            v = fma(wpx * xb, xb, v);
+        }
+        cpx = wave_sum(v);
+    }
     const double wu = ((t < K - 1) ? 1.0 : T.w_last) * iosc;
     const bool fixed_u = act && (t == K - 1) && T.fix_last_input;
     const bool tsoft = soft_fin && act && (t == K - 1);
@@ -459,6 +505,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
 #pragma unroll
         for (int g = 0; g < NG; ++g) cst(C::C_AV + g, 0.0);
+#pragma unroll
+        for (int i = 0; i < NV; ++i) { cst(C::C_VN + i, 0.0); cst(C::C_VE + i, 0.0); }
         if (lane == 0) lds[V_ONE] = 1.0;
         if (lane < NX) { lds[V_YI + lane] = 0.0; lds[V_YF + lane] = 0.0; }
         if (lane < 16) lds[V_ST + lane] = 0.0;
@@ -542,10 +590,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 } else if ((o -= NX * NX) < NX * NX) {  // M += W2' kappa (symmetric)
                     const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
                     L = qp_dpk(C::F_W2 + p * NU, 0); R = qp_dpk(C::F_KK + (NX + q) * NU, 0); O = (V_M + o) | (1 << 15);
-                } else if ((o -= NX * NX) < NX * NX) {  // Acl = A + Bt K  -> LDS Acl block of the stage
+                } else if ((o -= NX * NX) < NX * NX) {  // Acl = A + Bt K  -> global (+ LDS column-major for VC)
                     const int i = o / NX, j = o % NX;
                     L = qp_dpk(C::P_BTR + i * NU, 1); R = qp_dpk(C::F_KK + j * NU, 0);
-                    O = sink | ((C::B_ACL + o + 1) << 17); B = (C::P_A + j * NX + i) | (1 << 15) | (1 << 16);
+                    O = (C::NV > 0 ? C::F_ACLC + j * NX + i : sink) | ((C::B_ACL + o + 1) << 17);
+                    B = (C::P_A + j * NX + i) | (1 << 15) | (1 << 16);
                 }
                 d4[rep][0] = L; d4[rep][1] = R; d4[rep][2] = O; d4[rep][3] = B;
             }
@@ -553,6 +602,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         // decoded once per sweep; accumulating outputs (xe, M) are summed in registers
         QPRep q1[R1], q2[R2], q4[R4];
         double a1[R1], a2[R2], a4[R4];
+        // virtual control: the M contributions -Pi'' G^-1 Pi' of every stage (registers, like a4)
+        constexpr int R0 = (NX * NX + WAVE - 1) / WAVE;
+        double amv[R0];
+#pragma unroll
+        for (int r = 0; r < R0; ++r) amv[r] = 0.0;
 #pragma unroll
         for (int r = 0; r < R1; ++r) { q1[r] = qp_decode(d1[r], V_ONE, C::F_SINK, C::B_JNK); a1[r] = 0.0; }
 #pragma unroll
@@ -599,6 +653,62 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             const double blast = last ? 1.0 : 0.0;
             const int fbo = FBB + ts * C::FBS * 8;  // byte offset of this stage's output block (uniform)
             pf_load(ts - 3, nb);  // unconditional: stage K-1 re-issues K-4, ts-3 < 0 reads zeros
+            if constexpr (C::NV > 0) {
+                // ---- phase 0 (virtual control nu_ts): G = diag(D) + P', then [G^-1 Pi' | G^-1 | G^-1 P'] by
+                // Gauss-Jordan without pivoting (G is SPD): lane c < 4 NX owns column c of [G | Pi' | I | P'];
+                // the pivot column is broadcast by readlane (no LDS round trip per pivot).  At the last stage
+                // P' = Pi' = 0 and D = 1 (assemble), so nothing changes there.
+                const int c = lane < 4 * NX ? lane : 0, blk = c / NX, cc = c - blk * NX;
+                const int base = (blk == 1 ? C::F_PIP : C::F_PP) + cc * NX;   // P' symmetric: row = column
+                const double keep = blk == 2 ? 0.0 : 1.0;
+                const double dcc = lds[C::F_RING + C::P_D + cc];
+                const double diag = (blk == 2 ? 1.0 : 0.0) + (blk == 0 ? dcc : 0.0);
+                double col[NX];
+#pragma unroll
+                for (int i = 0; i < NX; ++i) col[i] = fma(keep, lds[base + i], qp_mask(i, cc) * diag);
+#pragma unroll
+                for (int k = 0; k < NX; ++k) {
+                    double pv[NX];
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) pv[i] = readlane_d(col[i], k);
+                    bad |= !(pv[k] > 0.0);
+                    const double rk = col[k] / pv[k];
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) col[i] = (i == k) ? rk : fma(-pv[i], rk, col[i]);
+                }
+                // outputs: G^-1 Pi' -> F_YPI / B_YPI, Z = G^-1 D (row-major) -> F_Z, G^-1 -> B_GI,
+                // G^-1 P' -> F_YP / B_YP (column-major)
+                const bool own = lane >= NX && lane < 4 * NX;
+                const int gcol = blk == 1 ? C::B_YPI : (blk == 2 ? C::B_GI : C::B_YP);
+#pragma unroll
+                for (int i = 0; i < NX; ++i) {
+                    const int lo = !own ? C::F_SINK + i
+                                        : (blk == 1 ? C::F_YPI + cc * NX + i
+                                                    : (blk == 2 ? C::F_Z + i * NX + cc : C::F_YP + cc * NX + i));
+                    lds[lo] = blk == 2 ? col[i] * dcc : col[i];
+                    wb.st((own ? gcol + cc * NX + i : C::B_JNK) * 8, fbo, col[i]);
+                }
+                wsync();
+                // P~ = D G^-1 P' (symmetrised) -> F_PP; M -= Pi'' G^-1 Pi' (registers)
+#pragma unroll
+                for (int r = 0; r < R0; ++r) {
+                    const int o = lane + r * WAVE, oo = o < NX * NX ? o : 0, i = oo / NX, j = oo - i * NX;
+                    const double pt = 0.5 * (lds[C::F_RING + C::P_D + i] * lds[C::F_YP + j * NX + i] +
+                                             lds[C::F_RING + C::P_D + j] * lds[C::F_YP + i * NX + j]);
+                    const double mv = qp_dot<NX>(lds, C::F_PIP + i * NX, C::F_YPI + j * NX);
+                    amv[r] -= o < NX * NX ? mv : 0.0;
+                    lds[o < NX * NX ? C::F_PP + o : C::F_SINK] = pt;
+                }
+                wsync();
+                // Pi~ = D G^-1 Pi' -> F_PIP (column-major: element o = j NX + i is row i)
+#pragma unroll
+                for (int r = 0; r < R0; ++r) {
+                    const int o = lane + r * WAVE, oo = o < NX * NX ? o : 0;
+                    const double v = lds[C::F_RING + C::P_D + (oo % NX)] * lds[C::F_YPI + oo];
+                    lds[o < NX * NX ? C::F_PIP + o : C::F_SINK] = v;
+                }
+                wsync();
+            }
             // ---- phase 1: T1 = P'A, T2 = P'Bt, W1 = A'Pi', W2 = Bt'Pi', u = P'e, xe += Pi''e
             qp_phase<NX, R1>(lds, q1, blast, wb, fbo, a1);
             wsync();
@@ -686,6 +796,16 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             qp_phase<NU, R4>(lds, q4, blast, wb, fbo, a4);
             if (ts > 0) pf_store(ts - 1, cb);
             wsync();
+            if constexpr (C::NV > 0) {
+                // ---- phase 5 (virtual control): the chain matrix Acl~ = G^-1 D Acl -> global (row-major)
+#pragma unroll
+                for (int r = 0; r < R0; ++r) {
+                    const int o = lane + r * WAVE, oo = o < NX * NX ? o : 0, i = oo / NX, j = oo - i * NX;
+                    const double v = qp_dot<NX>(lds, C::F_Z + i * NX, C::F_ACLC + j * NX);
+                    wb.st((o < NX * NX ? C::B_ACL2 + o : C::B_JNK) * 8, fbo, v);
+                }
+                wsync();
+            }
         };
         // stage K-1's packet is in LDS, K-2 in pf[1], K-3 in pf[2], K-4 in pf[0]
         int ts = K - 1;
@@ -708,6 +828,14 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         for (int r = 0; r < R4; ++r)
             if (d4[r][2] >= 0 && ((d4[r][2] >> 15) & 1)) lds[d4[r][2] & 0x7FFF] = a4[r];
         wsync();
+        if constexpr (C::NV > 0) {
+#pragma unroll
+            for (int r = 0; r < R0; ++r) {
+                const int o = lane + r * WAVE;
+                if (o < NX * NX) lds[V_M + o] += amv[r];
+            }
+            wsync();
+        }
         // Pi_0 -> persistent; LU with partial pivoting of M (lane 0, registers)
         for (int e = lane; e < NX * NX; e += WAVE) lds[V_PI0 + e] = lds[C::F_PIP + (e % NX) * NX + e / NX];
         if (fin && lane == 0) {
@@ -753,16 +881,32 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     };
 
     // ------------------------------------------------------------------ solve (one Newton rhs)
-    // In: q (NX), r (NU) of this node (registers), e (packet), V_XI0 / V_R2F (LDS).
-    // Out: dzo (NZ) = (dx_t, du_t), dyo (NX) = dy_t of this lane; V_DYI / V_DYF (LDS) the
+    // In: q (NX), r (NU), dv (NV: the linear term of nu_t, VC classes) of this node (registers), e (packet),
+    // V_XI0 / V_R2F (LDS).
+    // Out: dzo (NZ) = (dx_t, du_t), dyo (NX) = dy_t, dno (NV) = dnu_t of this lane; V_DYI / V_DYF (LDS) the
     // initial / terminal multiplier directions.  Assumes a __syncthreads() since the factor.
-    auto solve = [&](const double* q, const double* r, double* dzo, double* dyo) __attribute__((always_inline)) {
-        // ---- backward pre-pass: g = q + K'r + Acl'(P_{t+1} e)
+    // Virtual control: stage t sees P~ = D G^-1 P_{t+1} and p~ = p_{t+1} - (G^-1 P)'(p_{t+1} + d) in place of
+    // P_{t+1}, p_{t+1} (oracle/scvx_cpu.cpp riccati_factor), the chains run on Acl~ = G^-1 D Acl, and
+    // nu_t = xi_{t+1} - (A xi_t + Bt du_t + e_t) comes out of the forward chain.
+    auto solve = [&](const double* q, const double* r, const double* dv, double* dzo, double* dyo, double* dno)
+                     __attribute__((always_inline)) {
+        // ---- backward pre-pass: g = q + K'r + Acl'(P~ e - (G^-1 P)'d)
         fresh();
         if (act) {
-            double g[NX], Kt[NU * NX], u[NX], Ac[NX * NX];
-            ldb(Kt, C::B_K, NU * NX);
+            double g[NX], u[NX];
             ldb(u, C::B_U, NX);
+            if constexpr (NV > 0) {
+                double Y[NX * NX];
+                ldb(Y, C::B_YP, NX * NX);
+                hold(u, NX);
+                hold(Y, NX * NX);
+#pragma unroll
+                for (int j = 0; j < NX; ++j)
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) u[j] = fma(-Y[j * NX + i], dv[i], u[j]);
+            }
+            double Kt[NU * NX], Ac[NX * NX];
+            ldb(Kt, C::B_K, NU * NX);
             ldb(Ac, C::B_ACL, NX * NX);
             hold(Kt, NU * NX);
             hold(u, NX);
@@ -787,8 +931,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         // ---- backward chain p_t = Acl_t' p_{t+1} + g_t (lane i: element i); p_{t+1} broadcast
         // from lanes 0..NX-1 by a DPP row broadcast (NX <= 16), the Acl column / g of the next stage read ahead
         if (lane < NX) {
-            // lane i needs column i of Acl_t (stage block, B_ACL + k*NX + i)
-            const int va = (C::B_ACL + lane) * 8;
+            // lane i needs column i of Acl_t (stage block, B_CH + k*NX + i; Acl~ for VC)
+            const int va = (C::B_CH + lane) * 8;
             auto ldA = [&](int ts, double* an, double& gn) __attribute__((always_inline)) {
                 const int tc = ts > 0 ? ts : 0;
 #pragma unroll
@@ -851,9 +995,30 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
             for (int j = 0; j < NU; ++j) rh[j] = r[j];
             if (t < K - 1) {
+                double pn[NX];
+#pragma unroll
+                for (int i = 0; i < NX; ++i) pn[i] = lds[V_CH + (t + 1) * NX + i];
+                if constexpr (NV > 0) {
+                    // p~ = p - (G^-1 P)'(p + d);  xacc -= (G^-1 Pi)'(p + d)
+                    double Y[NX * NX], w[NX];
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) w[i] = pn[i] + dv[i];
+                    ldb(Y, C::B_YP, NX * NX);
+                    hold(Y, NX * NX);
+#pragma unroll
+                    for (int j = 0; j < NX; ++j)
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) pn[j] = fma(-Y[j * NX + i], w[i], pn[j]);
+                    ldb(Y, C::B_YPI, NX * NX);
+                    hold(Y, NX * NX);
+#pragma unroll
+                    for (int j = 0; j < NX; ++j)
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) xa[j] = fma(-Y[j * NX + i], w[i], xa[j]);
+                }
 #pragma unroll
                 for (int i = 0; i < NX; ++i) {
-                    const double h = uu[i] + lds[V_CH + (t + 1) * NX + i];
+                    const double h = uu[i] + pn[i];
 #pragma unroll
                     for (int j = 0; j < NU; ++j) rh[j] = fma(Bt[i * NU + j], h, rh[j]);
                 }
@@ -938,21 +1103,45 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                 for (int j = 0; j < NX; ++j) piv[i] = fma(Pi[i * NX + j], mu[j], piv[i]);
             if (t < K - 1) {
+                double fv[NX];
 #pragma unroll
                 for (int i = 0; i < NX; ++i) {
                     double f = ev[i];
 #pragma unroll
                     for (int j = 0; j < NU; ++j) f = fma(Bt[i * NU + j], v0[j], f);
-                    lds[V_G + t * NX + i] = f;
+                    fv[i] = f;
                 }
+                if constexpr (NV > 0) {
+                    // f~ = G^-1 (D o f - p_{t+1} - d) - (G^-1 Pi) mu   (V_CH still holds the backward chain)
+                    double Y[NX * NX], w[NX];
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) w[i] = fma(pld(C::G_D + i), fv[i], -lds[V_CH + (t + 1) * NX + i] - dv[i]);
+                    ldb(Y, C::B_GI, NX * NX);
+                    hold(Y, NX * NX);
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) {
+                        double v = 0.0;
+#pragma unroll
+                        for (int j = 0; j < NX; ++j) v = fma(Y[j * NX + i], w[j], v);
+                        fv[i] = v;
+                    }
+                    ldb(Y, C::B_YPI, NX * NX);
+                    hold(Y, NX * NX);
+#pragma unroll
+                    for (int i = 0; i < NX; ++i)
+#pragma unroll
+                        for (int j = 0; j < NX; ++j) fv[i] = fma(-Y[j * NX + i], mu[j], fv[i]);
+                }
+#pragma unroll
+                for (int i = 0; i < NX; ++i) lds[V_G + t * NX + i] = fv[i];
             }
         }
         wsync();
         stamp(7);
         // ---- forward chain xi_{t+1} = Acl_t xi_t + f_t
         if (lane < NX) {
-            // lane i needs row i of Acl_t (stage block, B_ACL + i*NX + k)
-            const int va = (C::B_ACL + lane * NX) * 8;
+            // lane i needs row i of Acl_t (stage block, B_CH + i*NX + k; Acl~ for VC)
+            const int va = (C::B_CH + lane * NX) * 8;
             auto ldA = [&](int ts, double* an, double& fn) __attribute__((always_inline)) {
                 const int tc = ts < K - 1 ? ts : K - 2;
 #pragma unroll
@@ -997,6 +1186,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         for (int i = 0; i < NX; ++i) ym[i] = 0.0;
 #pragma unroll
         for (int i = 0; i < NZ; ++i) dzo[i] = 0.0;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) dno[i] = 0.0;
         if (act) {
             double xi[NX], Cp[NX * NU], Kt[NU * NX], P[NX * NX];
             ldb(Kt, C::B_K, NU * NX);
@@ -1026,6 +1217,24 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             }
 #pragma unroll
             for (int j = 0; j < NU; ++j) dzo[NX + j] = du[j];
+            if constexpr (NV > 0) {
+                // dnu_t = xi_{t+1} - (A xi_t + Bt du_t + e_t)
+                double Ad[NX * NX], Bt[NX * NU], ev[NX];
+                ldn(Ad, C::C_DT, NX * NX);
+                ldn(Bt, C::C_BT, NX * NU);
+#pragma unroll
+                for (int i = 0; i < NX; ++i) ev[i] = pld(C::G_E + i);
+                hold(Ad, NX * NX); hold(Bt, NX * NU); hold(ev, NX);
+#pragma unroll
+                for (int i = 0; i < NX; ++i) {
+                    double v = lds[V_CH + (t + 1) * NX + i] - ev[i];
+#pragma unroll
+                    for (int k = 0; k < NX; ++k) v = fma(-Ad[k * NX + i], xi[k], v);
+#pragma unroll
+                    for (int j = 0; j < NU; ++j) v = fma(-Bt[i * NU + j], du[j], v);
+                    dno[i] = (t < K - 1) ? v : 0.0;
+                }
+            }
         }
         // lane t computed y_{t-1}: lane t owns y_t (from lane t+1); lane 0's is the initial multiplier
 #pragma unroll
@@ -1041,6 +1250,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     // Phase-local register copies: every node phase loads what it uses as one batch and stores
     // what it changes, so no node-sized state is live across the sweeps.
     double z[NZ], y[NX], sq[NQ], lq[NQ], av[NGA], ub[NU], sg[NSA][3], sb[NSA];
+    // virtual control state of this node (VC classes, lanes t < K-1): nu, e, and per component the slacks /
+    // duals of the rows nu - e <= 0 (index 2i) and -nu - e <= 0 (2i + 1)
+    double vn[NVA], ve[NVA], vs[2 * NVA], vl[2 * NVA];
     // row slacks s_r and duals lambda_r of this node: LDS [r][lane]
     auto s_ = [&](int r) __attribute__((always_inline)) -> double& { return lds[V_S + r * WAVE + lane]; };
     auto l_ = [&](int r) __attribute__((always_inline)) -> double& { return lds[V_L + r * WAVE + lane]; };
@@ -1062,9 +1274,17 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             for (int i = 0; i < 3; ++i) sg[q][i] = cld(C::C_SOFT + q * 4 + i);
             sb[q] = cld(C::C_SOFT + q * 4 + 3);
         }
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            vn[i] = cld(C::C_VN + i);
+            ve[i] = cld(C::C_VE + i);
+            vs[2 * i] = cld(C::C_VS + 2 * i); vs[2 * i + 1] = cld(C::C_VS + 2 * i + 1);
+            vl[2 * i] = cld(C::C_VL + 2 * i); vl[2 * i + 1] = cld(C::C_VL + 2 * i + 1);
+        }
     };
     auto hold_state = [&]() __attribute__((always_inline)) {
         hold(z, NZ); hold(y, NX); hold(sq, NQ); hold(lq, NQ); hold(av, NGA); hold(ub, NU);
+        if (NV > 0) { hold(vn, NV); hold(ve, NV); hold(vs, 2 * NV); hold(vl, 2 * NV); }
 #pragma unroll
         for (int q = 0; q < NS; ++q) { hold(sg[q], 3); hold(&sb[q], 1); }
 #pragma unroll
@@ -1084,6 +1304,13 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         for (int j = 0; j < NQ; ++j) { cst(C::C_SQ + j, sq[j]); cst(C::C_LQ + j, lq[j]); }
 #pragma unroll
         for (int g = 0; g < NG; ++g) cst(C::C_AV + g, av[g]);
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            cst(C::C_VN + i, vn[i]);
+            cst(C::C_VE + i, ve[i]);
+            cst(C::C_VS + 2 * i, vs[2 * i]); cst(C::C_VS + 2 * i + 1, vs[2 * i + 1]);
+            cst(C::C_VL + 2 * i, vl[2 * i]); cst(C::C_VL + 2 * i + 1, vl[2 * i + 1]);
+        }
     };
     auto grp_on = [&](int g) __attribute__((always_inline)) -> bool { return ineq && (g < NO ? g < nobs : has_coll); };
     auto row_on = [&](int r) __attribute__((always_inline)) -> bool {
@@ -1155,16 +1382,16 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     auto assemble = [&](bool unit, const double* Wi2uu, const double* rp) __attribute__((always_inline)) {
         double dbox[NX], Hpp[3][3], Huu[NU * NU];
 #pragma unroll
-        for (int i = 0; i < NX; ++i) dbox[i] = 2.0 * wfs;
+        for (int i = 0; i < NX; ++i) dbox[i] = 2.0 * (wfs + wpx);
 #pragma unroll
         for (int i = 0; i < 3; ++i) Hpp[i][0] = Hpp[i][1] = Hpp[i][2] = 0.0;
 #pragma unroll
         for (int i = 0; i < NU; ++i)
 #pragma unroll
             for (int j = 0; j < NU; ++j) Huu[i * NU + j] = (i == j ? 2.0 * wu : 0.0) + (soc ? Wi2uu[i * NU + j] : 0.0);
-        double Haa[NGA], Hpa[NGA][3];
+        double Haa[NGA], Hpa[NGA][3], D0[NGA];
 #pragma unroll
-        for (int g = 0; g < NGA; ++g) { Haa[g] = 0.0; Hpa[g][0] = Hpa[g][1] = Hpa[g][2] = 0.0; }
+        for (int g = 0; g < NGA; ++g) { Haa[g] = 0.0; D0[g] = 0.0; Hpa[g][0] = Hpa[g][1] = Hpa[g][2] = 0.0; }
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
             const double Dr = row_on(r) ? (unit ? 1.0 : l_(r) / s_(r)) : 0.0;
@@ -1179,31 +1406,55 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 for (int i = 0; i < NX; ++i) dbox[i] = fma(qp_mask(i, idx), Dr, dbox[i]);
             } else if (r < C::R_GRP) {
                 const int q = r - C::R_OBS, g = q < NO ? q : NO;
-#pragma unroll
-                for (int i = 0; i < 3; ++i)
-#pragma unroll
-                    for (int j = 0; j < 3; ++j) Hpp[i][j] += Dr * sg[q][i] * sg[q][j];
                 Haa[g] += Dr;
 #pragma unroll
                 for (int i = 0; i < 3; ++i) Hpa[g][i] += Dr * sg[q][i];
             } else {
                 Haa[r - C::R_GRP] += Dr;
+                D0[r - C::R_GRP] = Dr;
             }
         }
+        // slack groups eliminated: the position block gains H_pp - H_pa H_aa^-1 H_ap, written as the weighted
+        // covariance sum_r D_r (sg_r - hp)(sg_r - hp)' + D_0 hp hp' (hp = H_pa / H_aa, D_0 the slack's sign row):
+        // a sum of PSD terms.  The direct difference cancels once an active row's barrier weight dominates
+        // (D1 D2 / (D1 + D2) computed as D1 - D1^2 / (D1 + D2)) and broke the factorisation of the C3 agents
+        // whose obstacle slack is active at the optimum (oracle/scvx_cpu.cpp node_zz, the same form).
+        double hp[NGA][3];
 #pragma unroll
-        for (int g = 0; g < NG; ++g) {
-            const bool on = grp_on(g);
-            const double ih = on ? 1.0 / Haa[g] : 0.0;
-            double hp[3];
+        for (int g = 0; g < NGA; ++g) {
+            const double ih = (g < NG && grp_on(g)) ? 1.0 / Haa[g] : 0.0;
 #pragma unroll
-            for (int i = 0; i < 3; ++i) { hp[i] = Hpa[g][i] * ih; cst(C::C_GRP + g * 4 + i, hp[i]); }
-            cst(C::C_GRP + g * 4 + 3, ih);
+            for (int i = 0; i < 3; ++i) hp[g][i] = Hpa[g][i] * ih;
+            if (g < NG) {
+#pragma unroll
+                for (int i = 0; i < 3; ++i) cst(C::C_GRP + g * 4 + i, hp[g][i]);
+                cst(C::C_GRP + g * 4 + 3, ih);
+            }
 #pragma unroll
             for (int i = 0; i < 3; ++i)
 #pragma unroll
-                for (int j = 0; j < 3; ++j) Hpp[i][j] -= hp[i] * Hpa[g][j];
+                for (int j = 0; j < 3; ++j) Hpp[i][j] = fma(D0[g] * hp[g][i], hp[g][j], Hpp[i][j]);
+        }
+#pragma unroll
+        for (int r = C::R_OBS; r < C::R_GRP; ++r) {
+            const double Dr = row_on(r) ? (unit ? 1.0 : l_(r) / s_(r)) : 0.0;
+            const int q = r - C::R_OBS, g = q < NO ? q : NO;
+            double c[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) c[i] = sg[q][i] - hp[g][i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) Hpp[i][j] = fma(Dr * c[i], c[j], Hpp[i][j]);
         }
         if (!act) return;
+        // virtual control: nu's curvature after its epigraph variable is eliminated, 4 D1 D2 / (D1 + D2)
+        // (D = l/s of the rows nu - e <= 0, -nu - e <= 0; 2 at unit scaling); 1 at the last node (no nu)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            const double d1 = unit ? 1.0 : vl[2 * i] / vs[2 * i], d2 = unit ? 1.0 : vl[2 * i + 1] / vs[2 * i + 1];
+            pst(C::G_D + i, vact ? 4.0 * d1 * d2 / (d1 + d2) : 1.0);
+        }
         double Q[NX * NX], Cp[NX * NU];
         load_cp(Cp);
 #pragma unroll
@@ -1396,14 +1647,22 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         set_boundary(z);
         if (!factor()) { status = SCVX_STATUS_NUMERICAL; fail_code = 1.0; }
         __syncthreads();  // factor columns (global) -> lane-parallel solve passes
-        double dz[NZ], dy[NX], da[NGA];
-        solve(q, rr, dz, dy);
+        double dz[NZ], dy[NX], da[NGA], dv0[NVA], dnv[NVA];
+        // virtual control at unit scaling from nu = e = 0: nu's rhs is 0 (the two rows cancel), e's is -w_nu
+#pragma unroll
+        for (int i = 0; i < NVA; ++i) dv0[i] = 0.0;
+        solve(q, rr, dv0, dz, dy, dnv);
         recover_aux(dz, da);
         load_state();
 #pragma unroll
         for (int i = 0; i < NZ; ++i) z[i] += act ? dz[i] : 0.0;
 #pragma unroll
         for (int g = 0; g < NGA; ++g) av[g] += da[g];
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            vn[i] = vact ? dnv[i] : 0.0;
+            ve[i] = vact ? -0.5 * wnu : 0.0;   // (r_e - b dnu) / a with a = 2, b = 0
+        }
         double smin = 1e300, lmin = 1e300;
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
@@ -1424,6 +1683,15 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             smin = fmin(smin, T.u_max - sqrt(nu2));
             lmin = fmin(lmin, -T.u_max - sqrt(nu2));
         }
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {   // s = h - Gz, lambda = Gz - h of the rows nu - e <= 0, -nu - e <= 0
+            vs[2 * i] = ve[i] - vn[i]; vl[2 * i] = vn[i] - ve[i];
+            vs[2 * i + 1] = ve[i] + vn[i]; vl[2 * i + 1] = -vn[i] - ve[i];
+            if (vact) {
+                smin = fmin(smin, fmin(vs[2 * i], vs[2 * i + 1]));
+                lmin = fmin(lmin, fmin(vl[2 * i], vl[2 * i + 1]));
+            }
+        }
         smin = wave_min(smin); lmin = wave_min(lmin);
         const double shs = fmax(0.0, 1.0 - smin), shl = fmax(0.0, 1.0 - lmin);
 #pragma unroll
@@ -1431,12 +1699,15 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             if (row_on(r)) { s_(r) += shs; l_(r) += shl; }
         }
         if (soc) { sq[0] += shs; lq[0] += shl; }
+#pragma unroll
+        for (int i = 0; i < 2 * NV; ++i) { vs[i] = vact ? vs[i] + shs : 1.0; vl[i] = vact ? vl[i] + shl : 0.0; }
         store_state();
     }
     double degl = 0.0;
 #pragma unroll
     for (int r = 0; r < NR; ++r) degl += row_on(r) ? 1.0 : 0.0;
     degl += soc ? 1.0 : 0.0;
+    degl += vact ? 2.0 * NV : 0.0;
     const double deg = fmax(wave_sum(degl), 1.0);
     const double tol = T.tol > 0 ? T.tol : 1e-9;
 
@@ -1457,6 +1728,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         hold(dt, C::DSTR);
         double rp[NX];
         dyn_residual(z, dt, rp);
+#pragma unroll
+        for (int i = 0; i < NV; ++i) rp[i] -= vact ? vn[i] : 0.0;   // + nu_t in the dynamics
         // dual residual rd = Pz + q + A'y + G'lam (z and group parts)
         double rd[NZ], rda[NGA];
         // residual norms and Clarabel's normalisation of them (the solver dist_scvx_3d.py:110 calls):
@@ -1497,7 +1770,10 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             }
         }
 #pragma unroll
-        for (int i = 0; i < NX; ++i) rd[i] = tsoft ? 2.0 * wfs * (z[i] - a.x_final[agent * NX + i]) : 0.0;
+        for (int i = 0; i < NX; ++i) {
+            rd[i] = tsoft ? 2.0 * wfs * (z[i] - a.x_final[agent * NX + i]) : 0.0;
+            if (prox) rd[i] = fma(2.0 * wpx, z[i] - a.Xref[(agent * K + (act ? t : 0)) * NX + i], rd[i]);
+        }
 #pragma unroll
         for (int j = 0; j < NU; ++j) rd[NX + j] = 2.0 * wu * z[NX + j];
 #pragma unroll
@@ -1570,6 +1846,26 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 }
 #pragma unroll
                 for (int i = 0; i < NZ; ++i) { dres = fmax(dres, fabs(rd[i])); cst(C::C_RD + i, rd[i]); }
+                if (vact) {   // virtual control rows nu - e + s1 = 0, -nu - e + s2 = 0; rd = (-y + l1 - l2, w_nu - l1 - l2)
+#pragma unroll
+                    for (int i = 0; i < NV; ++i) {
+                        const double rc1 = vn[i] - ve[i] + vs[2 * i], rc2 = -vn[i] - ve[i] + vs[2 * i + 1];
+                        pres = fmax(pres, fmax(fabs(rc1), fabs(rc2)));
+                        nsl = fmax(nsl, fmax(vs[2 * i], vs[2 * i + 1]));
+                        nzd = fmax(nzd, fmax(vl[2 * i], vl[2 * i + 1]));
+                        nxv = fmax(nxv, fmax(fabs(vn[i]), fabs(ve[i])));
+                        gap += vs[2 * i] * vl[2 * i] + vs[2 * i + 1] * vl[2 * i + 1];
+                        const double rdn = -y[i] + vl[2 * i] - vl[2 * i + 1], rde = wnu - vl[2 * i] - vl[2 * i + 1];
+                        dres = fmax(dres, fmax(fabs(rdn), fabs(rde)));
+                        cst(C::C_VRD + 2 * i, rdn);
+                        cst(C::C_VRD + 2 * i + 1, rde);
+                        pobj += wnu * ve[i];
+                    }
+                }
+                if (prox) {   // w_prox ||x - xbar||^2 without its constant (as the soft terminal)
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) pobj += wpx * z[i] * (z[i] - 2.0 * a.Xref[(agent * K + t) * NX + i]);
+                }
 #pragma unroll
                 for (int g = 0; g < NG; ++g) {
                     if (grp_on(g)) { dres = fmax(dres, fabs(rda[g])); pobj += gweight(g) * av[g]; }
@@ -1584,7 +1880,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
         pres = wave_max(pres); dres = wave_max(dres);
         nb = wave_max(nb); nxv = wave_max(nxv); nsl = wave_max(nsl); nzd = wave_max(nzd);
-        gap = wave_sum(gap); pobj = wave_sum(pobj);
+        gap = wave_sum(gap); pobj = wave_sum(pobj) + cpx;
         const double pnorm = fmax(1.0, nb + nxv + nsl), dnorm = fmax(iosc, (qnorm + nxv) * iosc + nzd);  // caller's units / osc
         const double mu = gap / deg;
         if (!isfinite(pres + dres + mu)) { status = SCVX_STATUS_NUMERICAL; fail_code = 3.0; break; }
@@ -1666,9 +1962,23 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         // complementarity rhs of row r: predictor -s l ; corrector -s l - ds_a dl_a + sigma mu
         double sgmu = 0.0;
         double dz[NZ], dy[NX], da[NGA], dsq[NQ], dlq[NQ], cpv[NR];
+        double dnv[NVA], dne[NVA], vcpv[2 * NVA];   // virtual control directions, predictor products
         auto rco_of = [&](int r, bool corr) __attribute__((always_inline)) -> double {
             const double v = -s_(r) * l_(r);
             return corr ? v - cpv[r] + sgmu : v;
+        };
+        // virtual control rows of component i: complementarity rhs (rows 2i, 2i+1) and the directions
+        auto vrco = [&](int r, bool corr) __attribute__((always_inline)) -> double {
+            const double v = -vs[r] * vl[r];
+            return corr ? v - vcpv[r] + sgmu : v;
+        };
+        auto vrow_dir = [&](int i, bool corr, double* dsr, double* dlr) __attribute__((always_inline)) {
+            const double g1 = dnv[i] - dne[i], g2 = -dnv[i] - dne[i];
+            const double rc1 = vn[i] - ve[i] + vs[2 * i], rc2 = -vn[i] - ve[i] + vs[2 * i + 1];
+            dsr[0] = -rc1 - g1;
+            dlr[0] = (vrco(2 * i, corr) + vl[2 * i] * (rc1 + g1)) / vs[2 * i];
+            dsr[1] = -rc2 - g2;
+            dlr[1] = (vrco(2 * i + 1, corr) + vl[2 * i + 1] * (rc2 + g2)) / vs[2 * i + 1];
         };
         // Newton direction for the complementarity rhs (rows: rco_of, SOC: rcq2); directions out
         auto newton = [&](bool corr, const double* rcq2) __attribute__((always_inline)) {
@@ -1718,10 +2028,31 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             }
 #pragma unroll
             for (int j = 0; j < NQ; ++j) cst(C::C_RHO + j, rho[j]);
-            double q[NX], rr[NU];
+            double q[NX], rr[NU], dvl[NVA];
             reduce_rhs(r1, r1a, q, rr);
+#pragma unroll
+            for (int i = 0; i < NVA; ++i) dvl[i] = 0.0;
+            if constexpr (NV > 0) {
+                // rhs of (nu_i, e_i): -rd - sum_r G_r' (rco_r + l_r rc_r) / s_r, then e_i eliminated:
+                // nu's linear term -(r_nu - b/a r_e), a = D1 + D2, b = D2 - D1 (r_e kept for the recovery)
+                double vrd[2 * NV];
+                ldn(vrd, C::C_VRD, 2 * NV);
+                if (corr) ldn(vcpv, C::C_VCP, 2 * NV);
+                hold(vrd, 2 * NV);
+                if (corr) hold(vcpv, 2 * NV);
+#pragma unroll
+                for (int i = 0; i < NV; ++i) {
+                    const double rc1 = vn[i] - ve[i] + vs[2 * i], rc2 = -vn[i] - ve[i] + vs[2 * i + 1];
+                    const double c1 = -(vrco(2 * i, corr) + vl[2 * i] * rc1) / vs[2 * i];
+                    const double c2 = -(vrco(2 * i + 1, corr) + vl[2 * i + 1] * rc2) / vs[2 * i + 1];
+                    const double rn = -vrd[2 * i] + c1 - c2, re = -vrd[2 * i + 1] - c1 - c2;
+                    const double d1 = vl[2 * i] / vs[2 * i], d2 = vl[2 * i + 1] / vs[2 * i + 1];
+                    dvl[i] = vact ? -(rn - (d2 - d1) / (d1 + d2) * re) : 0.0;
+                    cst(C::C_VRE + i, re);
+                }
+            }
             stamp(2);
-            solve(q, rr, dz, dy);
+            solve(q, rr, dvl, dz, dy, dnv);
             // post-solve: group and SOC directions (state reloaded: nothing crossed the sweeps)
             fresh();
             issue_state();
@@ -1733,6 +2064,21 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             if (corr) hold(cpv, NR);
             hold(rho, NQ);
             recover_aux(dz, da);
+            if constexpr (NV > 0) {   // de = (r_e - b dnu) / a
+                double vre[NV];
+                ldn(vre, C::C_VRE, NV);
+                if (corr) ldn(vcpv, C::C_VCP, 2 * NV);
+                hold(vre, NV);
+                if (corr) hold(vcpv, 2 * NV);
+#pragma unroll
+                for (int i = 0; i < NV; ++i) {
+                    const double d1 = vl[2 * i] / vs[2 * i], d2 = vl[2 * i + 1] / vs[2 * i + 1];
+                    dne[i] = vact ? (vre[i] - (d2 - d1) * dnv[i]) / (d1 + d2) : 0.0;
+                    dnv[i] = vact ? dnv[i] : 0.0;
+                }
+#pragma unroll
+                for (int r = 0; r < 2 * NV; ++r) vcpv[r] = corr ? vcpv[r] : 0.0;
+            }
             if (soc) {
                 double v2[NQ], w2[NQ];
                 dsq[0] = -rcq[0];
@@ -1784,6 +2130,30 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                     q2 = fma(dsr, dlr, q2);
                     pr += 0.0 * (dsr + dlr);
                     if (!corr) cst(C::C_CP + r, dsr * dlr);
+                }
+            }
+            if constexpr (NV > 0) {
+                if (vact) {
+#pragma unroll
+                    for (int i = 0; i < NV; ++i) {
+                        double dsr[2], dlr[2];
+                        vrow_dir(i, corr, dsr, dlr);
+#pragma unroll
+                        for (int k = 0; k < 2; ++k) {
+                            const double sr = vs[2 * i + k], lr = vl[2 * i + k];
+                            const bool c1 = dsr[k] < 0.0 && sr * bd < bn * -dsr[k];
+                            bn = c1 ? sr : bn;
+                            bd = c1 ? -dsr[k] : bd;
+                            const bool c2 = dlr[k] < 0.0 && lr * bd < bn * -dlr[k];
+                            bn = c2 ? lr : bn;
+                            bd = c2 ? -dlr[k] : bd;
+                            q0 = fma(sr, lr, q0);
+                            q1 += fma(sr, dlr[k], lr * dsr[k]);
+                            q2 = fma(dsr[k], dlr[k], q2);
+                            pr += 0.0 * (dsr[k] + dlr[k]);
+                            if (!corr) cst(C::C_VCP + 2 * i + k, dsr[k] * dlr[k]);
+                        }
+                    }
                 }
             }
             double am = bn / bd;
@@ -1880,6 +2250,19 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 l_(r) += al * dlr;
             }
         }
+        if constexpr (NV > 0) {
+            if (vact) {
+#pragma unroll
+                for (int i = 0; i < NV; ++i) {
+                    double dsr[2], dlr[2];
+                    vrow_dir(i, true, dsr, dlr);
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) { vs[2 * i + k] += al * dsr[k]; vl[2 * i + k] += al * dlr[k]; }
+                    vn[i] += al * dnv[i];
+                    ve[i] += al * dne[i];
+                }
+            }
+        }
         if (act) {
 #pragma unroll
             for (int i = 0; i < NZ; ++i) z[i] += al * dz[i];
@@ -1921,6 +2304,20 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             for (int i = 0; i < NX; ++i) {
                 const double e = z[i] - a.x_final[agent * NX + i];
                 pobj += wfs * e * e;
+            }
+        }
+        if (prox) {   // w_prox ||x_t - xbar_t||^2 (with its constant: the objective in the caller's units)
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                const double e = z[i] - a.Xref[(agent * K + t) * NX + i];
+                pobj += wpx * e * e;
+            }
+        }
+        if (vact) {
+#pragma unroll
+            for (int i = 0; i < NV; ++i) {
+                pobj += wnu * ve[i];
+                a.nu[(agent * (K - 1) + t) * NX + i] = vn[i];
             }
         }
         a.slack_coll[agent * K + t] = (has_coll && ineq) ? av[NG > 0 ? NG - 1 : 0] : 0.0;

@@ -177,6 +177,13 @@ class QPSpec:
     # hard row d_{T-1} + x_{T-1} == x_des): with has_final=False and w_final > 0 the objective gains
     # w_final ||x_{K-1} - x_final||^2, so the subproblem stays feasible whatever the linearisation
     w_final: float = 0.0
+    # virtual control (the SCvx subproblem form of SCvx/optimization/sc_problem.py:60-68, build-side option for
+    # nonlinear models under the Jacobi update): nu_t in every dynamics row, + w_nu sum_t ||nu_t||_1; the
+    # subproblem is then feasible for any linearisation point.  Quadrotor (and one DI) classes only.
+    w_nu: float = 0.0
+    # proximal term w_prox sum_t ||x_t - xbar_t||^2: a soft trust region on the states (the hard trust region
+    # of dist_scvx_3d.py:84 bounds the inputs only)
+    w_prox: float = 0.0
 
     def to_c(self):
         n, m = MODEL_DIMS[self.model]
@@ -201,6 +208,9 @@ class QPSpec:
         t.u_max = 0.0 if self.u_max is None else float(self.u_max)
         t.max_iter, t.tol = int(self.max_iter), float(self.tol)
         t.w_final = float(self.w_final)
+        if self.w_nu < 0 or self.w_prox < 0:
+            raise ValueError("QPSpec: w_nu and w_prox must be >= 0")
+        t.w_nu, t.w_prox = float(self.w_nu), float(self.w_prox)
         return t
 
 
@@ -218,6 +228,7 @@ class QPSolver:
         self.X = torch.empty((N, K, n), dtype=torch.float64, device=device)
         self.U = torch.empty((N, K, m), dtype=torch.float64, device=device)
         self.slack = torch.empty((N, K), dtype=torch.float64, device=device)
+        self.nu = torch.zeros((N, K - 1, n), dtype=torch.float64, device=device)   # zeros unless w_nu > 0
         self.obj = torch.empty(N, dtype=torch.float64, device=device)
         self.status = torch.empty(N, dtype=torch.int32, device=device)
         self.iters = torch.empty(N, dtype=torch.int32, device=device)
@@ -257,11 +268,12 @@ class QPSolver:
             ctypes.byref(self.ctpl), self.N, _dev(disc, name="disc"), _dev(sigma, name="sigma"),
             _dev(Xref, name="Xref"), _dev(Uref, name="Uref"), _dev(x_init, name="x_init"), _dev(xf, name="x_final"),
             _dev(tr, name="tr"), _dev(coll_rows, name="coll_rows"), _dev(coll_count, torch.int32, "coll_count"),
-            _dev(self.X), _dev(self.U), _dev(self.slack), _dev(self.obj), _dev(self.status, torch.int32),
+            _dev(self.X), _dev(self.U), _dev(self.slack), _dev(self.nu), _dev(self.obj), _dev(self.status, torch.int32),
             _dev(self.iters, torch.int32), _dev(self.workspace), ctypes.c_size_t(self.workspace.numel() * 8),
             _stream(stream))
         check(rc, "scvx_qp_solve_batched")
-        return dict(X=self.X, U=self.U, slack_coll=self.slack, obj=self.obj, status=self.status, iters=self.iters)
+        return dict(X=self.X, U=self.U, slack_coll=self.slack, nu=self.nu, obj=self.obj, status=self.status,
+                    iters=self.iters)
 
 
 def qp_solve_batched(spec: QPSpec, disc, sigma, Xref, Uref, x_init, x_final, tr, coll_rows=None, coll_count=None):
@@ -468,10 +480,10 @@ def admm_consensus(X_new, nbr, rho, Y, Lam, pos_dim, primal=None, dual=None, str
 
 
 def jacobi_update(status, X_sol, U_sol, X, U, tr, prev_cost, grow=False, tr_max=float("inf"), X_out=None, U_out=None,
-                  stream=None):
+                  tie_rtol=0.0, stream=None):
     """Fused bookkeeping of one Jacobi SCvx iteration, per-agent trust-region rule
     (scvx_jacobi_update_batched): failed agents (status 2) keep (X, U), the others take (X_sol, U_sol);
-    tr halves where sum_{t<K-1} ||u_t||^2 rose above prev_cost, then a failed agent's radius halves
+    tr halves where sum_{t<K-1} ||u_t||^2 rose above prev_cost (1 + tie_rtol), then a failed agent's radius halves
     (or doubles up to tr_max with grow=True); prev_cost <- the new cost.  tr / prev_cost are updated in
     place; returns (X_out, U_out) (fresh tensors unless given)."""
     torch = _torch()
@@ -488,7 +500,7 @@ def jacobi_update(status, X_sol, U_sol, X, U, tr, prev_cost, grow=False, tr_max=
                                           _dev(U_sol, name="U_sol"), _dev(X, name="X"), _dev(U, name="U"),
                                           _dev(X_out, name="X_out"), _dev(U_out, name="U_out"), _dev(tr, name="tr"),
                                           _dev(prev_cost, name="prev_cost"), int(bool(grow)), float(tr_max),
-                                          _stream(stream))
+                                          float(tie_rtol), _stream(stream))
     check(rc, "scvx_jacobi_update_batched")
     return X_out, U_out
 

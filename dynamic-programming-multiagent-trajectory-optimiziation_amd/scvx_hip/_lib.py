@@ -38,7 +38,8 @@ class QPTemplate(ctypes.Structure):
         ("obs_center", (ctypes.c_double * 3) * SCVX_MAX_OBS), ("obs_radius", ctypes.c_double * SCVX_MAX_OBS),
         ("w_obs", ctypes.c_double), ("j_max", ctypes.c_int32), ("w_coll", ctypes.c_double),
         ("has_soc", ctypes.c_int32), ("u_max", ctypes.c_double), ("max_iter", ctypes.c_int32),
-        ("tol", ctypes.c_double), ("w_final", ctypes.c_double),
+        ("tol", ctypes.c_double), ("w_final", ctypes.c_double), ("w_nu", ctypes.c_double),
+        ("w_prox", ctypes.c_double),
     ]
 
 
@@ -92,7 +93,7 @@ def lib():
         L.scvx_integrate_nonlinear_batched.argtypes = [i32, vp, i32, i32, vp, vp, vp, i32, i32, vp, vp]
         L.scvx_qp_workspace_bytes.argtypes = [ctypes.POINTER(QPTemplate), i32]
         L.scvx_qp_workspace_bytes.restype = sz
-        L.scvx_qp_solve_batched.argtypes = [ctypes.POINTER(QPTemplate), i32] + [vp] * 15 + [vp, sz, vp]
+        L.scvx_qp_solve_batched.argtypes = [ctypes.POINTER(QPTemplate), i32] + [vp] * 16 + [vp, sz, vp]
         L.scvx_qp_set_trace.argtypes = [vp, i32, i32]
         L.scvx_collision_rows_batched.argtypes = [i32, i32, i32, i32, vp, i32, i32, dbl, dbl, i32, vp, vp, vp]
         L.scvx_collision_check_batched.argtypes = [i32, i32, i32, i32, vp, i32, i32, dbl, vp, vp, dbl, vp, vp, vp]
@@ -103,7 +104,7 @@ def lib():
         L.scvx_admm_consensus_batched.argtypes = [i32, i32, i32, i32, i32, vp, vp, dbl, vp, vp, vp, vp, vp]
         L.scvx_scp_game_solve_batched.argtypes = [ctypes.POINTER(SCPTemplate), i32] + [vp] * 18 + [vp, sz, vp]
         L.scvx_slab_update_batched.argtypes = [i32, i32, i32, i32, i32, vp, vp, vp, vp]
-        L.scvx_jacobi_update_batched.argtypes = [i32, i32, i32, i32] + [vp] * 9 + [i32, dbl, vp]
+        L.scvx_jacobi_update_batched.argtypes = [i32, i32, i32, i32] + [vp] * 9 + [i32, dbl, dbl, vp]
         sized = ("scvx_last_error", "scvx_qp_workspace_bytes", "scvx_scp_workspace_bytes")
         for fn in EXPORTS:
             getattr(L, fn).restype = getattr(L, fn).restype if fn in sized else i32

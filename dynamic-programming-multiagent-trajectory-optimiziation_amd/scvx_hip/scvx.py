@@ -34,8 +34,8 @@ class HipBackend:
     def qp_solver(self, spec, N, device):
         return QPSolver(spec, N, device=device)
 
-    def jacobi_update(self, status, X_sol, U_sol, X, U, tr, prev_cost, grow, tr_max):
-        return jacobi_update(status, X_sol, U_sol, X, U, tr, prev_cost, grow=grow, tr_max=tr_max)
+    def jacobi_update(self, status, X_sol, U_sol, X, U, tr, prev_cost, grow, tr_max, tie_rtol=0.0):
+        return jacobi_update(status, X_sol, U_sol, X, U, tr, prev_cost, grow=grow, tr_max=tr_max, tie_rtol=tie_rtol)
 
 
 @dataclass
@@ -62,11 +62,19 @@ class JacobiSCvx:
     tr_rule: "global" -- one trust region for all agents, halved when the total cost rises
              (dist_scvx_3d.py:248-252); "per_agent" -- the same rule applied to each agent's own
              cost (independent agents, configs C2/C3).
+    tie_rtol: per-agent rule only -- an agent's radius halves when its cost exceeds the previous one by
+             more than this relative margin (default 1e-9).  A converged agent's successive costs agree
+             only to rounding, so the reference's strict test would halve its radius on the rounding of
+             the cost sum, differently for every summation order (the per-agent rule is this build's; the
+             reference's global rule keeps the strict test).
+    fused_update: per-agent rule in one launch (csrc/jacobi.hip, default); False runs the same rules as
+             tensor ops.
     """
 
     def __init__(self, spec: QPSpec, x_init, x_final, sigma, tr0: float, coupling: Optional[CouplingSpec] = None,
                  tr_rule: str = "per_agent", group=None, nsub: Optional[int] = None, backend=None,
-                 on_fail: str = "halve", tr_max: Optional[float] = None, fused_update: bool = False):
+                 on_fail: str = "halve", tr_max: Optional[float] = None, fused_update: bool = True,
+                 tie_rtol: float = 1e-9):
         import torch
         self.torch = torch
         self.backend = backend or HipBackend()
@@ -79,9 +87,8 @@ class JacobiSCvx:
         if on_fail not in ("halve", "grow"):
             raise ValueError(f"on_fail must be 'halve' or 'grow', not {on_fail!r}")
         self.on_fail, self.tr_max = on_fail, float(tr0 if tr_max is None else tr_max)
-        # per-agent rule in one launch (csrc/jacobi.hip); opt-in: its cost summation order breaks the
-        # rounding-level ties of converged agents differently from the tensor form
         self.fused_update = fused_update
+        self.tie_rtol = float(tie_rtol)
         self.group = group
         self.nsub = nsub or DEFAULT_NSUB[spec.model]
         self.solver = self.backend.qp_solver(spec, self.N, self.device)
@@ -131,7 +138,7 @@ class JacobiSCvx:
         o2 = sub.solve(g(self.disc), g(self.sigma), g(X), g(U), g(self.x_init), g(self.x_final), g(self.tr),
                        g(rows_hi), g(count_hi))
         out = {k: v.clone() for k, v in out.items()}
-        for k in ("X", "U", "slack_coll", "obj", "status", "iters"):
+        for k in ("X", "U", "slack_coll", "nu", "obj", "status", "iters"):
             out[k].index_copy_(0, idx, o2[k])
         ok = out["status"] != 2
         still = int(violators().sum().item())
@@ -184,7 +191,7 @@ class JacobiSCvx:
         if self.fused_update and self.tr_rule == "per_agent" and fused is not None:
             # one launch for the update, the cost rule and the failure rule (csrc/jacobi.hip)
             Xn, Un = fused(out["status"], out["X"], out["U"], X, U, self.tr, self.prev_cost, self.on_fail == "grow",
-                           self.tr_max)
+                           self.tr_max, self.tie_rtol)
             self._mark(marks, "update")
             return Xn, Un, out
         failed = out["status"] == 2
@@ -200,7 +207,7 @@ class JacobiSCvx:
             self.tr.mul_(1.0 - 0.5 * shrink)
             self.prev_total.copy_(total)
         else:
-            shrink = (cost > self.prev_cost).to(torch.float64)
+            shrink = (cost > self.prev_cost * (1.0 + self.tie_rtol)).to(torch.float64)
             self.tr.mul_(1.0 - 0.5 * shrink)
             self.prev_cost.copy_(cost)
         if self.on_fail == "grow":

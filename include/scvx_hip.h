@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define SCVX_HIP_VERSION 1
+#define SCVX_HIP_VERSION 2
 
 #define SCVX_OK 0
 #define SCVX_EINVAL (-1)
@@ -82,7 +82,14 @@ int scvx_integrate_nonlinear_batched(int model_id, const double* params, int K, 
  *        a_o' (p_t - c_o) >= r_o - s_{t,o},  s_{t,o} >= 0,
  *           a_o = (pbar_t - c_o)/(||pbar_t - c_o|| + 1e-6)   (single_integrator_model.py:113-126)
  *        ||u_t||_2 <= u_max                    if has_soc                 (single_integrator_model.py:103-104)
- * with p_t = x_t[0:pos_dim].  Solved by a batched primal-dual interior-point method (Mehrotra
+ * with p_t = x_t[0:pos_dim].  With w_nu > 0 (virtual control, the SCvx subproblem form of
+ * SCvx/optimization/sc_problem.py:60-68) every dynamics row carries nu_t (t < K-1):
+ *        x_{t+1} = A_t x_t + B_t u_t + C_t u_{t+1} + S_t sigma + z_t + nu_t,
+ * and the objective gains the exact penalty w_nu sum_t ||nu_t||_1 (node-separable; the reference's
+ * SCProblem prices max_t ||nu_t||_1, scvx_scp_solve_batched below), so the subproblem stays feasible
+ * whatever the linearisation point (nonlinear models under the Jacobi update).  With w_prox > 0 the
+ * objective also gains w_prox sum_t ||x_t - xbar_t||^2, a soft trust region on the states (the trust
+ * region above bounds only the inputs, which leaves the states of a long integrator chain free).  Solved by a batched primal-dual interior-point method (Mehrotra
  * predictor-corrector, Nesterov-Todd scaling for the SOC) whose KKT systems are factored by a
  * Riccati recursion over the K nodes.
  * ------------------------------------------------------------------------------------------ */
@@ -112,6 +119,8 @@ typedef struct scvx_qp_template {
     int32_t max_iter;
     double tol;
     double w_final;         /* has_final = 0 and w_final > 0: soft terminal w_final ||x_{K-1} - x_final||^2 */
+    double w_nu;            /* > 0: virtual control nu_t with penalty w_nu sum_t ||nu_t||_1 (0: none) */
+    double w_prox;          /* > 0: proximal term w_prox sum_t ||x_t - xbar_t||^2 (a soft state trust region) */
 } scvx_qp_template;
 
 /*
@@ -120,7 +129,8 @@ typedef struct scvx_qp_template {
  *   x_final [N][n] (ignored unless has_final or w_final > 0), tr [N],
  *   coll_rows [N][K][j_max][pos_dim+1] rows (g, b), coll_count [N][K] (both ignored if j_max=0)
  * Outputs (device):
- *   X [N][K][n], U [N][K][m], slack_coll [N][K] (S_t, zeros if j_max = 0), obj [N],
+ *   X [N][K][n], U [N][K][m], slack_coll [N][K] (S_t, zeros if j_max = 0),
+ *   nu [N][K-1][n] (virtual control; required iff w_nu > 0, may be NULL otherwise), obj [N],
  *   status [N], iters [N]
  * workspace: caller-owned device scratch of at least scvx_qp_workspace_bytes(tpl, N) bytes.
  * Limits: 2 <= K <= 64 (one node per lane), n_u <= 4, <= 64 inequality rows per node.
@@ -128,7 +138,7 @@ typedef struct scvx_qp_template {
 int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const double* disc, const double* sigma,
                           const double* Xref, const double* Uref, const double* x_init, const double* x_final,
                           const double* tr, const double* coll_rows, const int32_t* coll_count, double* X,
-                          double* U, double* slack_coll, double* obj, int32_t* status, int32_t* iters,
+                          double* U, double* slack_coll, double* nu, double* obj, int32_t* status, int32_t* iters,
                           void* workspace, size_t workspace_bytes, void* stream);
 
 /* Bytes of caller-owned device scratch scvx_qp_solve_batched needs for N agents. */
@@ -328,7 +338,9 @@ int scvx_admm_consensus_batched(int N, int n_nbr, int K, int pos_dim, int n_x, c
  * scvx_hip/scvx.py JacobiSCvx.step, fused): per agent i, (X_out[i], U_out[i]) = (X_sol[i], U_sol[i]) if
  * status[i] != 2, else (X[i], U[i]) (Distributed_opt/dist_scvx_3d.py:113-118; X_out may alias X);
  * cost = sum_{t<K-1} ||U_out[i][t]||^2
- * (cost_fcn, :131-138); tr[i] *= 0.5 if cost > prev_cost[i] (:248-252, per agent); a failed agent's
+ * (cost_fcn, :131-138); tr[i] *= 0.5 if cost > prev_cost[i] (1 + tie_rtol) (:248-252, per agent;
+ * tie_rtol >= 0, e.g. 1e-9: successive costs of a converged agent agree only to rounding, so the
+ * reference's strict test (tie_rtol = 0) would halve on the rounding of the sum); a failed agent's
  * radius then halves (grow = 0) or doubles (grow = 1; every radius is then capped at tr_max);
  * prev_cost[i] = cost.
  * Device buffers: status [N] int32, X_sol / X / X_out [N][K][n_x], U_sol / U / U_out [N][K][n_u],
@@ -336,7 +348,8 @@ int scvx_admm_consensus_batched(int N, int n_nbr, int K, int pos_dim, int n_x, c
  */
 int scvx_jacobi_update_batched(int N, int K, int n_x, int n_u, const int32_t* status, const double* X_sol,
                                const double* U_sol, const double* X, const double* U, double* X_out, double* U_out,
-                               double* tr, double* prev_cost, int grow, double tr_max, void* stream);
+                               double* tr, double* prev_cost, int grow, double tr_max, double tie_rtol,
+                               void* stream);
 
 #ifdef __cplusplus
 }

@@ -20,13 +20,14 @@ class QPTemplate(ctypes.Structure):
         ("obs_center", (ctypes.c_double * 3) * MAX_OBS), ("obs_radius", ctypes.c_double * MAX_OBS),
         ("w_obs", ctypes.c_double), ("j_max", ctypes.c_int32), ("w_coll", ctypes.c_double),
         ("has_soc", ctypes.c_int32), ("u_max", ctypes.c_double), ("max_iter", ctypes.c_int32),
-        ("tol", ctypes.c_double), ("w_final", ctypes.c_double),
+        ("tol", ctypes.c_double), ("w_final", ctypes.c_double), ("w_nu", ctypes.c_double),
+        ("w_prox", ctypes.c_double),
     ]
 
 
 def make_template(n, m, K, pos_dim=3, has_final=True, fix_last_input=True, ineq_last=False, w_last=0.0,
                   box=(), obs=(), w_obs=1e6, j_max=0, w_coll=1e4, u_max=None, max_iter=60, tol=1e-9,
-                  model_id=0, w_final=0.0):
+                  model_id=0, w_final=0.0, w_nu=0.0, w_prox=0.0):
     t = QPTemplate()
     t.model_id, t.n_x, t.n_u, t.K, t.pos_dim = model_id, n, m, K, pos_dim
     t.has_final, t.fix_last_input, t.ineq_last, t.w_last = int(has_final), int(fix_last_input), int(ineq_last), w_last
@@ -43,6 +44,8 @@ def make_template(n, m, K, pos_dim=3, has_final=True, fix_last_input=True, ineq_
     t.u_max = 0.0 if u_max is None else u_max
     t.max_iter, t.tol = max_iter, tol
     t.w_final = w_final
+    t.w_nu = w_nu
+    t.w_prox = w_prox
     return t
 
 
@@ -66,11 +69,12 @@ def solve_batched(tpl, disc, sigma, Xref, Uref, x_init, x_final, tr, coll_rows=N
         coll_count = np.zeros(1, np.int32)
     coll_rows, coll_count = c(coll_rows, np.float64), c(coll_count, np.int32)
     X = np.zeros((N, K, n)); U = np.zeros((N, K, m)); S = np.zeros((N, K)); obj = np.zeros(N)
+    nu = np.zeros((N, K - 1, n))
     st = np.zeros(N, np.int32); it = np.zeros(N, np.int32)
     rc = lib.oracle_qp_solve_batched(ctypes.byref(tpl), N, _p(disc), _p(sigma), _p(Xref), _p(Uref), _p(x_init),
                                      _p(x_final), _p(tr), _p(coll_rows), _p(coll_count, ctypes.c_int32), _p(X),
-                                     _p(U), _p(S), _p(obj), _p(st, ctypes.c_int32), _p(it, ctypes.c_int32),
+                                     _p(U), _p(S), _p(nu), _p(obj), _p(st, ctypes.c_int32), _p(it, ctypes.c_int32),
                                      int(nthreads))
     if rc != 0:
         raise ValueError("oracle_qp_solve_batched failed")
-    return dict(X=X, U=U, slack_coll=S, obj=obj, status=st, iters=it)
+    return dict(X=X, U=U, slack_coll=S, nu=nu, obj=obj, status=st, iters=it)

@@ -31,6 +31,12 @@ def _soc_J(x):
     return x[0] * x[0] - x[1:] @ x[1:]
 
 
+def _soc_det(x):
+    """_soc_J without cancellation, floored at a tiny positive value (NT scaling of a boundary iterate)."""
+    n1 = np.linalg.norm(x[1:])
+    return max((x[0] - n1) * (x[0] + n1), 1e-300)
+
+
 def _jprod(dims, a, b):
     out = np.empty_like(a)
     nl = dims["l"]
@@ -93,7 +99,7 @@ def _nt_scaling(dims, s, z):
     i = nl
     for k in dims["q"]:
         ss, zz = s[i:i + k], z[i:i + k]
-        Js, Jz = _soc_J(ss), _soc_J(zz)
+        Js, Jz = _soc_det(ss), _soc_det(zz)
         sb, zb = ss / np.sqrt(Js), zz / np.sqrt(Jz)
         gam = np.sqrt((1.0 + sb @ zb) / 2.0)
         Jzb = zb.copy()
@@ -235,6 +241,11 @@ def build_agent_problem(prob):
       w_final                            -- > 0: soft terminal w_final ||x_{T-1} + d_{T-1} - x_final||^2 in
                                             place of the row (:74) (build-side option, QPSpec.w_final)
       fix_last_input (bool)              -- pin w_{T-1} = 0 (dist_scvx_3d leaves it free & unused)
+      w_nu                               -- > 0: virtual control nu_t (t < T-1) added to every dynamics row
+                                            (the SCvx form of SCvx/optimization/sc_problem.py:60-68) with the
+                                            exact penalty w_nu sum_t ||nu_t||_1 (CVXPY's epigraph
+                                            -e <= nu <= e, + w_nu sum e; build-side option QPSpec.w_nu)
+      w_prox                             -- > 0: + w_prox sum_t ||d_t||^2 (QPSpec.w_prox, a soft state trust region)
       pos_dim (3)
     Returns (P, q, A, b, G, h, dims, index dict).
     """
@@ -264,6 +275,10 @@ def build_agent_problem(prob):
         alloc("S", K - 1)
     if obs:
         alloc("so", (K - 1) * len(obs))
+    w_nu = prob.get("w_nu", 0.0)
+    if w_nu > 0:
+        alloc("nu", (K - 1) * n)         # virtual control (sc_problem.py:25, 67)
+        alloc("e", (K - 1) * n)          # its L1 epigraph
     nv = off
 
     def vd(t, i):
@@ -285,10 +300,17 @@ def build_agent_problem(prob):
         for i in range(n):
             P[vd(K - 1, i), vd(K - 1, i)] += 2.0 * w_final
             q[vd(K - 1, i)] += 2.0 * w_final * (Xr[K - 1, i] - prob["x_final"][i])
+    w_prox = prob.get("w_prox", 0.0)
+    if w_prox > 0:   # w_prox ||x_t - xbar_t||^2 = w_prox ||d_t||^2, every node (QPSpec.w_prox)
+        for t in range(K):
+            for i in range(n):
+                P[vd(t, i), vd(t, i)] += 2.0 * w_prox
     if has_coll:
         q[idx["S"][0]:idx["S"][1]] = prob["w_coll"]
     if obs:
         q[idx["so"][0]:idx["so"][1]] = prob["w_obs"]
+    if w_nu > 0:
+        q[idx["e"][0]:idx["e"][1]] = w_nu
 
     Aeq, beq = [], []
 
@@ -317,6 +339,8 @@ def build_agent_problem(prob):
                 r[vw(t, j)] -= Bm[t][i, j]
                 if Cm is not None:
                     r[vw(t + 1, j)] -= Cm[t][i, j]
+            if w_nu > 0:
+                r[idx["nu"][0] + t * n + i] -= 1.0
             beq.append(rhs0[i])
     if prob.get("fix_last_input", False):
         for j in range(m):
@@ -356,6 +380,11 @@ def build_agent_problem(prob):
             # a'(pbar + d - c) >= r - s   <=>  -a'd - s <= a'(pbar - c) - r
             ineq([(vd(t, i), -a[i]) for i in range(pd)] + [(so, -1.0)], a @ diff - rad)
             ineq([(so, -1.0)], 0.0)
+        if w_nu > 0:
+            for i in range(n):
+                vn, ve = idx["nu"][0] + t * n + i, idx["e"][0] + t * n + i
+                ineq([(vn, 1.0), (ve, -1.0)], 0.0)     # nu <= e
+                ineq([(vn, -1.0), (ve, -1.0)], 0.0)    # -nu <= e
     nl = len(Gl)
     qdims = []
     umax = prob.get("umax")
@@ -374,10 +403,19 @@ def build_agent_problem(prob):
     return P, q, Aeq, beq, G, h, dims, idx
 
 
-def solve_agent(prob, **kw):
-    """Solve one agent's reference-form subproblem; returns X_new (K,n), U_new (K,m), obj, info."""
+def solve_agent(prob, sparse=False, **kw):
+    """Solve one agent's reference-form subproblem; returns X_new (K,n), U_new (K,m), obj, info.
+    sparse=True: the same problem through oracle/scp_dense.py's sparse conic IPM (scipy splu on the
+    KKT matrix; the large quadrotor / virtual-control instances, where the dense LU takes minutes)."""
     P, q, A, b, G, h, dims, idx = build_agent_problem(prob)
-    sol = solve_conic_qp(P, q, A, b, G, h, dims, **kw)
+    if sparse:
+        import scipy.sparse as sp
+        from .scp_dense import solve_conic_qp_sparse
+        osc = max(1.0, float(np.abs(q).max(initial=0.0)))
+        sol = solve_conic_qp_sparse(sp.csr_matrix(P), q, sp.csr_matrix(A), b, sp.csr_matrix(G), h, dims,
+                                    tol=kw.get("tol", 1e-10), maxit=kw.get("maxit", 150), osc=osc)
+    else:
+        sol = solve_conic_qp(P, q, A, b, G, h, dims, **kw)
     x = sol["x"]
     K, n = prob["Xref"].shape
     m = prob["Uref"].shape[1]
@@ -392,10 +430,12 @@ def solve_agent(prob, **kw):
     info = dict(status=sol["status"], iters=sol["iters"], cert=kkt_certificate(P, q, A, b, G, h, dims, sol))
     if "S" in idx:
         info["S"] = x[idx["S"][0]:idx["S"][1]]
+    if "nu" in idx:
+        info["nu"] = x[idx["nu"][0]:idx["nu"][1]].reshape(K - 1, n)
     return prob["Xref"] + d, Ur + w, obj, info
 
 
-def constraint_violation(prob, X, U, S=None):
+def constraint_violation(prob, X, U, S=None, nu=None):
     """Max violation of the reference-form constraints (build_agent_problem) at absolute (X, U, S).
 
     Independent of any solver: the feasibility half of a parity certificate."""
@@ -414,6 +454,8 @@ def constraint_violation(prob, X, U, S=None):
             r = r + prob["C"][t] @ U[t + 1]
         if prob.get("c") is not None:
             r = r + prob["c"][t]
+        if nu is not None:
+            r = r + nu[t]
         dyn = max(dyn, np.abs(r).max())
     viol["dyn"] = dyn
     viol["tr"] = max(0.0, max(np.abs(w[t]).sum() - prob["tr"] for t in range(K - 1)))

@@ -99,6 +99,14 @@ def _max_step(dims, x, dx):
     return a
 
 
+def _soc_det(x):
+    """x0^2 - ||x1||^2 as (x0 - ||x1||)(x0 + ||x1||): no cancellation near the cone boundary, and floored
+    at a tiny positive value so the NT scaling of an iterate that rounding put on the boundary stays
+    finite (the square root / fourth root of a negative number was NaN)."""
+    n1 = np.linalg.norm(x[1:])
+    return max((x[0] - n1) * (x[0] + n1), 1e-300)
+
+
 def _nt_scaling(dims, s, z):
     """Sparse block-diagonal W, W^-1 with W z = W^-1 s (hyperbolic-rotation form for SOC)."""
     nl = dims["l"]
@@ -106,7 +114,7 @@ def _nt_scaling(dims, s, z):
     Wb, Wib = [sp.diags(d)], [sp.diags(1.0 / d)]
     for i, k in _cone_blocks(dims):
         ss, zz = s[i:i + k], z[i:i + k]
-        Js, Jz = ss[0] ** 2 - ss[1:] @ ss[1:], zz[0] ** 2 - zz[1:] @ zz[1:]
+        Js, Jz = _soc_det(ss), _soc_det(zz)
         sb, zb = ss / np.sqrt(Js), zz / np.sqrt(Jz)
         gam = np.sqrt((1.0 + sb @ zb) / 2.0)
         Jzb = zb.copy()

@@ -208,7 +208,8 @@ static double soc_step(const double* x, const double* dx, int k) {
 
 // ------------------------------------ per-agent solver --------------------------------------
 struct Node {
-    int nv = 0, na = 0;   // node vars = n + m + na
+    int nv = 0, na = 0;   // node vars = n + m + nnu + na: x, u, virtual control nu (t < K-1 when w_nu > 0), aux
+    int nnu = 0;
     Mat G;                // orthant rows (nr x nv)
     Vec h;
     int nr = 0;
@@ -226,6 +227,7 @@ struct Agent {
     std::vector<Mat> A, B, C;   // C[t] couples u_{t+1}
     std::vector<Vec> c;
     Vec x_init, x_final;
+    Vec xref;                    // Xbar (K*n): the proximal term's centre
     Vec y;                       // dynamics multipliers (K-1)*n
     Vec y_init, y_fin;
 };
@@ -253,6 +255,7 @@ static void setup_agent(Agent& ag, const scvx_qp_template* T, const double* disc
         for (int i = 0; i < n; ++i) ag.c[t][i] = d[n * n + 2 * n * m + i] * sigma + d[n * n + 2 * n * m + n + i];
     }
     ag.x_init.assign(x_init, x_init + n);
+    ag.xref.assign(Xr, Xr + (size_t)K * n);
     ag.x_final.assign(n, 0.0);
     if (T->has_final || T->w_final > 0.0) ag.x_final.assign(x_final, x_final + n);
     ag.nd.assign(K, Node());
@@ -260,8 +263,12 @@ static void setup_agent(Agent& ag, const scvx_qp_template* T, const double* disc
     for (int t = 0; t < K; ++t) {
         Node& N = ag.nd[t];
         bool ineq = (t < K - 1) || T->ineq_last;
-        N.na = ineq ? (T->n_obs + (coll ? 1 : 0)) : 0;
-        N.nv = n + m + N.na;
+        // virtual control nu_t in the dynamics of interval t (SCvx form, sc_problem.py:60-68) with
+        // the penalty w_nu ||nu_t||_1 through its epigraph -e <= nu <= e (e: aux, eliminated per node)
+        N.nnu = (T->w_nu > 0.0 && t < K - 1) ? n : 0;
+        N.na = (ineq ? (T->n_obs + (coll ? 1 : 0)) : 0) + N.nnu;
+        N.nv = n + m + N.nnu + N.na;
+        const int ab = n + m + N.nnu;   // first aux variable
         N.q.assign(N.nv, 0.0);
         N.pdiag.assign(N.nv, 0.0);
         double wu = (t < K - 1) ? 1.0 : T->w_last;
@@ -269,6 +276,11 @@ static void setup_agent(Agent& ag, const scvx_qp_template* T, const double* disc
         if (t == K - 1 && !T->has_final && T->w_final > 0.0) {  // soft terminal (kernel: tsoft)
             for (int i = 0; i < n; ++i) { N.pdiag[i] = 2.0 * T->w_final; N.q[i] = -2.0 * T->w_final * ag.x_final[i]; }
         }
+        if (T->w_prox > 0.0)   // proximal term w_prox ||x_t - xbar_t||^2 (its constant is added to obj below)
+            for (int i = 0; i < n; ++i) {
+                N.pdiag[i] += 2.0 * T->w_prox;
+                N.q[i] -= 2.0 * T->w_prox * Xr[(size_t)t * n + i];
+            }
         N.fixed_u = (t == K - 1) && T->fix_last_input;
         std::vector<Vec> rows;
         Vec hs;
@@ -291,7 +303,7 @@ static void setup_agent(Agent& ag, const scvx_qp_template* T, const double* disc
                 r = newrow(); rows[r][T->box_idx[b]] = -1.0; hs.push_back(-T->box_lo[b]);
             }
             for (int o = 0; o < T->n_obs; ++o) {
-                int ai = n + m + o;
+                int ai = ab + o;
                 double diff[3], nr = 0.0;
                 for (int i = 0; i < pd; ++i) { diff[i] = pb[i] - T->obs_center[o][i]; nr += diff[i] * diff[i]; }
                 nr = std::sqrt(nr) + 1e-6;
@@ -308,7 +320,7 @@ static void setup_agent(Agent& ag, const scvx_qp_template* T, const double* disc
                 N.q[ai] = T->w_obs;
             }
             if (coll) {
-                int ai = n + m + T->n_obs;
+                int ai = ab + T->n_obs;
                 int cnt = ccount[t];
                 for (int j = 0; j < cnt; ++j) {
                     const double* rw = crow + ((size_t)t * T->j_max + j) * (pd + 1);
@@ -321,6 +333,12 @@ static void setup_agent(Agent& ag, const scvx_qp_template* T, const double* disc
                 N.q[ai] = T->w_coll;
             }
             N.soc = T->has_soc != 0;
+        }
+        for (int i = 0; i < N.nnu; ++i) {   // nu_i - e_i <= 0, -nu_i - e_i <= 0
+            const int ei = ab + N.na - N.nnu + i;
+            int r = newrow(); rows[r][n + m + i] = 1.0; rows[r][ei] = -1.0; hs.push_back(0.0);
+            r = newrow(); rows[r][n + m + i] = -1.0; rows[r][ei] = -1.0; hs.push_back(0.0);
+            N.q[ei] = T->w_nu;
         }
         N.nr = (int)rows.size();
         N.G = Mat(N.nr, N.nv);
@@ -353,11 +371,22 @@ struct NodeLin {   // per-node quantities of one IPM iteration
 struct Riccati {
     std::vector<Mat> P, Kg, L, Pi, kap, Bt;
     std::vector<Vec> k0, p0;
+    // virtual control: G_t = H_nunu + P_{t+1} (Cholesky), YP = G^-1 P_{t+1}, YPi = G^-1 Pi_{t+1}, d_t
+    std::vector<Mat> LG, YP, YPi;
+    std::vector<Vec> dnu;
+    std::vector<Mat> Pe, Pie;   // effective next-stage P~, Pi~ of stage t (= P_{t+1}, Pi_{t+1} without nu)
     Mat M;
     bool ok = true;
 };
 
-// factor the Riccati recursion for node Hessians H_t (n+m square, in (x,u) coordinates)
+// factor the Riccati recursion for node Hessians H_t ((n+m+nnu) square, in (x,u,nu) coordinates)
+//
+// Virtual control nu_t (interval t, Hessian block H_nunu, no cross terms with x, u) is eliminated
+// inside stage t: with the next stage's value 1/2 xi'P xi + xi'(p + Pi mu),
+//   nu = -G^-1 (P y + p + Pi mu + d),  G = H_nunu + P,  y = A xi + Bt v + e,
+// and the stage sees the effective next-stage data  P~ = P - P G^-1 P = H_nunu G^-1 P,
+// Pi~ = H_nunu G^-1 Pi, p~ = p - P G^-1 (p + d), plus the terminal terms M -= Pi' G^-1 Pi and
+// xacc -= Pi' G^-1 (p + d).
 static void riccati_factor(const Agent& ag, const std::vector<Mat>& H, Riccati& R) {
     int n = ag.n, m = ag.m, K = ag.K;
     const bool fin = ag.T->has_final;
@@ -369,6 +398,12 @@ static void riccati_factor(const Agent& ag, const std::vector<Mat>& H, Riccati& 
     R.Bt.assign(K, Mat(n, m));
     R.k0.assign(K, Vec(m));
     R.p0.assign(K, Vec(n));
+    R.LG.assign(K, Mat());
+    R.YP.assign(K, Mat());
+    R.YPi.assign(K, Mat());
+    R.dnu.assign(K, Vec());
+    R.Pe.assign(K, Mat());
+    R.Pie.assign(K, Mat());
     R.M = Mat(n, n);
     R.ok = true;
     for (int t = 0; t < K - 1; ++t) {
@@ -392,7 +427,27 @@ static void riccati_factor(const Agent& ag, const std::vector<Mat>& H, Riccati& 
         }
         Mat Qh = Q, Sh = tr(S), Rh = Rm;
         if (t < K - 1) {
-            const Mat& Pn = R.P[t + 1];
+            Mat Pn = R.P[t + 1], Pin = R.Pi[t + 1];
+            const int nnu = ag.nd[t].nnu;
+            if (nnu) {
+                Mat Hn(n, n), G = R.P[t + 1];
+                for (int i = 0; i < n; ++i)
+                    for (int j = 0; j < n; ++j) { Hn(i, j) = H[t](n + m + i, n + m + j); G(i, j) += Hn(i, j); }
+                if (!chol(G)) { R.ok = false; return; }
+                R.LG[t] = G;
+                R.YP[t] = chol_solve_mat(G, R.P[t + 1]);
+                Pn = mul(Hn, R.YP[t]);
+                for (int i = 0; i < n; ++i)
+                    for (int j = 0; j < i; ++j) { double v = 0.5 * (Pn(i, j) + Pn(j, i)); Pn(i, j) = Pn(j, i) = v; }
+                if (fin) {
+                    R.YPi[t] = chol_solve_mat(G, R.Pi[t + 1]);
+                    Pin = mul(Hn, R.YPi[t]);
+                    Mat c = mul(tr(R.Pi[t + 1]), R.YPi[t]);
+                    for (size_t e = 0; e < R.M.a.size(); ++e) R.M.a[e] -= c.a[e];
+                }
+            }
+            R.Pe[t] = Pn;
+            R.Pie[t] = Pin;
             Mat PA = mul(Pn, ag.A[t]), PB = mul(Pn, R.Bt[t]);
             Qh = add(Q, mul(tr(ag.A[t]), PA));
             Sh = add(tr(S), mul(tr(R.Bt[t]), PA));
@@ -405,7 +460,17 @@ static void riccati_factor(const Agent& ag, const std::vector<Mat>& H, Riccati& 
             }
         }
         Mat L = Rh;
-        if (!chol(L)) { R.ok = false; return; }
+        if (!chol(L)) {
+            if (std::getenv("SCVX_DEBUG")) {
+                std::fprintf(stderr, "   chol(Rh) failed at stage %d:", t);
+                for (int i = 0; i < m; ++i) std::fprintf(stderr, " %.3e", Rh(i, i));
+                std::fprintf(stderr, " | Rm diag");
+                for (int i = 0; i < m; ++i) std::fprintf(stderr, " %.3e", Rm(i, i));
+                std::fprintf(stderr, "\n");
+            }
+            R.ok = false;
+            return;
+        }
         R.L[t] = L;
         Mat Kg = chol_solve_mat(L, Sh);
         for (double& v : Kg.a) v = -v;
@@ -429,7 +494,7 @@ static void riccati_factor(const Agent& ag, const std::vector<Mat>& H, Riccati& 
                 R.Pi[t] = add(I, mul(tr(Sh), kap));
                 R.M = (K >= 2) ? mul(ag.C[K - 2], kap) : Mat(n, n);
             } else {
-                const Mat& Pin = R.Pi[t + 1];
+                const Mat& Pin = R.Pie[t];
                 Mat rhs = mul(tr(R.Bt[t]), Pin);
                 if (ag.nd[t].fixed_u) rhs = Mat(m, n);
                 Mat kap = chol_solve_mat(L, rhs);
@@ -442,7 +507,7 @@ static void riccati_factor(const Agent& ag, const std::vector<Mat>& H, Riccati& 
     }
 }
 
-// Solve  min 1/2 dz'H dz - r1'dz  s.t. A dz = r2  ; returns dz (K*(n+m)), dy (K-1)*n, dyi, dyf
+// Solve  min 1/2 dz'H dz - r1'dz  s.t. A dz = r2  ; returns dz (per node n+m+nnu), dy (K-1)*n, dyi, dyf
 static bool riccati_solve(const Agent& ag, const std::vector<Mat>& H, Riccati& R, const std::vector<Vec>& r1,
                           const Vec& xi0, const std::vector<Vec>& e, const Vec& r2fin, std::vector<Vec>& dz,
                           Vec& dy, Vec& dyi, Vec& dyf) {
@@ -451,6 +516,7 @@ static bool riccati_solve(const Agent& ag, const std::vector<Mat>& H, Riccati& R
     const bool fin = ag.T->has_final;
     Vec xacc(n, 0.0);
     for (int t = K - 1; t >= 0; --t) {
+        const int nnu = ag.nd[t].nnu;
         Vec q(n), r(m);
         for (int i = 0; i < n; ++i) q[i] = -r1[t][i];
         for (int j = 0; j < m; ++j) r[j] = -r1[t][n + j];
@@ -458,10 +524,18 @@ static bool riccati_solve(const Agent& ag, const std::vector<Mat>& H, Riccati& R
             Vec ct = matTvec(ag.C[t - 1], q);
             for (int j = 0; j < m; ++j) r[j] += ct[j];
         }
-        Vec qh = q, rh = r;
+        Vec qh = q, rh = r, pw;   // pw = p_{t+1} + d_t (virtual control)
         if (t < K - 1) {
-            Vec h = matvec(R.P[t + 1], e[t]);
-            for (int i = 0; i < n; ++i) h[i] += R.p0[t + 1][i];
+            Vec pn = R.p0[t + 1];
+            if (nnu) {
+                R.dnu[t].assign(n, 0.0);
+                pw = pn;
+                for (int i = 0; i < n; ++i) { R.dnu[t][i] = -r1[t][n + m + i]; pw[i] += R.dnu[t][i]; }
+                Vec c = matTvec(R.YP[t], pw);   // (G^-1 P)' (p + d) = P G^-1 (p + d)
+                for (int i = 0; i < n; ++i) pn[i] -= c[i];
+            }
+            Vec h = matvec(R.Pe[t], e[t]);
+            for (int i = 0; i < n; ++i) h[i] += pn[i];
             Vec a = matTvec(ag.A[t], h), b = matTvec(R.Bt[t], h);
             for (int i = 0; i < n; ++i) qh[i] += a[i];
             for (int j = 0; j < m; ++j) rh[j] += b[j];
@@ -481,8 +555,12 @@ static bool riccati_solve(const Agent& ag, const std::vector<Mat>& H, Riccati& R
             } else {
                 Vec bk = matvec(R.Bt[t], k);
                 for (int i = 0; i < n; ++i) bk[i] += e[t][i];
-                Vec g = matTvec(R.Pi[t + 1], bk);
+                Vec g = matTvec(R.Pie[t], bk);
                 for (int i = 0; i < n; ++i) xacc[i] += g[i];
+                if (nnu) {
+                    Vec c = matTvec(R.YPi[t], pw);   // Pi' G^-1 (p + d)
+                    for (int i = 0; i < n; ++i) xacc[i] -= c[i];
+                }
             }
         }
     }
@@ -493,7 +571,7 @@ static bool riccati_solve(const Agent& ag, const std::vector<Mat>& H, Riccati& R
         if (!lu_solve(R.M, mu)) return false;
     }
     Vec xi = xi0;
-    dz.assign(K, Vec(n + m, 0.0));
+    dz.assign(K, Vec());
     dy.assign((size_t)(K - 1) * n, 0.0);
     auto pfull = [&](int t) {
         Vec p = R.p0[t];
@@ -509,6 +587,8 @@ static bool riccati_solve(const Agent& ag, const std::vector<Mat>& H, Riccati& R
         for (int i = 0; i < n; ++i) dyi[i] = -(Px[i] + p[i]);
     }
     for (int t = 0; t < K; ++t) {
+        const int nnu = ag.nd[t].nnu;
+        dz[t].assign(n + m + nnu, 0.0);
         Vec v = matvec(R.Kg[t], xi);
         for (int j = 0; j < m; ++j) v[j] += R.k0[t][j];
         if (fin) {
@@ -526,13 +606,63 @@ static bool riccati_solve(const Agent& ag, const std::vector<Mat>& H, Riccati& R
             Vec a = matvec(ag.A[t], xi), b = matvec(R.Bt[t], v);
             Vec xn(n);
             for (int i = 0; i < n; ++i) xn[i] = a[i] + b[i] + e[t][i];
-            Vec p = pfull(t + 1), Px = matvec(R.P[t + 1], xn);
+            Vec p = pfull(t + 1);
+            if (nnu) {   // nu = -G^-1 (P y + p + Pi mu + d)
+                Vec w = matvec(R.P[t + 1], xn);
+                for (int i = 0; i < n; ++i) w[i] += p[i] + R.dnu[t][i];
+                chol_solve(R.LG[t], w.data());
+                for (int i = 0; i < n; ++i) { dz[t][n + m + i] = -w[i]; xn[i] -= w[i]; }
+            }
+            Vec Px = matvec(R.P[t + 1], xn);
             for (int i = 0; i < n; ++i) dy[(size_t)t * n + i] = -(Px[i] + p[i]);
             xi = xn;
         }
     }
     dyf = mu;
     return true;
+}
+
+// The (x, u, nu) block of a node's Hessian with its aux variables eliminated:
+//   diag(pdiag) + sum_{rows r without aux} D_r g_r g_r' + sum_aux sum_{r in R_a} D_r (g_r - m_a)(g_r - m_a)',
+// m_a = sum_{R_a} D_r g_r / sum_{R_a} D_r, with g_r the row's (x, u, nu) part (every row of aux a has coefficient
+// -1 on it).  This is the Schur complement H_zz - H_za H_aa^-1 H_az written as a weighted covariance: a sum of
+// PSD terms, where the direct difference cancels catastrophically once one row's barrier weight dominates
+// (an active obstacle row next to its inactive slack-sign row: D1 D2 / (D1 + D2) computed as D1 - D1^2/(D1 + D2)
+// turned negative and broke the Riccati factorisation on 6 of the 1024 C3 agents).  The kernel does the same.
+static Mat node_zz(const Node& N, const Vec& D, int nz) {
+    Mat H(nz, nz);
+    for (int j = 0; j < nz; ++j) H(j, j) = N.pdiag[j];
+    std::vector<int> aux(N.nr, -1);
+    for (int r = 0; r < N.nr; ++r)
+        for (int a = 0; a < N.na; ++a)
+            if (N.G(r, nz + a) != 0.0) aux[r] = a;
+    for (int r = 0; r < N.nr; ++r) {
+        if (aux[r] >= 0) continue;
+        for (int i = 0; i < nz; ++i) {
+            const double gi = N.G(r, i);
+            if (gi == 0.0) continue;
+            for (int j = 0; j < nz; ++j) H(i, j) += D[r] * gi * N.G(r, j);
+        }
+    }
+    for (int a = 0; a < N.na; ++a) {
+        double dsum = 0.0;
+        Vec mean(nz, 0.0);
+        for (int r = 0; r < N.nr; ++r)
+            if (aux[r] == a) {
+                dsum += D[r];
+                for (int i = 0; i < nz; ++i) mean[i] += D[r] * N.G(r, i);
+            }
+        if (!(dsum > 0.0)) continue;
+        for (int i = 0; i < nz; ++i) mean[i] /= dsum;
+        for (int r = 0; r < N.nr; ++r)
+            if (aux[r] == a)
+                for (int i = 0; i < nz; ++i) {
+                    const double ci = N.G(r, i) - mean[i];
+                    if (ci == 0.0) continue;
+                    for (int j = 0; j < nz; ++j) H(i, j) += D[r] * ci * (N.G(r, j) - mean[j]);
+                }
+    }
+    return H;
 }
 
 // CVXOPT-style starting point: from the reference trajectory z_ref (aux = 0) take the minimiser of
@@ -562,10 +692,10 @@ static bool init_point(Agent& ag) {
             for (int j = 0; j < m; ++j) { Hf(n + j, n + j) += 1.0; rf[n + j] -= N.z[n + j]; }
         if (N.fixed_u)
             for (int j = 0; j < m; ++j) rf[n + j] = 0.0;
-        int nz = n + m, na = N.na;
-        H[t] = Mat(nz, nz);
-        for (int i = 0; i < nz; ++i)
-            for (int j = 0; j < nz; ++j) H[t](i, j) = Hf(i, j);
+        int nz = n + m + N.nnu, na = N.na;
+        H[t] = node_zz(N, Vec(N.nr, 1.0), nz);
+        if (N.soc)
+            for (int j = 0; j < m; ++j) H[t](n + j, n + j) += 1.0;
         r1[t].assign(rf.begin(), rf.begin() + nz);
         if (na > 0) {
             Mat Haa(na, na);
@@ -576,9 +706,6 @@ static bool init_point(Agent& ag) {
                 for (int j = 0; j < na; ++j) Hza[t](i, j) = Hf(i, nz + j);
             HaaL[t] = Haa;
             if (!chol(HaaL[t])) return false;
-            Mat X = chol_solve_mat(HaaL[t], tr(Hza[t]));
-            Mat corr = mul(Hza[t], X);
-            for (size_t i = 0; i < H[t].a.size(); ++i) H[t].a[i] -= corr.a[i];
             r1a[t].assign(rf.begin() + nz, rf.end());
             Vec ra = r1a[t];
             chol_solve(HaaL[t], ra.data());
@@ -601,6 +728,7 @@ static bool init_point(Agent& ag) {
             double v = z1[i] - ag.c[t][i];
             for (int k = 0; k < n; ++k) v -= ag.A[t](i, k) * z0[k];
             for (int j = 0; j < m; ++j) v -= ag.B[t](i, j) * z0[n + j] + ag.C[t](i, j) * z1[n + j];
+            if (ag.nd[t].nnu) v -= z0[n + m + i];
             e[t][i] = -v;
         }
     }
@@ -610,7 +738,7 @@ static bool init_point(Agent& ag) {
     double smin = 1e300, lmin = 1e300;
     for (int t = 0; t < K; ++t) {
         Node& N = ag.nd[t];
-        int nz = n + m;
+        int nz = n + m + N.nnu;
         for (int i = 0; i < nz; ++i) N.z[i] += dz[t][i];
         if (N.na > 0) {
             Vec ra = r1a[t];
@@ -661,10 +789,14 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
     double osc = 1.0;
     for (int t = 0; t < K; ++t)
         for (double v : ag.nd[t].q) osc = std::max(osc, std::fabs(v));
+    if (const char* e = std::getenv("SCVX_OSC")) osc = std::atof(e);   // diagnostics: force the objective scale
     for (int t = 0; t < K; ++t) {
         for (double& v : ag.nd[t].q) v /= osc;
         for (double& v : ag.nd[t].pdiag) v /= osc;
     }
+    double cprox = 0.0;   // w_prox sum ||xbar||^2 (caller's units)
+    if (T->w_prox > 0.0)
+        for (double v : ag.xref) cprox += T->w_prox * v * v;
     if (!init_point(ag)) { iters_out = 0; obj_out = 0.0; return SCVX_STATUS_NUMERICAL; }
     double dres_best = 1e300, pres_best = 1e300;
     for (it = 0;; ++it) {  // the residuals are evaluated once more after the last step (kernel: cap check)
@@ -693,6 +825,7 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
                 double v = z1[i] - ag.c[t][i];
                 for (int k = 0; k < n; ++k) v -= ag.A[t](i, k) * z0[k];
                 for (int j = 0; j < m; ++j) v -= ag.B[t](i, j) * z0[n + j] + ag.C[t](i, j) * z1[n + j];
+                if (ag.nd[t].nnu) v -= z0[n + m + i];
                 rp[t][i] = v;
                 pres = std::max(pres, std::fabs(v));
             }
@@ -747,6 +880,7 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
                     for (int i = 0; i < n; ++i) l.rd[k] -= ag.A[t](i, k) * yt[i];
                 for (int j = 0; j < m; ++j)
                     for (int i = 0; i < n; ++i) l.rd[n + j] -= ag.B[t](i, j) * yt[i];
+                for (int i = 0; i < N.nnu; ++i) l.rd[n + m + i] -= yt[i];
             }
             if (N.fixed_u)
                 for (int j = 0; j < m; ++j) l.rd[n + j] = 0.0;
@@ -759,6 +893,7 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
                 double zj = ag.nd[t].z[j];
                 pobj += 0.5 * ag.nd[t].pdiag[j] * zj * zj + ag.nd[t].q[j] * zj;
             }
+        pobj += cprox / osc;   // the proximal term's constant: the gap test is relative to the true objective
         if (std::getenv("SCVX_DEBUG")) std::fprintf(stderr, "it %d pres %.3e dres %.3e mu %.3e pobj %.6e\n", it, pres, dres, mu, pobj);
         if (!std::isfinite(pres + dres + mu)) { status = SCVX_STATUS_NUMERICAL; break; }
         const double pnorm = std::max(1.0, nb + nxv + nsl), dnorm = std::max(1.0 / osc, nq + nxv / osc + nzd);  // caller's units / osc
@@ -799,10 +934,11 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
                 for (int i = 0; i < m; ++i)
                     for (int j = 0; j < m; ++j) Hf(n + i, n + j) += l.soc.Wi2(1 + i, 1 + j);
             }
-            int nz = n + m, na = N.na;
-            l.Hxu = Mat(nz, nz);
-            for (int i = 0; i < nz; ++i)
-                for (int j = 0; j < nz; ++j) l.Hxu(i, j) = Hf(i, j);
+            int nz = n + m + N.nnu, na = N.na;
+            l.Hxu = node_zz(N, l.D, nz);
+            if (N.soc)
+                for (int i = 0; i < m; ++i)
+                    for (int j = 0; j < m; ++j) l.Hxu(n + i, n + j) += l.soc.Wi2(1 + i, 1 + j);
             if (na > 0) {
                 Mat Haa(na, na);
                 l.Hza = Mat(nz, na);
@@ -812,9 +948,6 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
                     for (int j = 0; j < na; ++j) l.Hza(i, j) = Hf(i, nz + j);
                 l.Haa_L = Haa;
                 if (!chol(l.Haa_L)) { status = fail_status; goto done; }
-                Mat X = chol_solve_mat(l.Haa_L, tr(l.Hza));  // na x nz
-                Mat corr = mul(l.Hza, X);
-                for (size_t i = 0; i < l.Hxu.a.size(); ++i) l.Hxu.a[i] -= corr.a[i];
             }
             H[t] = l.Hxu;
         }
@@ -845,7 +978,7 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
                     }
                     if (N.fixed_u)
                         for (int j = 0; j < m; ++j) rf[n + j] = 0.0;
-                    int nz = n + m;
+                    int nz = n + m + N.nnu;
                     r1[t].assign(rf.begin(), rf.begin() + nz);
                     if (N.na > 0) {
                         Vec ra(rf.begin() + nz, rf.end());
@@ -884,6 +1017,7 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
                                 double v = dzx[t + 1][i] - e[t][i];
                                 for (int k = 0; k < n; ++k) v -= ag.A[t](i, k) * dzx[t][k];
                                 for (int j = 0; j < m; ++j) v -= ag.B[t](i, j) * dzx[t][n + j] + ag.C[t](i, j) * dzx[t + 1][n + j];
+                                if (ag.nd[t].nnu) v -= dzx[t][n + m + i];
                                 e2 = std::max(e2, std::fabs(v));
                             }
                         }
@@ -902,7 +1036,7 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out) {
                 for (int t = 0; t < K; ++t) {
                     Node& N = ag.nd[t];
                     NodeLin& l = L[t];
-                    int nz = n + m;
+                    int nz = n + m + N.nnu;
                     dz[t].assign(N.nv, 0.0);
                     for (int i = 0; i < nz; ++i) dz[t][i] = dzx[t][i];
                     if (N.na > 0) {
@@ -1027,6 +1161,9 @@ done:
     obj_out = pobj * osc;
     if (!ag.T->has_final && ag.T->w_final > 0.0)  // the soft terminal's constant w_final ||x_final||^2
         for (int i = 0; i < n; ++i) obj_out += ag.T->w_final * ag.x_final[i] * ag.x_final[i];
+    if (ag.T->w_prox > 0.0)
+        for (int t = 0; t < K; ++t)
+            for (int i = 0; i < n; ++i) obj_out += ag.T->w_prox * ag.xref[(size_t)t * n + i] * ag.xref[(size_t)t * n + i];
     iters_out = it;
     return status;
 }
@@ -1037,7 +1174,7 @@ extern "C" int oracle_qp_solve_batched(const scvx_qp_template* tpl, int N, const
                                        const double* Xref, const double* Uref, const double* x_init,
                                        const double* x_final, const double* tr, const double* coll_rows,
                                        const int32_t* coll_count, double* X, double* U, double* slack_coll,
-                                       double* obj, int32_t* status, int32_t* iters, int nthreads) {
+                                       double* nu, double* obj, int32_t* status, int32_t* iters, int nthreads) {
     const int n = tpl->n_x, m = tpl->n_u, K = tpl->K, pd = tpl->pos_dim;
     if (n <= 0 || m <= 0 || K < 2 || m > 4 || pd > 3) return -1;
     const size_t stride = (size_t)(K - 1) * n * (n + 2 * m + 2);
@@ -1056,7 +1193,10 @@ extern "C" int oracle_qp_solve_batched(const scvx_qp_template* tpl, int N, const
         for (int t = 0; t < K; ++t) {
             for (int i = 0; i < n; ++i) X[((size_t)a * K + t) * n + i] = ag.nd[t].z[i];
             for (int j = 0; j < m; ++j) U[((size_t)a * K + t) * m + j] = ag.nd[t].z[n + j];
-            slack_coll[(size_t)a * K + t] = (tpl->j_max > 0 && ag.nd[t].na > 0) ? ag.nd[t].z[n + m + tpl->n_obs] : 0.0;
+            const Node& Nt = ag.nd[t];
+            slack_coll[(size_t)a * K + t] = (tpl->j_max > 0 && Nt.na > Nt.nnu) ? Nt.z[n + m + Nt.nnu + tpl->n_obs] : 0.0;
+            if (nu && t < K - 1)
+                for (int i = 0; i < n; ++i) nu[((size_t)a * (K - 1) + t) * n + i] = Nt.nnu ? Nt.z[n + m + i] : 0.0;
         }
     }
     return 0;

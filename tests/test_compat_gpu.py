@@ -81,8 +81,15 @@ def test_dist_scvx_3d_jacobi_sweep_matches_dense_oracle(cuda):
         Xn, Un, obj, prob = ref[nm]
         got_X, got_U = X1[nm][:, 0:6], X1[nm][:, 6:9]
         viol = qd.constraint_violation(prob, got_X, got_U, np.full(d.T, 1e9))
-        assert max(v for k, v in viol.items() if k != "coll") < 1e-8, viol
+        # Clarabel's primal test is relative: 1e-8 x (||b|| + ||x|| + ||s||), positions here reach ~22
+        assert max(v for k, v in viol.items() if k != "coll") < 2e-7, viol
         u_cost = np.sum(got_U[:-1] ** 2)
+        # the reference objective at the drop-in's solution: the shared slack of node t is the smallest one
+        # its rows allow, S_t = max(0, max_j (c_j - g_j' d_t)) (dist_scvx_3d.py:99-107)
+        d_ = got_X - prob["Xref"]
+        S = np.array([max(0.0, np.max(r[:, 3] - r[:, :3] @ d_[t, :3])) for t, r in enumerate(prob["coll"])])
+        full = u_cost + prob["w_coll"] * S.sum()
+        assert abs(full - obj) <= 1e-7 * max(1.0, obj), (nm, full, obj)   # slack-active robots included
         if obj < 1e3:  # no active collision slack: the minimum-energy trajectory is unique
             assert abs(u_cost - obj) <= 1e-8 * max(1.0, obj)
             assert np.abs(got_X - Xn).max() < 1e-6 and np.abs(got_U - Un).max() < 1e-6

@@ -83,23 +83,63 @@ def test_c3_family_matches_cpu_and_dense(cuda, umax, nobs):
         assert abs(og[a] - cpu["obj"][a]) <= 1e-8 * max(1.0, abs(cpu["obj"][a]))
         assert np.abs(Xg[a] - cpu["X"][a]).max() < 1e-6
         assert np.abs(Ug[a] - cpu["U"][a]).max() < 1e-6
-    compared = 0
-    for a in np.nonzero(ok)[0][:4]:
-        if compared == 2:
-            break
+    for a in range(N):   # every agent against the reference form (sparse KKT path of the dense oracle)
         A, B, C, S, z = pb.unpack_disc(dn[a], 6, 3)
         prob = dict(A=A, B=B, C=C, c=S * sc["sigma"][a] + z, Xref=sc["X"][a], Uref=sc["U"][a],
                     x_final=sc["x_final"][a], tr=0.25, box=box, obs=sc["obs"], w_obs=1e6, umax=umax,
                     fix_last_input=True)
         with np.errstate(all="ignore"):
-            Xd, Ud, objd, info = qd.solve_agent(prob, tol=1e-11, maxit=120)
-        if info["status"] != "optimal":  # the dense checker itself failed on this agent
-            continue
-        compared += 1
-        assert abs(og[a] - objd) <= 1e-7 * max(1.0, abs(objd))
+            Xd, Ud, objd, info = qd.solve_agent(prob, sparse=True, tol=1e-10)
+        assert info["status"] == "optimal", (a, info["status"])
+        assert abs(og[a] - objd) <= 1e-8 * max(1.0, abs(objd)), (a, og[a], objd)
         viol = qd.constraint_violation(prob, Xg[a], Ug[a])
         assert max(viol.values()) < 1e-7, viol
-    assert compared >= 1
+
+
+@pytest.mark.parametrize("umax", [1.0, 0.12])
+def test_c3_bench_construction_sample_matches_dense_oracle(cuda, umax):
+    """The headline workload itself (bench.py C3: workloads.synthetic_di(1024, seed=1), 8 spheres, SOC, box
+    |x|,|y| <= 12, tr 0.25, the bench's tolerance 1e-8) solved for all 1024 agents in one launch; 16 agents
+    (every 64th) checked against the reference-form oracle, each one of them (no sampling escape), plus
+    the tight u_max = 0.12 variant (the longest IPM runs).  Objective 1e-8 relative, feasibility 1e-7."""
+    from scvx_hip import workloads
+    N, K = 1024, 50
+    sc = workloads.synthetic_di(N, K=K, seed=1, obstacles=8)
+    X, U, sig = _t(sc["X"], cuda), _t(sc["U"], cuda), _t(sc["sigma"], cuda)
+    disc = scvx_hip.foh_batched("di", X, U, sig)
+    box = [(0, -12, 12), (1, -12, 12)]
+    spec = scvx_hip.QPSpec(model="di", K=K, box=box, obs=sc["obs"], w_obs=1e6, u_max=umax, tol=1e-8, max_iter=60)
+    out = scvx_hip.qp_solve_batched(spec, disc, sig, X, U, _t(sc["x_init"], cuda), _t(sc["x_final"], cuda),
+                                    _t(np.full(N, 0.25), cuda))
+    st = out["status"].cpu().numpy()
+    dn = disc.cpu().numpy()
+    Xg, Ug, og = out["X"].cpu().numpy(), out["U"].cpu().numpy(), out["obj"].cpu().numpy()
+
+    def dense(a, maxit=150):
+        A, B, C, S, z = pb.unpack_disc(dn[a], 6, 3)
+        prob = dict(A=A, B=B, C=C, c=S * sc["sigma"][a] + z, Xref=sc["X"][a], Uref=sc["U"][a],
+                    x_final=sc["x_final"][a], tr=0.25, box=box, obs=sc["obs"], w_obs=1e6, umax=umax,
+                    fix_last_input=True)
+        with np.errstate(all="ignore"):
+            return prob, qd.solve_agent(prob, sparse=True, tol=1e-11, maxit=maxit)
+
+    for a in range(0, N, 64):   # the sample: every one optimal and equal to the reference form
+        assert st[a] == 0, (a, st[a])
+        prob, (Xd, Ud, objd, info) = dense(a)
+        assert info["status"] == "optimal", (a, info["status"])
+        assert abs(og[a] - objd) <= 1e-8 * max(1.0, abs(objd)), (a, og[a], objd)
+        assert max(qd.constraint_violation(prob, Xg[a], Ug[a]).values()) < 1e-7, a
+    # optimal_inaccurate (Clarabel's reduced tolerances) within 1e-5 of the optimum
+    for a in np.nonzero(st == 1)[0]:
+        prob, (Xd, Ud, objd, info) = dense(a)
+        assert abs(og[a] - objd) <= 1e-5 * max(1.0, abs(objd)), (a, og[a], objd)
+    # a solver_error is an agent whose subproblem is infeasible: at u_max = 0.12 a goal more than
+    # u_max sigma^2 / 4 = 27 m away cannot be reached (the reference's Clarabel would report infeasible)
+    for a in np.nonzero(st == 2)[0]:
+        prob, (Xd, Ud, objd, info) = dense(a, maxit=60)
+        assert info["status"] != "optimal", a
+        assert np.linalg.norm(sc["x_final"][a][:3] - sc["x_init"][a][:3]) > 0.8 * umax * sc["sigma"][a] ** 2 / 4
+    assert (st == 0).mean() >= 0.99, np.bincount(st, minlength=3)
 
 
 def test_collision_rows_match_reference_formula(cuda):
@@ -195,22 +235,20 @@ def test_unicycle_and_si_classes_match_cpu_and_dense(cuda, model):
                                model_id=scvx_hip.MODEL_IDS[model])
     cpu = qp_cpu.solve_batched(tpl, dn, sig, X, U, X[:, 0], X[:, -1], tr)
     st = out["status"].cpu().numpy()
-    ok = cpu["status"] == 0
-    assert ok.sum() >= N // 2, cpu["status"]
-    assert (st[ok] == 0).all(), st
+    assert (cpu["status"] == 0).all(), cpu["status"]   # every agent (round 2 let half of them fail)
+    assert (st == 0).all(), st
     og, Xg = out["obj"].cpu().numpy(), out["X"].cpu().numpy()
-    for i in np.nonzero(ok)[0]:
+    for i in range(N):
         assert abs(og[i] - cpu["obj"][i]) <= 1e-8 * max(1.0, abs(cpu["obj"][i]))
         assert np.abs(Xg[i] - cpu["X"][i]).max() < 1e-6
-    i = int(np.nonzero(ok)[0][0])
-    A, B, C, S, z = pb.unpack_disc(dn[i], n, m)
-    prob = dict(A=A, B=B, C=C, c=S * sig[i] + z, Xref=X[i], Uref=U[i], x_final=X[i, -1], tr=0.5, box=box, obs=obs,
-                w_obs=1e6, umax=umax, fix_last_input=True, pos_dim=pd)
-    with np.errstate(all="ignore"):
-        Xd, Ud, objd, info = qd.solve_agent(prob, tol=1e-11, maxit=150)
-    assert info["status"] == "optimal"
-    assert abs(og[i] - objd) <= 1e-7 * max(1.0, abs(objd))
-    assert max(qd.constraint_violation(prob, Xg[i], out["U"].cpu().numpy()[i]).values()) < 1e-7
+        A, B, C, S, z = pb.unpack_disc(dn[i], n, m)
+        prob = dict(A=A, B=B, C=C, c=S * sig[i] + z, Xref=X[i], Uref=U[i], x_final=X[i, -1], tr=0.5, box=box,
+                    obs=obs, w_obs=1e6, umax=umax, fix_last_input=True, pos_dim=pd)
+        with np.errstate(all="ignore"):
+            Xd, Ud, objd, info = qd.solve_agent(prob, sparse=True, tol=1e-11)
+        assert info["status"] == "optimal"
+        assert abs(og[i] - objd) <= 1e-8 * max(1.0, abs(objd)), (i, og[i], objd)
+        assert max(qd.constraint_violation(prob, Xg[i], out["U"].cpu().numpy()[i]).values()) < 1e-7
 
 
 def test_soft_terminal_matches_twin_and_dense(cuda):
@@ -248,3 +286,25 @@ def test_soft_terminal_matches_twin_and_dense(cuda):
         assert info["status"] == "optimal"
         assert np.abs(Xg[a] - Xd).max() < 1e-6 and np.abs(Ug[a][:-1] - Ud[:-1]).max() < 1e-6
         assert abs(out["obj"][a].item() - objd) <= 1e-6 * max(1.0, abs(objd))
+
+
+def test_min_energy_closed_form(cuda):
+    """Known answer: with every inequality inactive (trust region 1e3, no box / obstacles / SOC / coupling)
+    the Q1 subproblem (dist_scvx_3d.py:51-111) is the minimum-energy transfer of the FOH-discretized double
+    integrator, u* = M'(M M')^-1 r (tests/test_independent_checks_cpu.min_energy_transfer) -- no solver
+    involved in the reference answer."""
+    from test_independent_checks_cpu import gramian_case, min_energy_transfer
+    sc, disc = gramian_case(N=16)
+    N, K = disc.shape[0], disc.shape[1] + 1
+    spec = scvx_hip.QPSpec(model="di", K=K, tol=1e-12, max_iter=80)
+    out = scvx_hip.qp_solve_batched(spec, _t(disc, cuda), _t(sc["sigma"], cuda), _t(sc["X"], cuda), _t(sc["U"], cuda),
+                                    _t(sc["x_init"], cuda), _t(sc["x_final"], cuda), _t(np.full(N, 1e3), cuda))
+    st = out["status"].cpu().numpy()
+    assert (st == 0).all(), st
+    Xg, Ug, og = out["X"].cpu().numpy(), out["U"].cpu().numpy(), out["obj"].cpu().numpy()
+    for a in range(N):
+        A, B, C, S, z = pb.unpack_disc(disc[a], 6, 3)
+        Xc, Uc, objc = min_energy_transfer(A, B, C, S * sc["sigma"][a] + z, sc["x_init"][a], sc["x_final"][a],
+                                           sc["U"][a][-1])
+        assert np.abs(Xg[a] - Xc).max() < 1e-8 and np.abs(Ug[a] - Uc).max() < 1e-9, a
+        assert abs(og[a] - objc) <= 1e-9 * max(1.0, objc), (a, og[a], objc)

@@ -22,7 +22,7 @@ def _disc(sc, model, N):
 
 def _check_agent(prob, cpu, a):
     with np.errstate(all="ignore"):
-        Xd, Ud, objd, info = qd.solve_agent(prob, tol=1e-11, maxit=150)
+        Xd, Ud, objd, info = qd.solve_agent(prob, sparse=True, tol=1e-10)
     assert info["status"] == "optimal", (a, info["status"])
     assert abs(cpu["obj"][a] - objd) <= 1e-8 * max(1.0, abs(objd)), (a, cpu["obj"][a], objd)
     assert np.abs(cpu["X"][a] - Xd).max() < 1e-6, a
