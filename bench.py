@@ -481,6 +481,9 @@ def main():
                     help="IPM relative stopping tolerance; default = Clarabel's defaults (tol_feas = tol_gap_rel = "
                          "1e-8), the solver of the reference's dist_scvx_3d.py:110")
     ap.add_argument("--dry-run", action="store_true", help="launcher/rendezvous check on CPU, no GPU work")
+    ap.add_argument("--tensor-update", action="store_true", help="c3: bookkeeping as tensor ops (not csrc/jacobi.hip)")
+    ap.add_argument("--tie-rtol", type=float, default=1e-9,
+                    help="c3 per-agent trust-region rule: relative margin of the cost-increase test (JacobiSCvx.tie_rtol)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -514,7 +517,8 @@ def main():
         model, box, j_max, n, m = "di", BOX, 0, 6, 3
         spec = scvx_hip.QPSpec(model="di", K=K, box=BOX, obs=sc["obs"], w_obs=1e6, u_max=U_MAX, tol=args.tol,
                                max_iter=60)
-        drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, tr_rule="per_agent")
+        drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, tr_rule="per_agent", tie_rtol=args.tie_rtol,
+                         fused_update=not args.tensor_update)
         n_obs = N_OBS
     else:
         sc, w, cfg = make_coupled(args.config, world, rank, device)
@@ -531,23 +535,35 @@ def main():
         it_state[0], it_state[1], out = drv.step(it_state[0], it_state[1], marks=marks)
         return out
 
+    status_ids = torch.arange(3, device=device, dtype=torch.int32)
+
+    def record(out, iters, iters_max, stats):
+        """Per-step device-side bookkeeping of the timed region (no host sync): summed and max IPM iterations,
+        status counts.  The warmup runs it too, so no torch kernel is loaded for the first time inside the
+        timed region (a first use costs ~40-180 ms of module loading on a fresh box)."""
+        iters.append(out["iters"].sum())
+        iters_max.append(out["iters"].max())
+        stats.append((out["status"][:, None] == status_ids).sum(dim=0))   # no sync (bincount would sync)
+
     for _ in range(args.warmup):
-        step()
+        out = step()
+        record(out, [], [], [])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     # timed region: exactly `steps` steps (the same code path as the warmup); every stage is bracketed
     # by HIP events on the launch stream (the QP kernel's mark pair gives its launch duration)
-    marks, iters, checks, stats = [], [], [], []
-    status_ids = torch.arange(3, device=device, dtype=torch.int32)
+    marks, iters, iters_max, checks, stats = [], [], [], [], []
     t0 = time.perf_counter()
+    host_ms = []
     for _ in range(args.steps):
         mk = []
+        th = time.perf_counter()
         out = step(mk)
+        host_ms.append(1e3 * (time.perf_counter() - th))
         marks.append(mk)
-        iters.append(out["iters"].sum())
-        stats.append((out["status"][:, None] == status_ids).sum(dim=0))   # device op, no sync (bincount syncs)
+        record(out, iters, iters_max, stats)
         if drv.last_check is not None:
             checks.append(dict(drv.last_check))
     torch.cuda.synchronize()
@@ -642,6 +658,10 @@ def main():
                                                                                   return_counts=True))},
             "status_counts": {str(k): int((status == k).sum()) for k in (0, 1, 2)},
             "status_counts_per_step": [[int(v) for v in c.tolist()[:3]] for c in stats],
+            "step_ms": [round(v, 4) for v in step_ms],
+            "host_ms_per_step": [round(v, 4) for v in host_ms],
+            "gap_ms_between_steps": [round(a[-1][1].elapsed_time(b[0][1]), 4) for a, b in zip(marks[:-1], marks[1:])],
+            "ipm_iters_max_per_step": [int(v) for v in torch.stack(iters_max).tolist()],
             "min_frac_status_0_1": min(float((c[0] + c[1]).item()) / N for c in stats),
             "coupling_check": checks or None,
             "cpu_baseline": cpu,

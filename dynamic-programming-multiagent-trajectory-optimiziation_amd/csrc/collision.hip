@@ -19,10 +19,15 @@
 // the same neighbour sequence j = 0..N_total-1, so node t's positions of a tile of TJ neighbours are
 // staged in LDS once per workgroup (cooperative loads) and read back as LDS broadcasts; the X_all
 // traffic is then ~N_total*pos_dim*8 bytes per workgroup instead of per agent.  Each lane keeps its
-// top-j_max list (S values and neighbour indices) in registers, with the same insertion / eviction
-// order as a sequential scan (so the kept set and the slot of every row are those of the
-// reference-order scan), and writes its rows once at the end.  X_all is the all-gathered
-// [N_total][K][n_x] state (RCCL all_gather over xGMI).
+// top-j_max list (S values and neighbour indices) in registers and writes its rows once at the end.
+// The kept SET is that of a reference-order sequential scan (up to how exact distance ties are
+// broken); the row ORDER is the insertion order of the pre-filtered scan below (the tau bound skips
+// neighbours a sequential scan would have inserted and later evicted), so it is not the sequential
+// scan's slot order -- the QP's solution depends on the order only through rounding.  X_all is the
+// all-gathered [N_total][K][n_x] state (RCCL all_gather over xGMI).
+//
+// Indexed form (scvx_collision_rows_indexed): local agent a is global agent idx[a] instead of i0 + a
+// -- the rows of an arbitrary subset, e.g. the agents the full-row check found violating.
 #include <hip/hip_runtime.h>
 
 #include "common.hpp"
@@ -55,7 +60,8 @@ __device__ __forceinline__ void coll_stage(double* tile, const double* __restric
 
 template <int JM>
 __global__ __launch_bounds__(64) void collision_rows_kernel(int K, int pd, int nx, int N_total, int N_local,
-                                                            const double* __restrict__ X_all, int i0, double R,
+                                                            const double* __restrict__ X_all, int i0,
+                                                            const int32_t* __restrict__ idx, double R,
                                                             double cull, int j_max, double* __restrict__ rows,
                                                             int32_t* __restrict__ count) {
     __shared__ double tile[COLL_TJ * 3];
@@ -63,7 +69,7 @@ __global__ __launch_bounds__(64) void collision_rows_kernel(int K, int pd, int n
     const int t = blockIdx.y;
     const long long a = (long long)blockIdx.x * 64 + lane;  // local agent
     const bool live = a < N_local;
-    const long long gi = i0 + a;  // global agent index
+    const long long gi = idx ? (live ? (long long)idx[a] : -1) : i0 + a;  // global agent index
     if (t >= K - 1) {             // no rows at the last node
         if (live) count[a * K + t] = 0;
         return;
@@ -277,23 +283,42 @@ extern "C" int scvx_collision_check_batched(int K, int pos_dim, int n_x, int N_t
     return scvx::check_launch("collision_check_kernel");
 }
 
+namespace {
+int collision_rows_launch(int K, int pos_dim, int n_x, int N_total, const double* X_all, int i0, const int32_t* idx,
+                          int N_local, double R, double cull_radius, int j_max, double* rows, int32_t* count,
+                          void* stream) {
+    if (N_local == 0) return SCVX_OK;
+    const dim3 grid((unsigned)((N_local + 63) / 64), (unsigned)K);
+    hipStream_t st = (hipStream_t)stream;
+    if (j_max <= 8)
+        hipLaunchKernelGGL(scvx::collision_rows_kernel<8>, grid, dim3(64), 0, st, K, pos_dim, n_x, N_total, N_local,
+                           X_all, i0, idx, R, cull_radius, j_max, rows, count);
+    else if (j_max <= 16)
+        hipLaunchKernelGGL(scvx::collision_rows_kernel<16>, grid, dim3(64), 0, st, K, pos_dim, n_x, N_total, N_local,
+                           X_all, i0, idx, R, cull_radius, j_max, rows, count);
+    else
+        hipLaunchKernelGGL(scvx::collision_rows_kernel<32>, grid, dim3(64), 0, st, K, pos_dim, n_x, N_total, N_local,
+                           X_all, i0, idx, R, cull_radius, j_max, rows, count);
+    return scvx::check_launch("collision_rows_kernel");
+}
+}  // namespace
+
 extern "C" int scvx_collision_rows_batched(int K, int pos_dim, int n_x, int N_total, const double* X_all, int i0,
                                            int N_local, double R, double cull_radius, int j_max, double* rows,
                                            int32_t* count, void* stream) {
     if (K < 2 || K > 64 || pos_dim < 1 || pos_dim > 3 || pos_dim > n_x || N_total < 0 || N_local < 0 || i0 < 0 ||
         i0 + N_local > N_total || j_max < 1 || j_max > 32 || !X_all || !rows || !count)
         return scvx::set_error(SCVX_EINVAL, "collision: bad args");
-    if (N_local == 0) return SCVX_OK;
-    const dim3 grid((unsigned)((N_local + 63) / 64), (unsigned)K);
-    hipStream_t st = (hipStream_t)stream;
-    if (j_max <= 8)
-        hipLaunchKernelGGL(scvx::collision_rows_kernel<8>, grid, dim3(64), 0, st, K, pos_dim, n_x, N_total, N_local,
-                           X_all, i0, R, cull_radius, j_max, rows, count);
-    else if (j_max <= 16)
-        hipLaunchKernelGGL(scvx::collision_rows_kernel<16>, grid, dim3(64), 0, st, K, pos_dim, n_x, N_total, N_local,
-                           X_all, i0, R, cull_radius, j_max, rows, count);
-    else
-        hipLaunchKernelGGL(scvx::collision_rows_kernel<32>, grid, dim3(64), 0, st, K, pos_dim, n_x, N_total, N_local,
-                           X_all, i0, R, cull_radius, j_max, rows, count);
-    return scvx::check_launch("collision_rows_kernel");
+    return collision_rows_launch(K, pos_dim, n_x, N_total, X_all, i0, nullptr, N_local, R, cull_radius, j_max, rows,
+                                 count, stream);
+}
+
+extern "C" int scvx_collision_rows_indexed(int K, int pos_dim, int n_x, int N_total, const double* X_all,
+                                           const int32_t* idx, int N_sel, double R, double cull_radius, int j_max,
+                                           double* rows, int32_t* count, void* stream) {
+    if (K < 2 || K > 64 || pos_dim < 1 || pos_dim > 3 || pos_dim > n_x || N_total < 0 || N_sel < 0 || j_max < 1 ||
+        j_max > 32 || !X_all || !rows || !count || (N_sel > 0 && !idx))
+        return scvx::set_error(SCVX_EINVAL, "collision: bad args");
+    return collision_rows_launch(K, pos_dim, n_x, N_total, X_all, 0, idx, N_sel, R, cull_radius, j_max, rows, count,
+                                 stream);
 }

@@ -132,6 +132,26 @@ def collision_rows(X_all, i0, n_local, R, j_max, pos_dim=3, cull_radius=0.0, row
     return rows, count
 
 
+def collision_rows_indexed(X_all, idx, R, j_max, pos_dim=3, cull_radius=0.0, rows=None, count=None, stream=None):
+    """Rows of dist_scvx_3d.py:93-107 for the agents idx (device int32, distinct, in [0, N_total)) of X_all
+    (scvx_collision_rows_indexed): rows [len(idx)][K][j_max][pos_dim+1], count [len(idx)][K]; rows / count
+    may be larger buffers whose leading len(idx) entries are written."""
+    torch = _torch()
+    N_total, K, n = X_all.shape
+    n_sel = int(idx.shape[0])
+    if rows is None:
+        rows = torch.zeros((n_sel, K, j_max, pos_dim + 1), dtype=torch.float64, device=X_all.device)
+    if count is None:
+        count = torch.zeros((n_sel, K), dtype=torch.int32, device=X_all.device)
+    if rows.shape[0] < n_sel or tuple(rows.shape[1:]) != (K, j_max, pos_dim + 1) or count.shape[0] < n_sel:
+        raise ValueError("collision_rows_indexed: rows / count too small")
+    rc = lib().scvx_collision_rows_indexed(K, pos_dim, n, N_total, _dev(X_all, name="X_all"), _dev(idx, torch.int32, "idx"),
+                                           n_sel, float(R), float(cull_radius), int(j_max), _dev(rows, name="rows"),
+                                           _dev(count, torch.int32, "count"), _stream(stream))
+    check(rc, "scvx_collision_rows_indexed")
+    return rows, count
+
+
 def collision_check(X_all, i0, X_new, slack, R, pos_dim=3, tol=1e-7, viol=None, vmax=None, stream=None):
     """Evaluate EVERY reference collision row (dist_scvx_3d.py:93-107) of local agents
     [i0, i0+N_local) at a solution X_new (N_local,K,n) with shared slacks slack (N_local,K), linearised
@@ -235,10 +255,10 @@ class QPSolver:
         self._dummy = torch.zeros(1, dtype=torch.float64, device=device)
         self._dummy_i = torch.zeros(1, dtype=torch.int32, device=device)
 
-    def _check_shapes(self, disc, sigma, Xref, Uref, x_init, x_final, tr, coll_rows, coll_count):
+    def _check_shapes(self, disc, sigma, Xref, Uref, x_init, x_final, tr, coll_rows, coll_count, N=None):
         """Host-side shape checks: the kernel indexes every buffer with the template's compile-time
         dimensions, so a mis-shaped tensor would be read out of bounds on the device."""
-        spec, N = self.spec, self.N
+        spec, N = self.spec, (self.N if N is None else N)
         n, m = MODEL_DIMS[spec.model]
         K = spec.K
         want = {"disc": (disc, (N, K - 1, disc_stride(spec.model))), "sigma": (sigma, (N,)),
@@ -258,20 +278,31 @@ class QPSolver:
             if tuple(t.shape) != shp:
                 raise ValueError(f"QPSolver.solve: {name} has shape {tuple(t.shape)}, expected {shp}")
 
-    def solve(self, disc, sigma, Xref, Uref, x_init, x_final, tr, coll_rows=None, coll_count=None, stream=None):
+    def solve(self, disc, sigma, Xref, Uref, x_init, x_final, tr, coll_rows=None, coll_count=None, stream=None, n=None):
+        """n (<= N): solve only n agents (the inputs' leading dimension); the outputs are the leading n rows
+        of the solver's buffers.  Returns dict of device tensors (views of reused buffers)."""
         torch = _torch()
-        self._check_shapes(disc, sigma, Xref, Uref, x_init, x_final, tr, coll_rows, coll_count)
+        n = self.N if n is None else int(n)
+        if not 0 <= n <= self.N:
+            raise ValueError(f"QPSolver.solve: n={n} outside [0, {self.N}]")
+        self._check_shapes(disc, sigma, Xref, Uref, x_init, x_final, tr, coll_rows, coll_count, N=n)
         if self.spec.j_max == 0:
             coll_rows, coll_count = self._dummy, self._dummy_i
         xf = x_final if x_final is not None else self._dummy
+        if n == 0:
+            return {k: v[:0] for k, v in self._outputs().items()}
         rc = lib().scvx_qp_solve_batched(
-            ctypes.byref(self.ctpl), self.N, _dev(disc, name="disc"), _dev(sigma, name="sigma"),
+            ctypes.byref(self.ctpl), n, _dev(disc, name="disc"), _dev(sigma, name="sigma"),
             _dev(Xref, name="Xref"), _dev(Uref, name="Uref"), _dev(x_init, name="x_init"), _dev(xf, name="x_final"),
             _dev(tr, name="tr"), _dev(coll_rows, name="coll_rows"), _dev(coll_count, torch.int32, "coll_count"),
             _dev(self.X), _dev(self.U), _dev(self.slack), _dev(self.nu), _dev(self.obj), _dev(self.status, torch.int32),
             _dev(self.iters, torch.int32), _dev(self.workspace), ctypes.c_size_t(self.workspace.numel() * 8),
             _stream(stream))
         check(rc, "scvx_qp_solve_batched")
+        out = self._outputs()
+        return out if n == self.N else {k: v[:n] for k, v in out.items()}
+
+    def _outputs(self):
         return dict(X=self.X, U=self.U, slack_coll=self.slack, nu=self.nu, obj=self.obj, status=self.status,
                     iters=self.iters)
 

@@ -15,8 +15,8 @@ import dataclasses
 from dataclasses import dataclass
 from typing import Optional
 
-from . import (DEFAULT_NSUB, MODEL_DIMS, QPSolver, QPSpec, collision_check, collision_rows, foh_batched,
-               jacobi_update)
+from . import (DEFAULT_NSUB, MODEL_DIMS, QPSolver, QPSpec, collision_check, collision_rows, collision_rows_indexed,
+               foh_batched, jacobi_update)
 
 
 class HipBackend:
@@ -27,6 +27,9 @@ class HipBackend:
 
     def collision_rows(self, X_all, i0, n_local, R, j_max, pos_dim, cull, rows, count):
         return collision_rows(X_all, i0, n_local, R, j_max, pos_dim, cull, rows, count)
+
+    def collision_rows_indexed(self, X_all, idx, R, j_max, pos_dim, cull, rows, count):
+        return collision_rows_indexed(X_all, idx, R, j_max, pos_dim, cull, rows, count)
 
     def collision_check(self, X_all, i0, X_new, slack, R, pos_dim, tol):
         return collision_check(X_all, i0, X_new, slack, R, pos_dim, tol)
@@ -110,10 +113,24 @@ class JacobiSCvx:
             self.rows = torch.zeros((self.N, spec.K, spec.j_max, spec.pos_dim + 1), dtype=torch.float64,
                                     device=self.device)
             self.count = torch.zeros((self.N, spec.K), dtype=torch.int32, device=self.device)
+        self._hi = None   # re-solve buffers of the full-row check (allocated at the first violation)
+
+    def _hi_buffers(self):
+        """Rows, counts and a QPSolver at j_max_hi sized for all N local agents, allocated once: a re-solve
+        uses their leading n_bad entries (QPSolver.solve(n=...))."""
+        if self._hi is None:
+            torch, spec, c = self.torch, self.spec, self.coupling
+            spec_hi = dataclasses.replace(spec, j_max=c.j_max_hi)
+            self._hi = dict(rows=torch.zeros((self.N, spec.K, c.j_max_hi, spec.pos_dim + 1), dtype=torch.float64,
+                                             device=self.device),
+                            count=torch.zeros((self.N, spec.K), dtype=torch.int32, device=self.device),
+                            solver=self.backend.qp_solver(spec_hi, self.N, self.device))
+        return self._hi
 
     def _enforce_all_rows(self, X_all, X, U, out):
         """Make the culled coupling exact: evaluate every reference row at the solution, re-solve the
-        violating agents with the j_max_hi nearest rows, count what still violates (overflow)."""
+        violating agents with the j_max_hi nearest rows (computed for those agents only), count what still
+        violates (overflow)."""
         torch, spec, c = self.torch, self.spec, self.coupling
         ok = out["status"] != 2
 
@@ -128,15 +145,13 @@ class JacobiSCvx:
         if n_bad == 0 or spec.j_max >= c.j_max_hi:
             return out
         idx = bad.nonzero().flatten()
-        spec_hi = dataclasses.replace(spec, j_max=c.j_max_hi)
-        rows_hi = torch.zeros((self.N, spec.K, c.j_max_hi, spec.pos_dim + 1), dtype=torch.float64, device=self.device)
-        count_hi = torch.zeros((self.N, spec.K), dtype=torch.int32, device=self.device)
-        self.backend.collision_rows(X_all, self.i0, self.N, c.R, c.j_max_hi, spec.pos_dim, c.cull_radius, rows_hi,
-                                    count_hi)
+        hi = self._hi_buffers()
+        gidx = (idx + self.i0).to(torch.int32)
+        self.backend.collision_rows_indexed(X_all, gidx, c.R, c.j_max_hi, spec.pos_dim, c.cull_radius, hi["rows"],
+                                            hi["count"])
         g = lambda t: t.index_select(0, idx).contiguous()  # noqa: E731
-        sub = self.backend.qp_solver(spec_hi, n_bad, self.device)
-        o2 = sub.solve(g(self.disc), g(self.sigma), g(X), g(U), g(self.x_init), g(self.x_final), g(self.tr),
-                       g(rows_hi), g(count_hi))
+        o2 = hi["solver"].solve(g(self.disc), g(self.sigma), g(X), g(U), g(self.x_init), g(self.x_final), g(self.tr),
+                                hi["rows"][:n_bad], hi["count"][:n_bad], n=n_bad)
         out = {k: v.clone() for k, v in out.items()}
         for k in ("X", "U", "slack_coll", "nu", "obj", "status", "iters"):
             out[k].index_copy_(0, idx, o2[k])
@@ -145,13 +160,15 @@ class JacobiSCvx:
         self.last_check.update(resolved=n_bad - still, overflow=still)
         return out
 
-    def gather_states(self, X):
-        """All-gather the local states (N,K,n) into X_all (N_total,K,n) -- RCCL over xGMI."""
+    def gather_states(self, X, async_op=False):
+        """All-gather the local states (N,K,n) into X_all (N_total,K,n) -- RCCL over xGMI.  async_op: return
+        a handle whose wait() makes the current stream wait for the collective (overlap with the FOH)."""
         if self.world == 1:
             self.X_all.copy_(X)
-        else:
-            self.torch.distributed.all_gather_into_tensor(self.X_all, X.contiguous(), group=self.group)
-        return self.X_all
+            return None if async_op else self.X_all
+        work = self.torch.distributed.all_gather_into_tensor(self.X_all, X.contiguous(), group=self.group,
+                                                             async_op=async_op)
+        return work if async_op else self.X_all
 
     def _mark(self, marks, name):
         """Record a timing event named `name` on the current (launch) stream (marks: list or None)."""
@@ -169,11 +186,15 @@ class JacobiSCvx:
         torch = self.torch
         spec = self.spec
         self._mark(marks, "start")
+        # the state all-gather (RCCL, its own stream) is issued first and overlaps the FOH launch
+        work = self.gather_states(X, async_op=True) if self.coupling is not None else None
         self.disc = self.backend.foh(spec.model, X, U, self.sigma, self.nsub, self.disc)
         self._mark(marks, "foh")
         rows = count = X_all = None
         if self.coupling is not None:
-            X_all = self.gather_states(X)
+            if work is not None:
+                work.wait()
+            X_all = self.X_all
             self._mark(marks, "gather")
             rows, count = self.backend.collision_rows(X_all, self.i0, self.N, self.coupling.R, spec.j_max,
                                                       spec.pos_dim, self.coupling.cull_radius, self.rows, self.count)

@@ -162,6 +162,15 @@ int scvx_collision_rows_batched(int K, int pos_dim, int n_x, int N_total, const 
                                 int32_t* count, void* stream);
 
 /*
+ * The same rows for an arbitrary subset of agents: local agent a (< N_sel) is global agent idx[a] of X_all
+ * (idx: device int32 [N_sel], distinct values in [0, N_total)).  rows [N_sel][K][j_max][pos_dim+1],
+ * count [N_sel][K].  Used for the agents the full-row check below found violating.
+ */
+int scvx_collision_rows_indexed(int K, int pos_dim, int n_x, int N_total, const double* X_all, const int32_t* idx,
+                                int N_sel, double R, double cull_radius, int j_max, double* rows, int32_t* count,
+                                void* stream);
+
+/*
  * A-posteriori check of the reference's FULL collision row set at a solution (replaces nothing in the
  * reference, which always solves with every row: Distributed_opt/dist_scvx_3d.py:93-107).  For every
  * local agent i, node t < K-1 and every j != i of X_all (the linearisation point):

@@ -289,3 +289,39 @@ def test_collision_rows_keep_the_nearest_neighbours(cuda, j_max):
             got = rows[a, t, :j_max]
             np.testing.assert_allclose(got[np.lexsort(got.T)], ref[np.lexsort(ref.T)], rtol=1e-12, atol=1e-12)
         assert cnt[a, K - 1] == 0
+
+
+def test_indexed_rows_and_partial_solve_match_the_full_launch(cuda):
+    """The re-solve path of the full-row check (scvx_hip/scvx.py JacobiSCvx._enforce_all_rows): rows of an
+    arbitrary subset of agents (scvx_collision_rows_indexed) equal, as sets, the rows the contiguous launch
+    gives those agents; a QPSolver sized for N solving only its first n agents (QPSolver.solve(n=...)) gives
+    bit-identical results to a solver sized for n."""
+    import torch
+    rng = np.random.default_rng(12)
+    N, K, R = 300, 6, 0.5
+    X_all = np.zeros((N, K, 6))
+    X_all[:, :, :3] = rng.normal(scale=2.0, size=(N, K, 3))
+    Xt = _t(X_all, cuda)
+    full, cfull = scvx_hip.collision_rows(Xt, 0, N, R, j_max=16)
+    idx = np.sort(rng.choice(N, 40, replace=False)).astype(np.int32)
+    rows = torch.zeros((64, K, 16, 4), dtype=torch.float64, device=cuda)     # larger buffer: leading 40 written
+    cnt = torch.zeros((64, K), dtype=torch.int32, device=cuda)
+    scvx_hip.collision_rows_indexed(Xt, torch.tensor(idx, device=cuda), R, 16, rows=rows, count=cnt)
+    full, cfull, rows, cnt = full.cpu().numpy(), cfull.cpu().numpy(), rows.cpu().numpy(), cnt.cpu().numpy()
+    for a, gi in enumerate(idx):
+        np.testing.assert_array_equal(cnt[a], cfull[gi])
+        for t in range(K - 1):
+            got, ref = rows[a, t, :cnt[a, t]], full[gi, t, :cfull[gi, t]]
+            np.testing.assert_array_equal(got[np.lexsort(got.T)], ref[np.lexsort(ref.T)])
+    # partial solve
+    from scvx_hip import workloads
+    sc = workloads.synthetic_di(48, K=50, seed=2, obstacles=8)
+    X, U, sig = _t(sc["X"], cuda), _t(sc["U"], cuda), _t(sc["sigma"], cuda)
+    disc = scvx_hip.foh_batched("di", X, U, sig)
+    spec = scvx_hip.QPSpec(model="di", K=50, box=[(0, -12, 12), (1, -12, 12)], obs=sc["obs"], w_obs=1e6, u_max=1.0)
+    n = 17
+    ins = [disc, sig, X, U, _t(sc["x_init"], cuda), _t(sc["x_final"], cuda), _t(np.full(48, 0.25), cuda)]
+    big = scvx_hip.QPSolver(spec, 48, device=cuda).solve(*[v[:n].contiguous() for v in ins], n=n)
+    small = scvx_hip.QPSolver(spec, n, device=cuda).solve(*[v[:n].contiguous() for v in ins])
+    for k in ("X", "U", "obj", "status", "iters"):
+        assert torch.equal(big[k], small[k]), k

@@ -26,14 +26,22 @@ class OracleBackend:
         return torch.from_numpy(d)
 
     def collision_rows(self, X_all, i0, n_local, R, j_max, pos_dim, cull, rows, count):
+        return self.collision_rows_indexed(X_all, torch.arange(i0, i0 + n_local), R, j_max, pos_dim, cull, rows, count)
+
+    def collision_rows_indexed(self, X_all, idx, R, j_max, pos_dim, cull, rows, count):
+        """The j_max nearest neighbours' rows per node (the kernel's selection: largest 2R - |d|), kept in
+        neighbour-index order."""
         Xa = X_all.numpy()
         trajs = [Xa[i] for i in range(Xa.shape[0])]
         rows.zero_(); count.zero_()
-        for a in range(n_local):
-            rr = pb.collision_rows(trajs, i0 + a, R, pos_dim)
+        for a, gi in enumerate(idx.tolist()):
+            rr = pb.collision_rows(trajs, gi, R, pos_dim)
+            others = [j for j in range(Xa.shape[0]) if j != gi]
             for t in range(Xa.shape[1] - 1):
-                rows[a, t, :len(rr[t])] = torch.from_numpy(rr[t])
-                count[a, t] = len(rr[t])
+                dist = [np.linalg.norm(Xa[gi, t, :pos_dim] - Xa[j, t, :pos_dim]) for j in others]
+                keep = sorted(sorted(range(len(others)), key=lambda k: dist[k])[:j_max])
+                rows[a, t, :len(keep)] = torch.from_numpy(rr[t][keep])
+                count[a, t] = len(keep)
         return rows, count
 
     def collision_check(self, X_all, i0, X_new, slack, R, pos_dim, tol):
@@ -61,14 +69,14 @@ class _CpuQP:
         self.tpl = qp_cpu.make_template(6, 3, spec.K, box=spec.box, j_max=spec.j_max, w_coll=spec.w_coll,
                                         tol=spec.tol, max_iter=spec.max_iter)
 
-    def solve(self, disc, sigma, Xref, Uref, x_init, x_final, tr, rows=None, count=None):
+    def solve(self, disc, sigma, Xref, Uref, x_init, x_final, tr, rows=None, count=None, n=None):
         o = qp_cpu.solve_batched(self.tpl, disc.numpy(), sigma.numpy(), Xref.numpy(), Uref.numpy(), x_init.numpy(),
                                  x_final.numpy(), tr.numpy(), rows.numpy(), count.numpy())
         return {k: torch.from_numpy(np.asarray(v)) for k, v in o.items()}
 
 
-def _problem():
-    sc = pb.synthetic_di(N_TOTAL, K=K, seed=4, spread=3.0)  # close starts/goals -> active coupling
+def _problem(n=N_TOTAL):
+    sc = pb.synthetic_di(n, K=K, seed=4, spread=3.0)  # close starts/goals -> active coupling
     return sc
 
 
@@ -123,3 +131,59 @@ def test_sharded_jacobi_matches_single_process():
     assert all(res[r][2] == 0 for r in res)
     # the coupling is live: some node of some agent is pushed by a neighbour row
     assert not np.allclose(X_single, _problem()["X"])
+
+
+N_CULL, J_MAX = 8, 2
+
+
+def _run_culled(rank, world, port, q):
+    """The culled coupling path of the C4 / C5 configurations: the QP keeps the J_MAX nearest rows per node,
+    every reference row is checked at the solution, violating agents are re-solved with all N - 1 rows
+    (j_max_hi), the global trust-region rule all-reduces the cost."""
+    import scvx_hip
+    from scvx_hip.scvx import CouplingSpec, JacobiSCvx
+    if world > 1:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    sc = _problem(N_CULL)
+    n_loc = N_CULL // world
+    sl = slice(rank * n_loc, (rank + 1) * n_loc)
+    T = lambda a: torch.tensor(np.ascontiguousarray(a))
+    spec = scvx_hip.QPSpec(model="di", K=K, box=[(0, -20, 20)], j_max=J_MAX, w_coll=1e4, tol=1e-10, max_iter=80)
+    drv = JacobiSCvx(spec, T(sc["x_init"][sl]), T(sc["x_final"][sl]), T(sc["sigma"][sl]), 0.3,
+                     coupling=CouplingSpec(R=1.0, j_max_hi=N_CULL - 1), tr_rule="global", backend=OracleBackend())
+    X, U = T(sc["X"][sl]).clone(), T(sc["U"][sl]).clone()
+    checks = []
+    for _ in range(ITERS):
+        Xn, Un, out = drv.step(X, U)
+        X, U = Xn.clone(), Un.clone()
+        checks.append(dict(drv.last_check))
+    q.put((rank, X.numpy(), drv.tr.numpy(), checks, int(out["status"].max())))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def test_sharded_culled_coupling_matches_single_process():
+    """World 1 against world 2 (gloo) on the culled path: bit-identical iterates and radii, and the check's
+    counts (violated / re-solved / overflow) summed over the ranks equal to the single process's, at every
+    step.  The dropped rows bind here (some agents violate and are re-solved), so the re-solve path runs."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    _run_culled(0, 1, 0, q)
+    _, X_single, tr_single, ck_single, st = q.get()
+    assert st == 0
+    assert sum(c["violated"] for c in ck_single) > 0           # the culled rows bind: the re-solve path ran
+    assert all(c["overflow"] == 0 for c in ck_single)           # and made every step exact
+    port = _free_port()
+    procs = [ctx.Process(target=_run_culled, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (x, tr, ck, s_)) for r, x, tr, ck, s_ in (q.get(timeout=300) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    np.testing.assert_array_equal(np.concatenate([res[0][0], res[1][0]]), X_single)
+    np.testing.assert_array_equal(res[0][1], tr_single[:N_CULL // 2])
+    for k in range(ITERS):
+        for key in ("violated", "resolved", "overflow"):
+            assert res[0][2][k][key] + res[1][2][k][key] == ck_single[k][key], (k, key)

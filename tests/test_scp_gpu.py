@@ -116,3 +116,22 @@ def test_scproblem_second_iterate_and_iteration_count(cuda):
     assert abs(obj - ref["obj"]) <= 1e-7 * abs(ref["obj"])
     assert abs(g["sigma"][0] - ref["sigma"]) < 1e-6
     assert abs(int(g["iters"][0]) - cpu["iters"]) <= 2
+
+
+@pytest.mark.parametrize("K", [30, 100])
+def test_scproblem_lp_value_matches_highs(cuda, K):
+    """The SCP kernel's optimal value on the SCProblem LPs (unicycle: no SOC, the objective is linear)
+    against SciPy's HiGHS on the reference-form assembly -- a solver that shares nothing with either the
+    kernel or oracle/scp_dense.py (tests/test_independent_checks_cpu.py checks the oracles the same way).
+    Trust radii 100 (inactive), 5 and 1 (binding).  Value 1e-7 relative (the kernel's tolerance 1e-9)."""
+    import torch
+    from oracle import scp_dense as sd
+    from test_independent_checks_cpu import _uni_instances, highs_value
+    probs = _uni_instances(K)
+    g = solve_gpu(probs, torch, cuda)
+    assert np.isin(g["status"], (0, 1)).all(), g["status"]
+    for a, p in enumerate(probs):
+        v = highs_value(p)
+        obj = sd.scp_objective(p, g["X"][a], g["U"][a], g["nu"][a], float(g["sigma"][a]))
+        assert abs(obj - v) <= 1e-7 * max(1.0, abs(v)), (a, obj, v)
+        assert sd.scp_violation(p, g["X"][a], g["U"][a], g["nu"][a], float(g["sigma"][a])) < 1e-7
