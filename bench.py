@@ -93,7 +93,7 @@ def qp_rows(n, m, n_box, n_obs, j_max, soc):
     return (1 << m) + 2 * n_box + 2 * n_obs + (j_max + 1 if j_max else 0) + ((m + 1) if soc else 0)
 
 
-def committed_traffic(kernel_prefix="scvx::qp_ipm_kernel<scvx::QPCfg<6, 3, 2, 8, 0>"):
+def committed_traffic(kernel_prefix="scvx::qp_ipm_kernel<scvx::QPCfg<6, 3, 2, 8, 0, 0>"):
     """HBM-side bytes per launch of the dominant kernel from the newest committed rocprofv3 --pmc
     summary (profiles/*_pmc_traffic.json, made by tools/pmc_summary.py from separate FETCH_SIZE /
     WRITE_SIZE passes of this same bench, gfx950 FETCH_SIZE x2 correction applied); None if absent."""

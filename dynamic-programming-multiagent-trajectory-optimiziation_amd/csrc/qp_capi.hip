@@ -98,7 +98,8 @@ extern "C" int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const d
                                      const double* Xref, const double* Uref, const double* x_init,
                                      const double* x_final, const double* tr, const double* coll_rows,
                                      const int32_t* coll_count, double* X, double* U, double* slack_coll,
-                                     double* nu, double* obj, int32_t* status, int32_t* iters, void* workspace,
+                                     double* nu, double* obj, int32_t* status, int32_t* iters,
+                                     const int32_t* warm, void* workspace,
                                      size_t workspace_bytes, void* stream) {
     const ModelTable* mt = nullptr;
     int cls = -1;
@@ -112,13 +113,14 @@ extern "C" int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const d
         return set_error(SCVX_EINVAL, "qp: w_final > 0 (soft terminal) needs has_final = 0");
     if (tpl->j_max > 0 && (!coll_rows || !coll_count)) return set_error(SCVX_EINVAL, "qp: collision rows required");
     if (tpl->w_nu > 0.0 && !nu) return set_error(SCVX_EINVAL, "qp: nu output required (w_nu > 0)");
+    if (warm && tpl->K < 2 * tpl->n_x) return set_error(SCVX_EUNSUPPORTED, "qp: warm start needs K >= 2 n_x");
     const size_t need = ws_bytes(*mt, cls, N, tpl->K);
     if (!workspace || workspace_bytes < need) return set_error(SCVX_EWORKSPACE, "qp: workspace too small");
     QPArgs a{};
     a.T = *tpl;
     a.N = N;
     a.disc = disc; a.sigma = sigma; a.Xref = Xref; a.Uref = Uref; a.x_init = x_init; a.x_final = x_final;
-    a.tr = tr; a.coll_rows = coll_rows; a.coll_count = coll_count;
+    a.tr = tr; a.coll_rows = coll_rows; a.coll_count = coll_count; a.warm = warm;
     a.X = X; a.U = U; a.slack_coll = slack_coll; a.nu = nu; a.obj = obj; a.status = status; a.iters = iters;
     a.ws = (double*)workspace;
     a.ws_agent = (long long)(need / sizeof(double) / (size_t)N);

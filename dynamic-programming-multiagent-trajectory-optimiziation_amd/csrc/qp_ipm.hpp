@@ -57,6 +57,7 @@ struct QPArgs {
     const double* tr;
     const double* coll_rows;
     const int32_t* coll_count;
+    const int32_t* warm; // per agent: start from the state this workspace holds from the agent's last solve
     double* X;
     double* U;
     double* slack_coll;
@@ -82,9 +83,11 @@ constexpr int qp_gpk(int nx, int nu, int nv = 0) {
 constexpr int qp_even(int x) { return (x + 1) & ~1; }
 // workspace columns (K doubles each: one per node) of a capacity class
 constexpr int qp_ncol(int nx, int nu, int nb, int ns, int ng, int nv = 0) {
-    // disc^T | Bt | soft rows | groups | rd | r1a | cP | ub | node state | SOC | virtual control state
+    // disc^T | Bt | soft rows | groups | rd | r1a | cP | ub | node state | SOC | virtual control state |
+    // warm-start state (row duals, initial / terminal multipliers)
     return qp_dstr(nx, nu) + nx * nu + 4 * ns + 4 * ng + (nx + nu) + ng + ((1 << nu) + 2 * nb + ns + ng) + nu +
-           ((nx + nu) + nx + 2 * (nu + 1) + ng) + (3 * (nu + 1) + 1 + (nu + 1)) + 11 * nv;
+           ((nx + nu) + nx + 2 * (nu + 1) + ng) + (3 * (nu + 1) + 1 + (nu + 1)) + 11 * nv +
+           ((1 << nu) + 2 * nb + ns + ng) + 1;
 }
 // factor outputs per stage (stage-major block): K, kappa, LD, W2, P, Pi, u, Acl, [virtual control: G^-1 P,
 // G^-1 Pi, G^-1, Acl~], one junk slot (the global store of lanes without an output of their own)
@@ -97,6 +100,8 @@ constexpr long long qp_ws_doubles(int nx, int nu, int nb, int ns, int ng, int K,
 }
 // byte offset of every access of a lane without a node (t >= K): beyond num_records of any workspace
 constexpr int QP_OOB = 0x40000000;
+// warm start: floor of every slack and dual of the previous iterate (scaled units; oracle/scvx_cpu.cpp)
+constexpr double QP_WARM_ETA = 1e-3;
 
 // VC_ = 1: the virtual-control class (scvx_qp_template.w_nu > 0): nu_t in every dynamics row, priced
 // w_nu ||nu_t||_1 through its epigraph -e <= nu <= e.  nu is eliminated inside each Riccati stage
@@ -188,7 +193,10 @@ struct QPCfg {
     // (nu, e parts)
     static constexpr int C_VN = C_RHO + NQ, C_VE = C_VN + NV, C_VS = C_VE + NV, C_VL = C_VS + 2 * NV,
                          C_VRE = C_VL + 2 * NV, C_VCP = C_VRE + NV, C_VRD = C_VCP + 2 * NV;
-    static constexpr int NCOL = C_VRD + 2 * NV;
+    // warm start: the row duals lambda_r at the last iterate (NR), and y_init (lanes 0..NX-1) / y_fin (lanes
+    // NX..2NX-1) in one column (needs K >= 2 NX: the host checks)
+    static constexpr int C_WL = C_VRD + 2 * NV, C_WY = C_WL + NR;
+    static constexpr int NCOL = C_WY + 1;
     static_assert(NCOL == qp_ncol(NX, NU, NB, NS, NG, NV), "column count");
     // LDS (doubles, compile-time offsets except the K-sized blocks at the end):
     // factor: the current stage's packet, P', Pi' (col-major), T1, T2 (col-major), W1, W2 (col-major), Qh,
@@ -341,6 +349,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     // virtual control (VC classes): weight of the epigraph variables e; lanes t < K-1 carry nu_t
     if (NV > 0) qnorm = fmax(qnorm, T.w_nu);
     const bool vact = NV > 0 && act && t < K - 1;
+    const bool warm = a.warm != nullptr && a.warm[agent] != 0;   // wave-uniform
     // proximal term w_prox ||x_t - xbar_t||^2 (every node): linear term -2 w_prox xbar_t
     const bool prox = T.w_prox > 0.0;
     if (prox) {
@@ -493,22 +502,24 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
         // initial node state: z = (xbar, ubar), y = 0, slack groups 0
 #pragma unroll
-        for (int i = 0; i < NX; ++i) {
-            cst(C::C_Z + i, act ? a.Xref[(agent * K + t) * NX + i] : 0.0);
-            cst(C::C_Y + i, 0.0);
+        for (int j = 0; j < NU; ++j) cst(C::C_UB + j, act ? a.Uref[(agent * K + t) * NU + j] : 0.0);
+        if (warm) {   // the last solve's primal / dual state stays in place; its y_init / y_fin to LDS
+            if (lane < 2 * NX) lds[V_YI + lane] = wb.ld(vt, C::C_WY * colb);   // (V_YF = V_YI + NX)
+        } else {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                cst(C::C_Z + i, act ? a.Xref[(agent * K + t) * NX + i] : 0.0);
+                cst(C::C_Y + i, 0.0);
+            }
+#pragma unroll
+            for (int j = 0; j < NU; ++j) cst(C::C_Z + NX + j, act ? a.Uref[(agent * K + t) * NU + j] : 0.0);
+#pragma unroll
+            for (int g = 0; g < NG; ++g) cst(C::C_AV + g, 0.0);
+#pragma unroll
+            for (int i = 0; i < NV; ++i) { cst(C::C_VN + i, 0.0); cst(C::C_VE + i, 0.0); }
+            if (lane < NX) { lds[V_YI + lane] = 0.0; lds[V_YF + lane] = 0.0; }
         }
-#pragma unroll
-        for (int j = 0; j < NU; ++j) {
-            const double u = act ? a.Uref[(agent * K + t) * NU + j] : 0.0;
-            cst(C::C_UB + j, u);
-            cst(C::C_Z + NX + j, u);
-        }
-#pragma unroll
-        for (int g = 0; g < NG; ++g) cst(C::C_AV + g, 0.0);
-#pragma unroll
-        for (int i = 0; i < NV; ++i) { cst(C::C_VN + i, 0.0); cst(C::C_VE + i, 0.0); }
         if (lane == 0) lds[V_ONE] = 1.0;
-        if (lane < NX) { lds[V_YI + lane] = 0.0; lds[V_YF + lane] = 0.0; }
         if (lane < 16) lds[V_ST + lane] = 0.0;
     }
     // C_{t-1} (column-major as disc) of this node, from the transposed disc of node t-1 (the lane below)
@@ -1613,9 +1624,45 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     int it = 0;
     double fail_code = 0.0;
     // ------------------------------------------------------------------ starting point
+    if (warm) {
+        // warm start (the Jacobi SCvx loop re-solves each agent's subproblem re-linearised at its own last
+        // solution): z, y, the group and SOC duals and the row duals are the last iterate's; the slacks are
+        // recomputed from this solve's rows at z; every slack and dual is floored at QP_WARM_ETA inside its
+        // cone (oracle/scvx_cpu.cpp warm_point does the same).  C3: 12.3 -> ~5 IPM iterations on average.
+        load_state();
+        double wl[NR];
+        ldn(wl, C::C_WL, NR);
+        hold(wl, NR);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            double gz, h;
+            row_eval(r, z, av, gz, h);
+            const bool on = row_on(r);
+            s_(r) = on ? fmax(h - gz, QP_WARM_ETA) : 1.0;
+            l_(r) = on ? fmax(wl[r], QP_WARM_ETA) : 0.0;
+        }
+        if (soc) {
+            double nu2 = 0.0, nl2 = 0.0;
+            sq[0] = T.u_max;
+#pragma unroll
+            for (int j = 0; j < NU; ++j) { sq[1 + j] = z[NX + j]; nu2 += z[NX + j] * z[NX + j]; nl2 += lq[1 + j] * lq[1 + j]; }
+            sq[0] = fmax(sq[0], sqrt(nu2) + QP_WARM_ETA);
+            lq[0] = fmax(lq[0], sqrt(nl2) + QP_WARM_ETA);
+        } else {
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) { sq[j] = 0.0; lq[j] = 0.0; }
+        }
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            vs[2 * i] = vact ? fmax(ve[i] - vn[i], QP_WARM_ETA) : 1.0;
+            vs[2 * i + 1] = vact ? fmax(ve[i] + vn[i], QP_WARM_ETA) : 1.0;
+            vl[2 * i] = vact ? fmax(vl[2 * i], QP_WARM_ETA) : 0.0;
+            vl[2 * i + 1] = vact ? fmax(vl[2 * i + 1], QP_WARM_ETA) : 0.0;
+        }
+        store_state();
+    } else {
     // minimiser of 1/2 z'Pz + q'z + 1/2 ||Gz - h||^2 s.t. Az = b from z_ref (aux = 0), unit scaling
     // (CVXOPT coneqp initialisation; oracle/qp_dense.py does the same on the dense form)
-    {
         fresh();
         double dt[C::DSTR];
         issue_state();
@@ -2285,6 +2332,10 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 
     // ------------------------------------------------------------------ outputs
     load_state();
+    // the warm-start state of the next solve: row duals and the initial / terminal multipliers
+#pragma unroll
+    for (int r = 0; r < NR; ++r) cst(C::C_WL + r, l_(r));
+    cst(C::C_WY, lane < 2 * NX ? lds[V_YI + lane] : 0.0);
     if (a.trace && agent == a.trace_agent && lane == 0) {
         double* dd = a.trace + 8 * a.trace_cap;
         dd[0] = 0.0; dd[1] = 0.0; dd[2] = (double)(__builtin_amdgcn_s_memtime() - cyc_all0);

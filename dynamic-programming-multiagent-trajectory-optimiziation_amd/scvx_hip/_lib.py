@@ -93,7 +93,7 @@ def lib():
         L.scvx_integrate_nonlinear_batched.argtypes = [i32, vp, i32, i32, vp, vp, vp, i32, i32, vp, vp]
         L.scvx_qp_workspace_bytes.argtypes = [ctypes.POINTER(QPTemplate), i32]
         L.scvx_qp_workspace_bytes.restype = sz
-        L.scvx_qp_solve_batched.argtypes = [ctypes.POINTER(QPTemplate), i32] + [vp] * 16 + [vp, sz, vp]
+        L.scvx_qp_solve_batched.argtypes = [ctypes.POINTER(QPTemplate), i32] + [vp] * 17 + [vp, sz, vp]
         L.scvx_qp_set_trace.argtypes = [vp, i32, i32]
         L.scvx_collision_rows_batched.argtypes = [i32, i32, i32, i32, vp, i32, i32, dbl, dbl, i32, vp, vp, vp]
         L.scvx_collision_rows_indexed.argtypes = [i32, i32, i32, i32, vp, vp, i32, dbl, dbl, i32, vp, vp, vp]

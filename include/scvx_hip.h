@@ -132,6 +132,12 @@ typedef struct scvx_qp_template {
  *   X [N][K][n], U [N][K][m], slack_coll [N][K] (S_t, zeros if j_max = 0),
  *   nu [N][K-1][n] (virtual control; required iff w_nu > 0, may be NULL otherwise), obj [N],
  *   status [N], iters [N]
+ * warm [N] (device int32, may be NULL): agents with warm[a] != 0 start from the primal-dual point their
+ *   previous solve left in this workspace (same template, same agent slot): z, the multipliers and the
+ *   inequality duals are kept, the slacks recomputed from the new rows, every slack / dual floored
+ *   inside its cone.  The optimum and the stopping rule are unchanged; the Jacobi SCvx loop, which
+ *   re-solves each agent re-linearised at its own solution, needs ~2.4x fewer IPM iterations (C3).
+ *   Requires K >= 2 n_x.  warm = NULL (or all 0): the CVXOPT-style cold start.
  * workspace: caller-owned device scratch of at least scvx_qp_workspace_bytes(tpl, N) bytes.
  * Limits: 2 <= K <= 64 (one node per lane), n_u <= 4, <= 64 inequality rows per node.
  */
@@ -139,7 +145,7 @@ int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const double* disc
                           const double* Xref, const double* Uref, const double* x_init, const double* x_final,
                           const double* tr, const double* coll_rows, const int32_t* coll_count, double* X,
                           double* U, double* slack_coll, double* nu, double* obj, int32_t* status, int32_t* iters,
-                          void* workspace, size_t workspace_bytes, void* stream);
+                          const int32_t* warm, void* workspace, size_t workspace_bytes, void* stream);
 
 /* Bytes of caller-owned device scratch scvx_qp_solve_batched needs for N agents. */
 size_t scvx_qp_workspace_bytes(const scvx_qp_template* tpl, int N);

@@ -53,7 +53,16 @@ def _p(a, ty=ctypes.c_double):
     return a.ctypes.data_as(ctypes.POINTER(ty))
 
 
-def solve_batched(tpl, disc, sigma, Xref, Uref, x_init, x_final, tr, coll_rows=None, coll_count=None, nthreads=1):
+def warm_doubles(tpl):
+    lib = foh_oracle.lib()
+    lib.oracle_qp_warm_doubles.restype = ctypes.c_longlong
+    return int(lib.oracle_qp_warm_doubles(ctypes.byref(tpl)))
+
+
+def solve_batched(tpl, disc, sigma, Xref, Uref, x_init, x_final, tr, coll_rows=None, coll_count=None, nthreads=1,
+                  warm=None, wstate=None):
+    """warm (N,) int32 / wstate (N, warm_doubles(tpl)) float64 (experiment): agents with warm[a] != 0 start
+    from the primal-dual state a previous call left in wstate[a]; every call writes its final state there."""
     """All arrays agent-major numpy float64 (see include/scvx_hip.h).  Returns dict of outputs."""
     lib = foh_oracle.lib()
     if not hasattr(lib, "_qp_ready"):
@@ -74,7 +83,9 @@ def solve_batched(tpl, disc, sigma, Xref, Uref, x_init, x_final, tr, coll_rows=N
     rc = lib.oracle_qp_solve_batched(ctypes.byref(tpl), N, _p(disc), _p(sigma), _p(Xref), _p(Uref), _p(x_init),
                                      _p(x_final), _p(tr), _p(coll_rows), _p(coll_count, ctypes.c_int32), _p(X),
                                      _p(U), _p(S), _p(nu), _p(obj), _p(st, ctypes.c_int32), _p(it, ctypes.c_int32),
-                                     int(nthreads))
+                                     int(nthreads),
+                                     _p(warm, ctypes.c_int32) if warm is not None else None,
+                                     _p(wstate) if wstate is not None else None)
     if rc != 0:
         raise ValueError("oracle_qp_solve_batched failed")
     return dict(X=X, U=U, slack_coll=S, nu=nu, obj=obj, status=st, iters=it)

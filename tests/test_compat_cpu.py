@@ -136,7 +136,7 @@ def test_library_exports_every_header_symbol():
     assert rc == -1 and b"bad args" in L.scvx_last_error()
     t = _lib.QPTemplate()
     t.K = 100
-    assert L.scvx_qp_solve_batched(ctypes.byref(t), 1, *([None] * 16), None, 0, None) == -2
+    assert L.scvx_qp_solve_batched(ctypes.byref(t), 1, *([None] * 17), None, 0, None) == -2
     assert L.scvx_version() >= 2   # v2: w_nu / w_prox template fields, the nu output
 
 

@@ -69,7 +69,7 @@ class _CpuQP:
         self.tpl = qp_cpu.make_template(6, 3, spec.K, box=spec.box, j_max=spec.j_max, w_coll=spec.w_coll,
                                         tol=spec.tol, max_iter=spec.max_iter)
 
-    def solve(self, disc, sigma, Xref, Uref, x_init, x_final, tr, rows=None, count=None, n=None):
+    def solve(self, disc, sigma, Xref, Uref, x_init, x_final, tr, rows=None, count=None, n=None, warm=None):
         o = qp_cpu.solve_batched(self.tpl, disc.numpy(), sigma.numpy(), Xref.numpy(), Uref.numpy(), x_init.numpy(),
                                  x_final.numpy(), tr.numpy(), rows.numpy(), count.numpy())
         return {k: torch.from_numpy(np.asarray(v)) for k, v in o.items()}

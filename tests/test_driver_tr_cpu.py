@@ -12,7 +12,7 @@ class _StubQP:
     def __init__(self, status):
         self.status = status
 
-    def solve(self, disc, sigma, Xref, Uref, x_init, x_final, tr, rows=None, count=None):
+    def solve(self, disc, sigma, Xref, Uref, x_init, x_final, tr, rows=None, count=None, n=None, warm=None):
         N = Xref.shape[0]
         return {"X": Xref + 1.0, "U": Uref * 0.5, "slack_coll": torch.zeros(N, Xref.shape[1], dtype=torch.float64),
                 "obj": torch.zeros(N, dtype=torch.float64), "status": self.status.clone(),

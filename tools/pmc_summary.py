@@ -27,7 +27,7 @@ def collect(prefix, kernel):
     return {c: sum(v.values()) / len(v) for c, v in per.items()}, names
 
 
-def main(prefix, out, kernel="qp_ipm_kernel<scvx::QPCfg<6, 3, 2, 8, 0>"):
+def main(prefix, out, kernel="qp_ipm_kernel<scvx::QPCfg<6, 3, 2, 8, 0, 0>"):
     c, names = collect(prefix, kernel)
     res = {"kernel": next(iter(names.values()), kernel).split("(")[0].replace("void ", ""),
            "source": prefix + "_*", "raw_per_launch": c}
