@@ -6,8 +6,12 @@ Same constructor, attributes (model, K, n_x, n_u, dt, f, A, B) and methods; same
 per-interval matrices, :75-85) and the same ownership rule: the returned arrays belong to the object
 and are overwritten by the next call (:20-24, :87).  The reference integrates with LSODA; the kernels
 use fixed-step RK4 on the equivalent forward-sensitivity system (agreement ~1e-8 relative, the
-LSODA tolerance; tests/test_foh_gpu.py).  There is no CPU fallback: a model without device
-dynamics (attribute `scvx_model`) is rejected.
+LSODA tolerance; tests/test_foh_gpu.py).  Models: the four built-in device models (attribute
+`scvx_model`, or the drop-in model classes), or ANY other model -- its f/A/B are compiled for the GPU at
+run time (scvx_hip.rtc.DeviceModel, hipRTC): `model.scvx_device_model` if the model provides one,
+otherwise the model's own get_equations() callables re-traced symbolically (the reference's models are
+sympy-lambdified numpy, which traces exactly).  There is no CPU fallback: a model that neither names
+device dynamics nor traces is rejected.
 """
 import numpy as np
 
@@ -18,13 +22,33 @@ _BY_CLASS = {"UnicycleModel": "unicycle", "SingleIntegratorModel": "si", "Double
 
 
 def device_model(model):
+    """Built-in model name ("di" | "unicycle" | "si" | "quad") or a runtime-compiled DeviceModel."""
+    dm = getattr(model, "scvx_device_model", None)
+    if dm is not None:
+        if dm.dims != (model.n_x, model.n_u):
+            raise ValueError(f"{type(model).__name__}: scvx_device_model dims {dm.dims} != (n_x, n_u)")
+        return dm
     name = getattr(model, "scvx_model", "") or _BY_CLASS.get(type(model).__name__, "")
-    if name not in scvx_hip.MODEL_DIMS:
-        raise ValueError(f"{type(model).__name__}: no device dynamics for the MI355X FOH kernel "
-                         f"(set model.scvx_model to one of {sorted(scvx_hip.MODEL_DIMS)})")
-    if scvx_hip.MODEL_DIMS[name] != (model.n_x, model.n_u):
-        raise ValueError(f"{type(model).__name__}: n_x/n_u do not match device model {name!r}")
-    return name
+    if name:
+        if name not in scvx_hip.MODEL_DIMS:
+            raise ValueError(f"{type(model).__name__}: unknown device model {name!r} "
+                             f"(built-in: {sorted(scvx_hip.MODEL_DIMS)})")
+        if scvx_hip.MODEL_DIMS[name] != (model.n_x, model.n_u):
+            raise ValueError(f"{type(model).__name__}: n_x/n_u do not match device model {name!r}")
+        return name
+    from scvx_hip.rtc import DeviceModel
+    f, A, B = model.get_equations()
+    return DeviceModel.from_callables(f, A, B, model.n_x, model.n_u)
+
+
+def builtin_model(model, what):
+    """The built-in device model name of `model`, for the kernels that are compiled per model class
+    (the SCP subproblem, the inter-sample search): a runtime-compiled user model is rejected loudly."""
+    dm = device_model(model)
+    if not isinstance(dm, str):
+        raise NotImplementedError(f"{what}: compiled for the built-in models {sorted(scvx_hip.MODEL_DIMS)}; "
+                                  f"{type(model).__name__} runs on the runtime-compiled FOH path only")
+    return dm
 
 
 class FirstOrderHold:
@@ -55,23 +79,32 @@ class FirstOrderHold:
     def calculate_discretization(self, X, U, sigma):
         """X (n_x, K), U (n_u, K), sigma -> (A_bar, B_bar, C_bar, S_bar, z_bar)."""
         Xd, Ud, sd = self._to_dev(X, U, sigma)
-        disc = scvx_hip.foh_batched(self._name, Xd, Ud, sd, nsub=self._nsub, params=self._params)
-        outs = scvx_hip.unpack_disc(disc[0], self._name)
+        if isinstance(self._name, str):
+            disc = scvx_hip.foh_batched(self._name, Xd, Ud, sd, nsub=self._nsub, params=self._params)
+            outs = scvx_hip.unpack_disc(disc[0], self._name)
+        else:
+            disc = self._name.foh(Xd, Ud, sd, nsub=self._nsub, params=self._params)
+            outs = self._name.unpack_disc(disc[0])
         for dst, src in zip((self.A_bar, self.B_bar, self.C_bar, self.S_bar, self.z_bar), outs):
             dst[...] = src.cpu().numpy()
         return self.A_bar, self.B_bar, self.C_bar, self.S_bar, self.z_bar
 
     def integrate_nonlinear_piecewise(self, X_lin, U, sigma):
         Xd, Ud, sd = self._to_dev(X_lin, U, sigma)
-        out = scvx_hip.integrate_nonlinear(self._name, Xd, Ud, sd, True, params=self._params)
+        out = self._roll(Xd, Ud, sd, True)
         return out[0].cpu().numpy().T.copy()
 
     def integrate_nonlinear_full(self, x0, U, sigma):
         X = np.zeros((self.n_x, self.K))
         X[:, 0] = np.asarray(x0, float).reshape(-1)
         Xd, Ud, sd = self._to_dev(X, U, sigma)
-        out = scvx_hip.integrate_nonlinear(self._name, Xd, Ud, sd, False, params=self._params)
+        out = self._roll(Xd, Ud, sd, False)
         return out[0].cpu().numpy().T.copy()
+
+    def _roll(self, Xd, Ud, sd, piecewise):
+        if isinstance(self._name, str):
+            return scvx_hip.integrate_nonlinear(self._name, Xd, Ud, sd, piecewise, params=self._params)
+        return self._name.integrate_nonlinear(Xd, Ud, sd, piecewise, params=self._params)
 
     def _dx(self, x, t, u0, u1, sigma):
         """Nonlinear dynamics in physical time with u interpolated by t/(dt*sigma) (:157-162); host-side,

@@ -17,7 +17,7 @@ import numpy as np
 
 import scvx_hip
 
-from ..discretization.first_order_hold import device_model
+from ..discretization.first_order_hold import builtin_model
 from ..global_parameters import K as GLOBAL_K
 from .variables import Parameter, ParameterError, ProblemResult, SolverError, Variable
 
@@ -49,7 +49,7 @@ class SCProblem:
         self.n_u = model.n_u
         self.K = GLOBAL_K
         self.device = device
-        self._dev_model = device_model(model)
+        self._dev_model = builtin_model(model, "SCProblem")
         n, m, K = self.n_x, self.n_u, self.K
         self.var = {"X": Variable((n, K), name="X"), "U": Variable((m, K), name="U"),
                     "nu": Variable((n, K - 1), name="nu"), "sigma": Variable((), name="sigma", nonneg=True)}

@@ -20,7 +20,7 @@ import numpy as np
 
 import scvx_hip
 
-from ..discretization.first_order_hold import FirstOrderHold, device_model
+from ..discretization.first_order_hold import FirstOrderHold, builtin_model
 from ..global_parameters import CONV_TOL, MAX_ITER, TRUST_RADIUS0, WEIGHT_NU, WEIGHT_SIGMA, WEIGHT_SLACK, K
 from ..utils.logging import Logger
 from .sc_problem import SCProblem, _solver
@@ -41,9 +41,9 @@ class BatchedSCVXSolver:
         self.weight_nu = WEIGHT_NU
         self.weight_slack = WEIGHT_SLACK
         self.weight_sigma = WEIGHT_SIGMA
-        self._name = device_model(self.models[0])
+        self._name = builtin_model(self.models[0], "BatchedSCVXSolver")
         for m in self.models[1:]:
-            if device_model(m) != self._name:
+            if builtin_model(m, "BatchedSCVXSolver") != self._name:
                 raise ValueError("BatchedSCVXSolver: all agents must share one model class")
         self.problems = [SCProblem(m, device=device) for m in self.models]
         self.loggers = [Logger() for _ in self.models]

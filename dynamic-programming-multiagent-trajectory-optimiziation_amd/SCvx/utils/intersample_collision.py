@@ -20,7 +20,7 @@ import numpy as np
 
 import scvx_hip
 
-from ..discretization.first_order_hold import device_model
+from ..discretization.first_order_hold import builtin_model
 
 
 def _t(a, device):
@@ -33,7 +33,7 @@ class SegmentRollout:
     tau in [0, t dt_phys], dt_phys = foh.dt * sigma (make_segment_f, :104-126)."""
 
     def __init__(self, foh, u0, u1, sigma):
-        self.model = device_model(foh.model)
+        self.model = builtin_model(foh.model, "SegmentRollout")
         self.params = getattr(foh.model, "scvx_params", None)
         self.device = getattr(foh, "_device", "cuda")
         self.u0 = np.asarray(u0, float).reshape(-1)
@@ -134,7 +134,7 @@ def segment_minima(foh, X: np.ndarray, U: np.ndarray, obstacles: Sequence, T, si
     """All segments x obstacles of one trajectory (X (n,K), U (m,K)) in one kernel launch:
     {(k, obstacle_index): [(t*, h0, grad_x, grad_u), ...]} -- what game_si_model.py:156-176
     computes with K-1 make_segment_f / find_critical_times / linearize_h rounds."""
-    model = device_model(foh.model)
+    model = builtin_model(foh.model, "segment_minima")
     dev = getattr(foh, "_device", "cuda")
     K = X.shape[1]
     out = scvx_hip.intersample_batched(model, _t(np.asarray(X, float).T[None], dev), _t(np.asarray(U, float).T[None], dev),

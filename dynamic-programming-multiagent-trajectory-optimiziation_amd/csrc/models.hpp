@@ -12,11 +12,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-namespace scvx {
+#include "foh_body.hpp"  // ModelParams
 
-struct ModelParams {
-    double p[8];  // quadrotor: mass, g, Jx, Jy, Jz
-};
+namespace scvx {
 
 struct DoubleIntegrator3D {
     static constexpr int N = 6, M = 3, ID = 0;

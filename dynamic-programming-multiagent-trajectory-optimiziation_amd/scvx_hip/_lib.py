@@ -20,7 +20,10 @@ EXPORTS = ("scvx_version", "scvx_last_error", "scvx_foh_batched", "scvx_integrat
            "scvx_qp_solve_batched", "scvx_qp_workspace_bytes", "scvx_qp_set_trace",
            "scvx_collision_rows_batched", "scvx_collision_rows_indexed", "scvx_collision_check_batched", "scvx_scp_solve_batched", "scvx_scp_workspace_bytes",
            "scvx_intersample_batched", "scvx_admm_consensus_batched", "scvx_scp_game_solve_batched",
-           "scvx_slab_update_batched", "scvx_jacobi_update_batched")
+           "scvx_slab_update_batched", "scvx_jacobi_update_batched", "scvx_rtc_model_create",
+           "scvx_rtc_model_source", "scvx_rtc_model_log", "scvx_rtc_model_destroy", "scvx_rtc_foh_batched",
+           "scvx_rtc_integrate_nonlinear_batched")
+SCVX_MAX_MODEL_PARAMS, SCVX_RTC_MAX_NX, SCVX_RTC_MAX_NU = 16, 16, 8
 
 
 class ScvxError(RuntimeError):
@@ -106,7 +109,17 @@ def lib():
         L.scvx_scp_game_solve_batched.argtypes = [ctypes.POINTER(SCPTemplate), i32] + [vp] * 18 + [vp, sz, vp]
         L.scvx_slab_update_batched.argtypes = [i32, i32, i32, i32, i32, vp, vp, vp, vp]
         L.scvx_jacobi_update_batched.argtypes = [i32, i32, i32, i32] + [vp] * 9 + [i32, dbl, dbl, vp]
-        sized = ("scvx_last_error", "scvx_qp_workspace_bytes", "scvx_scp_workspace_bytes")
+        cpp = ctypes.POINTER(ctypes.c_char_p)
+        L.scvx_rtc_model_create.argtypes = [i32, i32, cpp, cpp, cpp, ctypes.c_char_p, ctypes.POINTER(vp)]
+        L.scvx_rtc_model_source.argtypes = [vp]
+        L.scvx_rtc_model_source.restype = ctypes.c_char_p
+        L.scvx_rtc_model_log.argtypes = [vp]
+        L.scvx_rtc_model_log.restype = ctypes.c_char_p
+        L.scvx_rtc_model_destroy.argtypes = [vp]
+        L.scvx_rtc_foh_batched.argtypes = [vp, vp, i32, i32, i32, vp, vp, vp, i32, vp, vp]
+        L.scvx_rtc_integrate_nonlinear_batched.argtypes = [vp, vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp]
+        sized = ("scvx_last_error", "scvx_qp_workspace_bytes", "scvx_scp_workspace_bytes", "scvx_rtc_model_source",
+                 "scvx_rtc_model_log")
         for fn in EXPORTS:
             getattr(L, fn).restype = getattr(L, fn).restype if fn in sized else i32
         _lib = L

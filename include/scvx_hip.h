@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define SCVX_HIP_VERSION 2
+#define SCVX_HIP_VERSION 3
 
 #define SCVX_OK 0
 #define SCVX_EINVAL (-1)
@@ -64,6 +64,48 @@ int scvx_foh_batched(int model_id, const double* params, int K, int N, const dou
 int scvx_integrate_nonlinear_batched(int model_id, const double* params, int K, int N, const double* X,
                                      const double* U, const double* sigma, int nsub, int piecewise,
                                      double* Xout, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Runtime-compiled user models (hipRTC).  The reference's FirstOrderHold(model, K) integrates ANY
+ * BaseModel through its numpy f/A/B callables (SCvx/discretization/first_order_hold.py:13-50,
+ * 89-125; SCvx/models/base_model.py:16-24).  Here a user model is given as C expressions and
+ * compiled for gfx950 at run time into the same RK4 forward-sensitivity kernel the built-in models
+ * use (csrc/foh_body.hpp); no CPU path exists.
+ *
+ * Expressions are HIP C++ double expressions in x[0..n_x), u[0..n_u), p[0..SCVX_MAX_MODEL_PARAMS)
+ * (the params array of the launch) and any name the prelude defines:
+ *   f_exprs  n_x entries         f_i(x, u)
+ *   A_exprs  n_x*n_x, row-major  dA_ij = d f_i / d x_j
+ *   B_exprs  n_x*n_u, row-major  dB_ij = d f_i / d u_j
+ * A NULL entry, "" or "0" is a structural zero (skipped in the generated matrix-vector products).
+ * prelude: optional statements (e.g. `const double c2 = cos(x[2]);`) evaluated before the
+ * expressions in each of f, A and B.  n_x <= 16, n_u <= 8.
+ *
+ * scvx_rtc_model_create compiles (no GPU needed); the code object is loaded on the calling
+ * thread's current device at the first launch.  On a compile error it returns SCVX_EINVAL with
+ * *out set to a model that holds only the generated source and the compiler log (read them with
+ * scvx_rtc_model_source / _log, then destroy it; launches on it fail); other errors leave *out NULL.
+ * ------------------------------------------------------------------------------------------ */
+#define SCVX_MAX_MODEL_PARAMS 16
+#define SCVX_RTC_MAX_NX 16
+#define SCVX_RTC_MAX_NU 8
+typedef struct scvx_rtc_model scvx_rtc_model;
+
+int scvx_rtc_model_create(int n_x, int n_u, const char* const* f_exprs, const char* const* A_exprs,
+                          const char* const* B_exprs, const char* prelude, scvx_rtc_model** out);
+/* generated HIP source (for inspection) and the last compile log; buffers are the model's */
+const char* scvx_rtc_model_source(const scvx_rtc_model* model);
+const char* scvx_rtc_model_log(const scvx_rtc_model* model);
+int scvx_rtc_model_destroy(scvx_rtc_model* model);
+
+/* as scvx_foh_batched / scvx_integrate_nonlinear_batched; params: n_params <= SCVX_MAX_MODEL_PARAMS
+ * doubles (host memory, copied into the launch), p[i] = 0 beyond n_params */
+int scvx_rtc_foh_batched(const scvx_rtc_model* model, const double* params, int n_params, int K, int N,
+                         const double* X, const double* U, const double* sigma, int nsub, double* out,
+                         void* stream);
+int scvx_rtc_integrate_nonlinear_batched(const scvx_rtc_model* model, const double* params, int n_params,
+                                         int K, int N, const double* X, const double* U, const double* sigma,
+                                         int nsub, int piecewise, double* Xout, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Batched trust-region subproblem (one per agent), the convex solve the reference hands to

@@ -137,10 +137,11 @@ def test_library_exports_every_header_symbol():
     t = _lib.QPTemplate()
     t.K = 100
     assert L.scvx_qp_solve_batched(ctypes.byref(t), 1, *([None] * 17), None, 0, None) == -2
-    assert L.scvx_version() >= 2   # v2: w_nu / w_prox template fields, the nu output
+    assert L.scvx_version() >= 3   # v2: w_nu / w_prox template fields, the nu output; v3: scvx_rtc_*
 
 
 def test_first_order_hold_rejects_models_without_device_dynamics():
+    """A model that neither names built-in device dynamics nor has traceable f/A/B (scvx_hip.rtc)."""
     from SCvx.discretization.first_order_hold import FirstOrderHold
 
     class Custom:
