@@ -122,7 +122,12 @@ class ADMMCoordinator:
                     o = batch.solve(disc[s_], Xr[s_].clone(), Ur[s_].clone(), sig[s_], tr[s_], x_init[s_], x_final[s_],
                                     nbr_pos=pos, nbr_Y=Y[s_], nbr_Lam=Lam[s_])
                     bad[i] = o["status"][0] >= 2
-                    X[i], U[i] = o["X"][0], o["U"][0]
+                    # a failed agent keeps its previous (finite) iterate, so the agents after it in this
+                    # round never see a non-finite X[i]; the round then raises on the first failed agent,
+                    # as the reference aborts at the failing solve (cvxpy raises) -- without a host sync
+                    # per agent
+                    X[i] = torch.where(bad[i], X[i], o["X"][0])
+                    U[i] = torch.where(bad[i], U[i], o["U"][0])
                     outs.append({k: v.clone() for k, v in o.items()})
                 out = {k: torch.cat([o[k] for o in outs]) for k in outs[0]}
             if bool(bad.any()):                                       # one host read per round

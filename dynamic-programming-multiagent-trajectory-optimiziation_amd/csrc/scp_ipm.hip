@@ -51,7 +51,8 @@ struct SCPArgs {
 struct SCPLay {
     int RH, NS, Q, RL, ROWS, stride;
     int o_rows, o_q, o_P, o_At, o_Bt, o_ct, o_z, o_sig, o_s, o_lam, o_wl, o_sw, o_lt, o_H, o_f, o_rd, o_rc, o_rsig,
-        o_t, o_rho, o_rhs, o_dz, o_dsig, o_ds, o_dl, o_dsa, o_dla, o_y, o_yp, o_rp, o_K, o_Pr, o_pv, o_kv, o_LD, o_nh;
+        o_t, o_rho, o_rhs, o_dz, o_dsig, o_ds, o_dl, o_dsa, o_dla, o_y, o_yp, o_rp, o_K, o_Pr, o_pv, o_kv, o_LD, o_nh,
+        o_zb, o_sgb;
 };
 
 // augmented game states: u~_k = u_{k-1} (m), th~_k = th_{k-1} (1 when the model has a heading)
@@ -108,6 +109,8 @@ __host__ __device__ inline SCPLay scp_layout(const scvx_scp_template& T) {
     L.o_kv = take(NUA);
     L.o_LD = take(NUA * NUA);
     L.o_nh = take(1);
+    L.o_zb = take(NZ);       // best iterate (z, soft slacks) once the reduced tolerances hold
+    L.o_sgb = take(L.NS);
     L.stride = (o + 7) & ~7;
     if (L.stride < 64) L.stride = 64;  // the junk block after the K node blocks holds one slot per lane
     return L;
@@ -948,6 +951,8 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
     // direction broke down (Riccati overflow in the end-game), relaxed x0.01 after every taken step
     double regv = T.reg;
     double pres_best = INFINITY, dres_best = INFINITY;
+    double score_best = INFINITY;  // max(pres/pscale, dres/dscale, gap/max(1,|pobj|)) of the snapshot (o_zb / o_sgb)
+    bool restore = false;
 #ifdef SCP_TRACE
     long long tr_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     long long tr_last = __builtin_amdgcn_s_memtime();
@@ -1060,12 +1065,26 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
         // insufficient progress (ECOS's end-game exit): once the reduced tolerances hold, a residual
         // that jumps 100x above its best (the Newton systems' accuracy floor, barrier ratios ~1e16) ends
         // the solve as optimal_inaccurate instead of letting the iterate drift away
+        // ... on the best iterate seen since they first held (ECOS restores its best iterate there)
         if (near_ok && (pres > fmax(100.0 * pres_best, T.tol * pscale) || dres > fmax(100.0 * dres_best, T.tol * dscale))) {
             status = 1;
+            restore = score_best < INFINITY;
             break;
         }
         pres_best = fmin(pres_best, pres);
         dres_best = fmin(dres_best, dres);
+        {
+            const double score = fmax(fmax(pres / pscale, dres / dscale), gap / fmax(1.0, fabs(pobj)));
+            if (near_ok && score < score_best) {  // snapshot (uniform branch: the scores are wave reductions)
+                score_best = score;
+                for (int t = lane; t < K; t += WAVE) {
+                    double* B = nb(t);
+                    #pragma unroll
+                    for (int i = 0; i < NZ; ++i) B[Ly.o_zb + i] = B[Ly.o_z + i];
+                    for (int r = 0; r < NS; ++r) B[Ly.o_sgb + r] = B[Ly.o_sig + r];
+                }
+            }
+        }
         const double mu = gap / deg;
         if (lane < NX) sMisc[lane] = nb(0)[Ly.o_z + lane] - xinit[lane];  // r_init
         // ---- scaling and node Hessians
@@ -1352,6 +1371,15 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
 #endif
 
     if (status == 1 && it == T.max_iter && !near_ok) status = 2;   // cap reached far from optimal
+    if (restore) {
+        for (int t = lane; t < K; t += WAVE) {
+            double* B = nb(t);
+            #pragma unroll
+            for (int i = 0; i < NZ; ++i) B[Ly.o_z + i] = B[Ly.o_zb + i];
+            for (int r = 0; r < NS; ++r) B[Ly.o_sig + r] = B[Ly.o_sgb + r];
+        }
+        __syncthreads();
+    }
     // ------------------------------------------------------------------ outputs
     double sigv = sfix ? sref : nb(0)[Ly.o_z + SIG];
     double numaxl = 0.0, softl = 0.0, admml = 0.0;

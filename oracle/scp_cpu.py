@@ -314,6 +314,8 @@ class SCPSolver:
         pscale, dscale = 1.0 + hmax, 1.0 + qmax
         status, it, near_ok = "max_iter", 0, False
         pres_best = dres_best = np.inf
+        score_best, snap = np.inf, None   # best iterate once the reduced tolerances hold (kernel: o_zb / o_sgb)
+        self.restored = False
         self.trace = []
         self._regv = self.reg     # kernel: regv (x100 retry after a breakdown, x0.01 after a step)
         for it in range(self.max_iter):
@@ -357,11 +359,18 @@ class SCPSolver:
             near_ok = (pres < max(1e-4, self.tol) * pscale and dres < max(1e-4, self.tol) * dscale
                        and gap < max(5e-5, self.tol) * max(1.0, abs(pobj)))   # ECOS reduced tolerances
             # insufficient progress (kernel: pres_best / dres_best): a residual jumping 100x above its best
+            # (ECOS returns its best iterate there: restore the snapshot below)
             if near_ok and (pres > max(100.0 * pres_best, self.tol * pscale)
                             or dres > max(100.0 * dres_best, self.tol * dscale)):
                 status = "inaccurate"
+                if snap is not None:
+                    z, sig = snap[0].copy(), [x.copy() for x in snap[1]]
+                    self.restored = True
                 break
             pres_best, dres_best = min(pres_best, pres), min(dres_best, dres)
+            score = max(pres / pscale, dres / dscale, gap / max(1.0, abs(pobj)))
+            if near_ok and score < score_best:
+                score_best, snap = score, (z.copy(), [x.copy() for x in sig])
             # scaling
             Wn = [self._nt(nd, s[k], lam[k]) for k, nd in enumerate(nodes)]
             lt = [self._Wmul(nd, Wn[k], lam[k], 0) for k, nd in enumerate(nodes)]   # lambda~ = W lam

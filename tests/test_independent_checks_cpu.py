@@ -150,3 +150,20 @@ def test_twin_virtual_control_matches_dense_oracle(tr0, w_nu, w_prox):
         # strong convexity in U (Hessian 2I): ||U - U*||^2 <= gap, the stopping rule's 1e-10 x objective
         assert np.abs(cpu["U"][a][:-1] - Ud[:-1]).max() < max(1e-6, 3.0 * np.sqrt(1e-10 * ref))
         assert max(qd.constraint_violation(prob, cpu["X"][a], cpu["U"][a], nu=cpu["nu"][a]).values()) < 1e-8
+
+
+@pytest.mark.parametrize("tr", [5.0, 1.0])
+def test_twin_end_game_exit_returns_best_iterate(tr):
+    """ECOS's insufficient-progress exit (oracle/scp_cpu.py, csrc/scp_ipm.hip): at tol 1e-13 the LP's
+    Newton systems hit their accuracy floor, a residual jumps 100x above its best and the solve ends as
+    optimal_inaccurate on the BEST iterate seen since the reduced tolerances held (restored), whose value
+    HiGHS confirms to 1e-8."""
+    from oracle import scp_problems as spp
+    p = spp.scp_instance("unicycle", K=30, tr=tr)
+    sol = scp_cpu.SCPSolver(p, tol=1e-13, max_iter=100)
+    o = sol.solve()
+    assert o["status"] == "inaccurate" and sol.restored
+    v = highs_value(p)
+    obj = sd.scp_objective(p, o["X"], o["U"], o["nu"], float(o["sigma"]))
+    assert abs(obj - v) <= 1e-8 * max(1.0, abs(v)), (obj, v)
+    assert sd.scp_violation(p, o["X"], o["U"], o["nu"], float(o["sigma"])) < 1e-7

@@ -135,3 +135,20 @@ def test_scproblem_lp_value_matches_highs(cuda, K):
         obj = sd.scp_objective(p, g["X"][a], g["U"][a], g["nu"][a], float(g["sigma"][a]))
         assert abs(obj - v) <= 1e-7 * max(1.0, abs(v)), (a, obj, v)
         assert sd.scp_violation(p, g["X"][a], g["U"][a], g["nu"][a], float(g["sigma"][a])) < 1e-7
+
+
+@pytest.mark.parametrize("tr", [5.0, 1.0])
+def test_end_game_exit_returns_best_iterate(cuda, tr):
+    """tol 1e-13 drives the kernel into ECOS's insufficient-progress exit (status 1): the outputs are the
+    best iterate since the reduced tolerances held (as the CPU twin, tests/test_independent_checks_cpu.py),
+    and their value is HiGHS's to 1e-8."""
+    import torch
+    from oracle import scp_dense as sd, scp_problems as spp
+    from test_independent_checks_cpu import highs_value
+    p = spp.scp_instance("unicycle", K=30, tr=tr)
+    g = solve_gpu([p], torch, cuda, tol=1e-13)
+    assert g["status"][0] == 1, g["status"]
+    v = highs_value(p)
+    obj = sd.scp_objective(p, g["X"][0], g["U"][0], g["nu"][0], float(g["sigma"][0]))
+    assert abs(obj - v) <= 1e-8 * max(1.0, abs(v)), (obj, v)
+    assert sd.scp_violation(p, g["X"][0], g["U"][0], g["nu"][0], float(g["sigma"][0])) < 1e-7
