@@ -638,7 +638,9 @@ def main():
             "config": {"workload": workload, "agents_per_gpu": N, "K": K, "parallelism": f"agents sharded x{world}"},
             "roofline": {"bound": "fp64_valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                         "traffic_unit": "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE)", "traffic_source": traffic_src,
+                         "traffic_unit": "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE; warm-started launches as in the "
+                                         "timed region: the PMC command's cold first launch excluded)",
+                         "traffic_source": traffic_src,
                          "kernel": "qp_ipm_kernel", "kernel_ms": qp_ms,
                          "algorithmic_flops_per_launch": qp_flops, "algorithmic_bytes_per_launch": qp_bytes,
                          "hbm_achieved_gbs": qp_gbs, "hbm_frac": qp_gbs / HBM_PEAK_GBS,

@@ -1766,17 +1766,30 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     // iteration cap is reported `optimal_inaccurate` only if it meets the reduced tolerances below,
     // otherwise `solver_error` (ECOS / Clarabel report a cap far from optimal as a failure too)
     for (it = 0; status != SCVX_STATUS_NUMERICAL; ++it) {
+        // The disc row is consumed in two register chunks (A | S z, then B | C), so the whole row (DSTR
+        // doubles) is never live next to the iterate: that peak made the C3 class spill.  The second
+        // chunk's loads are issued once the first chunk is dead (one extra round trip per iteration).
         fresh();
-        double dt[C::DSTR], Cpr[NX * NU];
+        double Cpr[NX * NU], dA[NX * NX], dSz[2 * NX];
         issue_state();
-        ldn(dt, C::C_DT, C::DSTR);
+        ldn(dA, C::C_DT, NX * NX);
+        ldn(dSz, C::C_DT + NX * NX + 2 * NX * NU, 2 * NX);
         load_cp(Cpr);
         hold_state();
-        hold(dt, C::DSTR);
-        double rp[NX];
-        dyn_residual(z, dt, rp);
+        hold(dA, NX * NX);
+        hold(dSz, 2 * NX);
+        double zn[NZ];
 #pragma unroll
-        for (int i = 0; i < NV; ++i) rp[i] -= vact ? vn[i] : 0.0;   // + nu_t in the dynamics
+        for (int i = 0; i < NZ; ++i) zn[i] = __shfl_down(z[i], 1, WAVE);
+        // rp_t = x_{t+1} - A x_t - B u_t - C u_{t+1} - S sigma - z (lane t < K-1), the dyn_residual order
+        double rp[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            double v = zn[i] - fma(dSz[i], sig, dSz[NX + i]);
+#pragma unroll
+            for (int k = 0; k < NX; ++k) v -= dA[k * NX + i] * z[k];
+            rp[i] = v;
+        }
         // dual residual rd = Pz + q + A'y + G'lam (z and group parts)
         double rd[NZ], rda[NGA];
         // residual norms and Clarabel's normalisation of them (the solver dist_scvx_3d.py:110 calls):
@@ -1784,12 +1797,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         // (inf-norms; b = every constant of the equality and inequality rows, x = primal variables,
         // s = slacks, z = every multiplier: rows, cone, dynamics, boundary conditions)
         double pres = 0.0, dres = 0.0, gap = 0.0, nb = 0.0, nxv = 0.0, nsl = 0.0, nzd = 0.0, pobj = 0.0;
-#pragma unroll
-        for (int i = 0; i < NX; ++i) pres = fmax(pres, fabs(rp[i]));
         if (t < K - 1) {
 #pragma unroll
-            for (int i = 0; i < NX; ++i)
-                nb = fmax(nb, fabs(fma(dt[NX * NX + 2 * NX * NU + i], sig, dt[NX * NX + 2 * NX * NU + NX + i])));
+            for (int i = 0; i < NX; ++i) nb = fmax(nb, fabs(fma(dSz[i], sig, dSz[NX + i])));
         }
         if (act) {
 #pragma unroll
@@ -1825,6 +1835,59 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         for (int j = 0; j < NU; ++j) rd[NX + j] = 2.0 * wu * z[NX + j];
 #pragma unroll
         for (int g = 0; g < NGA; ++g) rda[g] = gweight(g);
+        {
+            // dynamics and boundary multipliers first (y_{t-1} from lane t-1), so that the disc row and
+            // C_{t-1} are dead before the row loop (register pressure of the residual phase)
+            double ym[NX];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) ym[i] = __shfl_up(y[i], 1, WAVE);
+            if (act) {
+                if (t == 0) {
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) rd[i] += lds[V_YI + i];
+                }
+                if (t == K - 1 && fin) {
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) rd[i] += lds[V_YF + i];
+                }
+                if (t >= 1) {
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) rd[i] += ym[i];
+#pragma unroll
+                    for (int j = 0; j < NU; ++j)
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) rd[NX + j] -= Cpr[j * NX + i] * ym[i];
+                }
+                if (t < K - 1) {
+#pragma unroll
+                    for (int k = 0; k < NX; ++k)
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) rd[k] -= dA[k * NX + i] * y[i];
+                }
+            }
+        }
+        {   // second chunk: B | C
+            double dBC[2 * NX * NU];
+            ldn(dBC, C::C_DT + NX * NX, 2 * NX * NU);
+            hold(dBC, 2 * NX * NU);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                double v = rp[i];
+#pragma unroll
+                for (int j = 0; j < NU; ++j) v -= dBC[j * NX + i] * z[NX + j] + dBC[NX * NU + j * NX + i] * zn[NX + j];
+                rp[i] = (t < K - 1) ? v : 0.0;
+            }
+            if (act && t < K - 1) {
+#pragma unroll
+                for (int j = 0; j < NU; ++j)
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) rd[NX + j] -= dBC[j * NX + i] * y[i];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NV; ++i) rp[i] -= vact ? vn[i] : 0.0;   // + nu_t in the dynamics
+#pragma unroll
+        for (int i = 0; i < NX; ++i) pres = fmax(pres, fabs(rp[i]));
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
             double gz, h;
@@ -1856,37 +1919,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             for (int j = 0; j < NQ; ++j) rcq[j] = 0.0;
         }
         {
-            // dynamics multipliers: y_{t-1} from lane t-1
-            double ym[NX];
-#pragma unroll
-            for (int i = 0; i < NX; ++i) ym[i] = __shfl_up(y[i], 1, WAVE);
             if (act) {
-                if (t == 0) {
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) rd[i] += lds[V_YI + i];
-                }
-                if (t == K - 1 && fin) {
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) rd[i] += lds[V_YF + i];
-                }
-                if (t >= 1) {
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) rd[i] += ym[i];
-#pragma unroll
-                    for (int j = 0; j < NU; ++j)
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) rd[NX + j] -= Cpr[j * NX + i] * ym[i];
-                }
-                if (t < K - 1) {
-#pragma unroll
-                    for (int k = 0; k < NX; ++k)
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) rd[k] -= dt[k * NX + i] * y[i];
-#pragma unroll
-                    for (int j = 0; j < NU; ++j)
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) rd[NX + j] -= dt[NX * NX + j * NX + i] * y[i];
-                }
                 if (fixed_u) {
 #pragma unroll
                     for (int j = 0; j < NU; ++j) rd[NX + j] = 0.0;
@@ -1954,6 +1987,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
         dres_best = fmin(dres_best, dres);
         pres_best = fmin(pres_best, pres);
+        // diagnostics trace, residual part (written here so these values die before the direction phases)
+        if (a.trace && agent == a.trace_agent && lane == 0 && it < a.trace_cap) {
+            double* tr_ = a.trace + 8 * it;
+            tr_[0] = pres; tr_[1] = dres; tr_[2] = gap; tr_[3] = pobj * osc; tr_[7] = mu;
+        }
         // SOC Nesterov-Todd scaling (hyperbolic-rotation form, W lam = W^-1 s)
         double Wi2uu[NU * NU];
 #pragma unroll
@@ -2246,7 +2284,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         const double aa = fmin(1.0, max_step(false, quad, probe));
         const double gap_a = wave_sum(fma(aa, fma(aa, quad[2], quad[1]), quad[0]));
         const double mu_a = gap_a / deg;
-        const double sgm = mu > 0 ? pow(fmax(mu_a, 0.0) / mu, 3.0) : 0.0;
+        // (the cube as products: pow() would keep its polynomial constants live across the IPM loop)
+        const double sgr = mu > 0 ? fmax(mu_a, 0.0) / mu : 0.0;
+        const double sgm = sgr * sgr * sgr;
         // ---- corrector
         sgmu = sgm * mu;
         if (soc) {
@@ -2285,7 +2325,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
         if (a.trace && agent == a.trace_agent && lane == 0 && it < a.trace_cap) {
             double* tr_ = a.trace + 8 * it;
-            tr_[0] = pres; tr_[1] = dres; tr_[2] = gap; tr_[3] = pobj * osc; tr_[4] = aa; tr_[5] = al; tr_[6] = sgm; tr_[7] = mu;
+            tr_[4] = aa; tr_[5] = al; tr_[6] = sgm;
         }
         // ---- update
 #pragma unroll

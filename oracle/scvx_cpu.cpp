@@ -1182,7 +1182,8 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out, const double*
                     for (int j = 0; j <= m; ++j) gap_a += (N.ssoc[j] + aa * dsq[t][j]) * (N.lsoc[j] + aa * dlq[t][j]);
             }
             double mu_a = gap_a / std::max(deg, 1);
-            double sig = std::pow(std::max(mu_a, 0.0) / mu, 3.0);
+            const double sgr = std::max(mu_a, 0.0) / mu;   // the kernel's cube (products, not pow)
+            double sig = sgr * sgr * sgr;
             // corrector
             for (int t = 0; t < K; ++t) {
                 Node& N = ag.nd[t];

@@ -5,8 +5,11 @@ counts half the bytes of wide coalesced reads on gfx950 -> x2; WRITE_SIZE (KiB) 
 counters (SQ_WAVE_CYCLES, SQ_WAIT_*, SQ_ACTIVE_INST_*) count quad-cycles (x4 = shader cycles); the
 SQ_INSTS_* counters count wave-instructions.
 
-usage: python tools/pmc_summary.py <gpurun_out/pmc_TAG> <out.json> [kernel-substring]
-       (reads every <gpurun_out/pmc_TAG>_*/run_counter_collection.csv)"""
+usage: python tools/pmc_summary.py <gpurun_out/pmc_TAG> <out.json> [kernel-substring] [skip]
+       (reads every <gpurun_out/pmc_TAG>_*/run_counter_collection.csv)
+skip: drop each pass's first `skip` dispatches of the kernel from the per-launch averages (the PMC
+command's warmup launch is a cold QP start; the bench's timed launches are warm-started, so skip=1
+gives the timed region's per-launch figures); the all-launch traffic is kept as traffic_bytes_all."""
 import collections
 import csv
 import glob
@@ -14,26 +17,36 @@ import json
 import sys
 
 
-def collect(prefix, kernel):
+def collect(prefix, kernel, skip=0):
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     names = {}
     for f in sorted(glob.glob(prefix + "_*/run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
             if kernel not in r["Kernel_Name"]:
                 continue
-            key = (f, r["Dispatch_Id"])
+            key = (f, int(r["Dispatch_Id"]))
             per[r["Counter_Name"]][key] += float(r["Counter_Value"])
             names[r["Counter_Name"]] = r["Kernel_Name"]
-    return {c: sum(v.values()) / len(v) for c, v in per.items()}, names
+    out = {}
+    for c, v in per.items():
+        keep = []
+        for f in sorted({k[0] for k in v}):
+            keep += sorted((k for k in v if k[0] == f), key=lambda k: k[1])[skip:]
+        out[c] = sum(v[k] for k in keep) / max(len(keep), 1)
+    return out, names
 
 
-def main(prefix, out, kernel="qp_ipm_kernel<scvx::QPCfg<6, 3, 2, 8, 0, 0>"):
-    c, names = collect(prefix, kernel)
+def main(prefix, out, kernel="qp_ipm_kernel<scvx::QPCfg<6, 3, 2, 8, 0, 0>", skip="0"):
+    skip = int(skip)
+    c, names = collect(prefix, kernel, skip)
     res = {"kernel": next(iter(names.values()), kernel).split("(")[0].replace("void ", ""),
-           "source": prefix + "_*", "raw_per_launch": c}
+           "source": prefix + "_*", "skipped_first_dispatches_per_pass": skip, "raw_per_launch": c}
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         fb, wb = 2.0 * 1024 * c["FETCH_SIZE"], 1024 * c["WRITE_SIZE"]
         res.update(fetch_bytes_corrected=fb, write_bytes=wb, traffic_bytes=fb + wb)
+        if skip:
+            ca, _ = collect(prefix, kernel, 0)
+            res["traffic_bytes_all"] = 2.0 * 1024 * ca["FETCH_SIZE"] + 1024 * ca["WRITE_SIZE"]
     w = c.get("SQ_WAVES")
     if w and "SQ_WAVE_CYCLES" in c:
         cyc = 4 * c["SQ_WAVE_CYCLES"] / w
@@ -60,4 +73,4 @@ def main(prefix, out, kernel="qp_ipm_kernel<scvx::QPCfg<6, 3, 2, 8, 0, 0>"):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])
