@@ -214,6 +214,79 @@ struct Soc {
     }
 };
 
+// ---- hot row loops of the node phases, as functions with __restrict__ operands: inlined, the
+// parameters' noalias becomes scoped alias metadata, so the compiler may move the next row's loads
+// above this row's stores (the layout offsets are runtime values and would otherwise alias) and
+// unroll with the loads of several rows in flight.  Arithmetic and accumulation order are unchanged.
+// residual, hard rows: rd += a_r l_r, rc_r = a_r z + s_r - h_r
+template <int NZ>
+__device__ __forceinline__ void rows_residual(const double* __restrict__ rows, const double* __restrict__ lam,
+                                              const double* __restrict__ sl, double* __restrict__ rc, int nh,
+                                              const double (&z)[NZ], double (&rd)[NZ], double& presl, double& gapl) {
+    constexpr int RS = NZ + 1;
+    #pragma unroll 2
+    for (int r = 0; r < nh; ++r) {
+        const double* ar = rows + r * RS;
+        const double l = lam[r], s = sl[r];
+        #pragma unroll
+        for (int i = 0; i < NZ; ++i) rd[i] += ar[i] * l;
+        double v = 0.0;
+        #pragma unroll
+        for (int i = 0; i < NZ; ++i) v += ar[i] * z[i];
+        const double rcv = v + s - ar[NZ];
+        rc[r] = rcv;
+        presl = fmax(presl, fabs(rcv));
+        gapl += s * l;
+    }
+}
+// direction, LP rows: rho = rcomp / lt, t = rho / wl + rc / wl^2 (stored); f += a_r t_r on hard rows
+template <int NZ>
+__device__ __forceinline__ void rows_direction(const double* __restrict__ rows, const double* __restrict__ lt_,
+                                               const double* __restrict__ wl_, const double* __restrict__ dsa,
+                                               const double* __restrict__ dla, const double* __restrict__ rc,
+                                               double* __restrict__ rho_, double* __restrict__ t_, int r0, int r1,
+                                               bool hard, bool corr, double sgmu, double (&f)[NZ]) {
+    constexpr int RS = NZ + 1;
+    #pragma unroll 2
+    for (int r = r0; r < r1; ++r) {
+        const double lt = lt_[r], wl = wl_[r];
+        double rcv = -lt * lt;
+        if (corr) rcv += -(dsa[r] * dla[r]) + sgmu;
+        const double rho = rcv / lt;
+        const double tv = rho / wl + rc[r] / (wl * wl);
+        rho_[r] = rho;
+        t_[r] = tv;
+        if (hard) {
+            const double* ar = rows + r * RS;
+            #pragma unroll
+            for (int i = 0; i < NZ; ++i) f[i] += ar[i] * tv;
+        }
+    }
+}
+// step recovery, hard rows: ds = -rc - a_r dz, dl = rho / wl + (rc + a_r dz) / wl^2, ratio test
+template <int NZ>
+__device__ __forceinline__ void rows_step(const double* __restrict__ rows, const double* __restrict__ wl_,
+                                          const double* __restrict__ rc_, const double* __restrict__ rho_,
+                                          const double* __restrict__ sl, const double* __restrict__ lam,
+                                          double* __restrict__ ds_, double* __restrict__ dl_, int nh,
+                                          const double (&dz)[NZ], double& amax) {
+    constexpr int RS = NZ + 1;
+    #pragma unroll 2
+    for (int r = 0; r < nh; ++r) {
+        const double* ar = rows + r * RS;
+        double gdz = 0.0;
+        #pragma unroll
+        for (int i = 0; i < NZ; ++i) gdz += ar[i] * dz[i];
+        const double wl = wl_[r], rc = rc_[r];
+        const double ds = -rc - gdz;
+        const double dl = rho_[r] / wl + (rc + gdz) / (wl * wl);
+        ds_[r] = ds;
+        dl_[r] = dl;
+        if (ds < 0.0) amax = fmin(amax, -sl[r] / ds);
+        if (dl < 0.0) amax = fmin(amax, -lam[r] / dl);
+    }
+}
+
 template <int NX, int NU, int NE>
 __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restrict__ ws_all, const double* __restrict__ disc_all) {
     // workspace and disc come in as kernel pointer arguments (known global address space): read out
@@ -977,16 +1050,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
                 pobjl += z[i] * (B[Ly.o_q + i] + 0.5 * (v - B[Ly.o_q + i]));
                 rd[i] = v;
             }
-            for (int r = 0; r < nh; ++r) {
-                const double* ar = rowp(B, r);
-                const double l = B[Ly.o_lam + r], s = B[Ly.o_s + r];
-                #pragma unroll
-                for (int i = 0; i < NZ; ++i) rd[i] += ar[i] * l;
-                const double rc = dot(ar, z) + s - ar[NZ];
-                B[Ly.o_rc + r] = rc;
-                presl = fmax(presl, fabs(rc));
-                gapl += s * l;
-            }
+            rows_residual<NZ>(B + Ly.o_rows, B + Ly.o_lam, B + Ly.o_s, B + Ly.o_rc, nh, z, rd, presl, gapl);
             for (int r = 0; r < NS; ++r) {
                 const double* ar = rowp(B, RH + r);
                 const double l1 = B[Ly.o_lam + RH + 2 * r], l2 = B[Ly.o_lam + RH + 2 * r + 1];
@@ -1175,21 +1239,10 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
                 #pragma unroll
                 for (int i = 0; i < NZ; ++i) f[i] = B[Ly.o_rd + i];
                 // LP rows: lt = sqrt(s l), wl = sqrt(s/l); rcomp = -lt^2 [- (ds_a/wl)(wl dl_a) + sg mu]
-                for (int r = 0; r < NLP; ++r) {
-                    if (r >= nh && r < RH) continue;
-                    const double lt = B[Ly.o_lt + r], wl = B[Ly.o_wl + r];
-                    double rcv = -lt * lt;
-                    if (corr) rcv += -(B[Ly.o_dsa + r] * B[Ly.o_dla + r]) + sgmu;
-                    const double rho = rcv / lt;
-                    const double tv = rho / wl + B[Ly.o_rc + r] / (wl * wl);
-                    B[Ly.o_rho + r] = rho;
-                    B[Ly.o_t + r] = tv;
-                    if (r < nh) {
-                        const double* ar = rowp(B, r);
-                        #pragma unroll
-                        for (int i = 0; i < NZ; ++i) f[i] += ar[i] * tv;
-                    }
-                }
+                rows_direction<NZ>(B + Ly.o_rows, B + Ly.o_lt, B + Ly.o_wl, B + Ly.o_dsa, B + Ly.o_dla, B + Ly.o_rc,
+                                   B + Ly.o_rho, B + Ly.o_t, 0, nh, true, corr, sgmu, f);
+                rows_direction<NZ>(B + Ly.o_rows, B + Ly.o_lt, B + Ly.o_wl, B + Ly.o_dsa, B + Ly.o_dla, B + Ly.o_rc,
+                                   B + Ly.o_rho, B + Ly.o_t, RH, NLP, false, corr, sgmu, f);
                 for (int r = 0; r < NS; ++r) {
                     const double* ar = rowp(B, RH + r);
                     const double wl1 = B[Ly.o_wl + RH + 2 * r], wl2 = B[Ly.o_wl + RH + 2 * r + 1];
@@ -1255,7 +1308,8 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
                     if (ds < 0.0) amax = fmin(amax, -B[Ly.o_s + r] / ds);
                     if (dl < 0.0) amax = fmin(amax, -B[Ly.o_lam + r] / dl);
                 };
-                for (int r = 0; r < nh; ++r) lpstep(r, dot(rowp(B, r), dz));
+                rows_step<NZ>(B + Ly.o_rows, B + Ly.o_wl, B + Ly.o_rc, B + Ly.o_rho, B + Ly.o_s, B + Ly.o_lam, B + Ly.o_ds,
+                              B + Ly.o_dl, nh, dz, amax);
                 for (int r = 0; r < NS; ++r) {
                     const double* ar = rowp(B, RH + r);
                     const double wl1 = B[Ly.o_wl + RH + 2 * r], wl2 = B[Ly.o_wl + RH + 2 * r + 1];
