@@ -484,6 +484,8 @@ def main():
     ap.add_argument("--tensor-update", action="store_true", help="c3: bookkeeping as tensor ops (not csrc/jacobi.hip)")
     ap.add_argument("--tie-rtol", type=float, default=1e-9,
                     help="c3 per-agent trust-region rule: relative margin of the cost-increase test (JacobiSCvx.tie_rtol)")
+    ap.add_argument("--warm-status", type=int, default=0, choices=(0, 1),
+                    help="JacobiSCvx.warm_max_status: warm-start agents whose last solve had status <= this")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -518,7 +520,7 @@ def main():
         spec = scvx_hip.QPSpec(model="di", K=K, box=BOX, obs=sc["obs"], w_obs=1e6, u_max=U_MAX, tol=args.tol,
                                max_iter=60)
         drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, tr_rule="per_agent", tie_rtol=args.tie_rtol,
-                         fused_update=not args.tensor_update)
+                         fused_update=not args.tensor_update, warm_max_status=args.warm_status)
         n_obs = N_OBS
     else:
         sc, w, cfg = make_coupled(args.config, world, rank, device)
@@ -528,7 +530,7 @@ def main():
         spec = scvx_hip.QPSpec(model=model, K=K, box=box, obs=cfg["obs"], w_obs=1e6, j_max=j_max, w_coll=1e4,
                                tol=args.tol, max_iter=60, **cfg["vc"])
         drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, coupling=CouplingSpec(R=cfg["R"]),
-                         tr_rule="global")
+                         tr_rule="global", warm_max_status=args.warm_status)
     it_state = [w["X"].clone(), w["U"].clone()]   # the current iterate (X, U), rebound every step
 
     def step(marks=None):

@@ -287,6 +287,37 @@ __device__ __forceinline__ void rows_step(const double* __restrict__ rows, const
     }
 }
 
+// LP-row scaling: wl = sqrt(s / l), lt = sqrt(s l) on rows [r0, r1)
+__device__ __forceinline__ void rows_scale(const double* __restrict__ sl, const double* __restrict__ lam,
+                                           double* __restrict__ wl, double* __restrict__ lt, int r0, int r1) {
+    #pragma unroll 4
+    for (int r = r0; r < r1; ++r) {
+        const double s = sl[r], l = lam[r];
+        wl[r] = sqrt(s / l);
+        lt[r] = sqrt(s * l);
+    }
+}
+// predictor complementarity sum_r (s + aa ds)(l + aa dl) on rows [r0, r1) (accumulated in row order)
+__device__ __forceinline__ void rows_mu(const double* __restrict__ sl, const double* __restrict__ lam,
+                                        const double* __restrict__ ds, const double* __restrict__ dl, int r0, int r1,
+                                        double aa, double& mual) {
+    #pragma unroll 4
+    for (int r = r0; r < r1; ++r) mual += (sl[r] + aa * ds[r]) * (lam[r] + aa * dl[r]);
+}
+// y[r] = x[r] on rows [0, n)
+__device__ __forceinline__ void rows_copy2(const double* __restrict__ x1, const double* __restrict__ x2,
+                                           double* __restrict__ y1, double* __restrict__ y2, int n) {
+    #pragma unroll 4
+    for (int r = 0; r < n; ++r) { y1[r] = x1[r]; y2[r] = x2[r]; }
+}
+// s += al ds, l += al dl on rows [r0, r1)
+__device__ __forceinline__ void rows_update(double* __restrict__ sl, double* __restrict__ lam,
+                                            const double* __restrict__ ds, const double* __restrict__ dl, int r0,
+                                            int r1, double al) {
+    #pragma unroll 4
+    for (int r = r0; r < r1; ++r) { sl[r] += al * ds[r]; lam[r] += al * dl[r]; }
+}
+
 template <int NX, int NU, int NE>
 __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restrict__ ws_all, const double* __restrict__ disc_all) {
     // workspace and disc come in as kernel pointer arguments (known global address space): read out
@@ -623,6 +654,9 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
     __syncthreads();
 
     auto soft_w = [&](int r) -> double { return r < T.n_obs ? w_obs : w_col; };
+    // the node cost Hessian P is identically zero for the plain SCProblem (an LP: no ADMM, no game
+    // terms); its loads are skipped then (uniform)
+    const bool hasP = T.n_nbr > 0 || NE > 0;
 
     // ------------------------------------------------------------------ stage packets
     // The Riccati sweeps are sequential over nodes, so every global load inside a stage is exposed
@@ -913,7 +947,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
         const int nh = (int)B[Ly.o_nh];
         double Hu[NZ * NZ], f[NZ];
         #pragma unroll
-        for (int e = 0; e < NZ * NZ; ++e) Hu[e] = B[Ly.o_P + e];
+        for (int e = 0; e < NZ * NZ; ++e) Hu[e] = hasP ? B[Ly.o_P + e] : 0.0;
         #pragma unroll
         for (int i = 0; i < NZ; ++i) f[i] = B[Ly.o_q + i];
         for (int r = 0; r < nh; ++r) {
@@ -1045,8 +1079,9 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             #pragma unroll
             for (int i = 0; i < NZ; ++i) {
                 double v = B[Ly.o_q + i];
-                #pragma unroll
-                for (int j = 0; j < NZ; ++j) v += B[Ly.o_P + i * NZ + j] * z[j];
+                if (hasP)
+                    #pragma unroll
+                    for (int j = 0; j < NZ; ++j) v += B[Ly.o_P + i * NZ + j] * z[j];
                 pobjl += z[i] * (B[Ly.o_q + i] + 0.5 * (v - B[Ly.o_q + i]));
                 rd[i] = v;
             }
@@ -1157,14 +1192,9 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             const int nh = (int)B[Ly.o_nh];
             double Hu[NZ * NZ];
             #pragma unroll
-            for (int e = 0; e < NZ * NZ; ++e) Hu[e] = B[Ly.o_P + e];
-            for (int r = 0; r < NLP; ++r) {
-                if (r >= nh && r < RH) continue;
-                const double s = B[Ly.o_s + r], l = B[Ly.o_lam + r];
-                const double wl = sqrt(s / l);
-                B[Ly.o_wl + r] = wl;
-                B[Ly.o_lt + r] = sqrt(s * l);
-            }
+            for (int e = 0; e < NZ * NZ; ++e) Hu[e] = hasP ? B[Ly.o_P + e] : 0.0;
+            rows_scale(B + Ly.o_s, B + Ly.o_lam, B + Ly.o_wl, B + Ly.o_lt, 0, nh);
+            rows_scale(B + Ly.o_s, B + Ly.o_lam, B + Ly.o_wl, B + Ly.o_lt, RH, NLP);
             for (int r = 0; r < nh; ++r) {
                 const double* ar = rowp(B, r);
                 const double d = B[Ly.o_lam + r] / B[Ly.o_s + r];
@@ -1353,17 +1383,11 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
         for (int t = lane; t < K; t += WAVE) {
             double* B = nb(t);
             const int nh = (int)B[Ly.o_nh];
-            for (int r = 0; r < RL; ++r) {
-                if (r >= nh && r < RH) continue;
-                const double ds = B[Ly.o_ds + r], dl = B[Ly.o_dl + r];
-                mual += (B[Ly.o_s + r] + aa * ds) * (B[Ly.o_lam + r] + aa * dl);
-            }
+            rows_mu(B + Ly.o_s, B + Ly.o_lam, B + Ly.o_ds, B + Ly.o_dl, 0, nh, aa, mual);
+            rows_mu(B + Ly.o_s, B + Ly.o_lam, B + Ly.o_ds, B + Ly.o_dl, RH, RL, aa, mual);
             // Mehrotra corrector terms in scaled coordinates: LP (ds_a / wl) * (wl dl_a) = ds_a dl_a;
             // SOC: keep ds_a, dl_a raw (scaled inside direction())
-            for (int r = 0; r < RL; ++r) {
-                B[Ly.o_dsa + r] = B[Ly.o_ds + r];
-                B[Ly.o_dla + r] = B[Ly.o_dl + r];
-            }
+            rows_copy2(B + Ly.o_ds, B + Ly.o_dl, B + Ly.o_dsa, B + Ly.o_dla, RL);
         }
         const double mu_a = wave_sum(mual) / deg;
         const double sg = (mu_a / mu) * (mu_a / mu) * (mu_a / mu);
@@ -1403,11 +1427,8 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             #pragma unroll
             for (int i = 0; i < NZ; ++i) B[Ly.o_z + i] += al * B[Ly.o_dz + i];
             for (int r = 0; r < NS; ++r) B[Ly.o_sig + r] += al * B[Ly.o_dsig + r];
-            for (int r = 0; r < RL; ++r) {
-                if (r >= nh && r < RH) continue;
-                B[Ly.o_s + r] += al * B[Ly.o_ds + r];
-                B[Ly.o_lam + r] += al * B[Ly.o_dl + r];
-            }
+            rows_update(B + Ly.o_s, B + Ly.o_lam, B + Ly.o_ds, B + Ly.o_dl, 0, nh, al);
+            rows_update(B + Ly.o_s, B + Ly.o_lam, B + Ly.o_ds, B + Ly.o_dl, RH, RL, al);
             if (t < K - 1)
                 #pragma unroll
                 for (int i = 0; i < NXA; ++i) B[Ly.o_y + i] += al * (B[Ly.o_yp + i] - B[Ly.o_y + i]);

@@ -76,12 +76,14 @@ class JacobiSCvx:
              optimal (QPSolver.solve(warm=...), include/scvx_hip.h): the next subproblem is the same agent's
              re-linearised at that solution.  The optimum and the stopping rule are unchanged; C3 needs
              ~2.4x fewer IPM iterations.  False: every solve starts cold (CVXOPT-style).
+    warm_max_status: the previous solve qualifies when its status is <= this (0: optimal only; 1: also
+             optimal_inaccurate, whose iterate meets the reduced tolerances).
     """
 
     def __init__(self, spec: QPSpec, x_init, x_final, sigma, tr0: float, coupling: Optional[CouplingSpec] = None,
                  tr_rule: str = "per_agent", group=None, nsub: Optional[int] = None, backend=None,
                  on_fail: str = "halve", tr_max: Optional[float] = None, fused_update: bool = True,
-                 tie_rtol: float = 1e-9, warm_start: bool = True):
+                 tie_rtol: float = 1e-9, warm_start: bool = True, warm_max_status: int = 0):
         import torch
         self.torch = torch
         self.backend = backend or HipBackend()
@@ -97,7 +99,8 @@ class JacobiSCvx:
         self.fused_update = fused_update
         self.tie_rtol = float(tie_rtol)
         self.warm_start = warm_start and spec.K >= 2 * MODEL_DIMS[spec.model][0]
-        self.warm = None   # (N,) int32 device: the previous solve of the agent was optimal
+        self.warm = None   # (N,) int32 device: the previous solve of the agent qualifies as a warm start
+        self.warm_max_status = int(warm_max_status)
         self.group = group
         self.nsub = nsub or DEFAULT_NSUB[spec.model]
         self.solver = self.backend.qp_solver(spec, self.N, self.device)
@@ -208,7 +211,7 @@ class JacobiSCvx:
         out = self.solver.solve(self.disc, self.sigma, X, U, self.x_init, self.x_final, self.tr, rows, count,
                                 warm=self.warm)
         if self.warm_start:
-            self.warm = (out["status"] == 0).to(torch.int32)
+            self.warm = (out["status"] <= self.warm_max_status).to(torch.int32)
         self._mark(marks, "qp")
         if self.coupling is not None and self.coupling.check:
             out = self._enforce_all_rows(X_all, X, U, out)
