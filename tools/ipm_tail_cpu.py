@@ -2,7 +2,9 @@
 through the CPU restatements (oracle/foh_ref.c + oracle/scvx_cpu.cpp, the kernel's twin), printing the
 IPM-iteration histogram of every step.  Used to try IPM algorithm changes on the CPU twin before they
 go into qp_ipm.hpp (the kernel time is the slowest agent's iteration count x the per-iteration latency).
-usage: python tools/ipm_tail_cpu.py [steps] [N] [threads]"""
+usage: python tools/ipm_tail_cpu.py [steps] [N] [threads]
+WARM=1: warm-start every agent from its previous solve (JacobiSCvx's default; the kernel's rule).
+DUMP=path.npz: save the last step's inputs and per-agent iteration counts (to replay a tail agent)."""
 import os
 import sys
 import time
@@ -27,10 +29,18 @@ tr = np.full(N, bench.TR0)
 prev = np.full(N, np.inf)
 tot = []
 tot_cost = []
+WARM = os.environ.get("WARM") == "1"
+wstate = np.zeros((N, qp_cpu.warm_doubles(tpl))) if WARM else None
+warm = np.zeros(N, np.int32)
 for s in range(steps):
     t0 = time.time()
     disc = np.stack([np.hstack([o.T for o in foh_oracle.foh("di", X[a].T, U[a].T, sc["sigma"][a])]) for a in range(N)])
-    o = qp_cpu.solve_batched(tpl, disc, sc["sigma"], X, U, sc["x_init"], sc["x_final"], tr, nthreads=threads)
+    w_in = wstate.copy() if (WARM and os.environ.get("DUMP")) else None
+    o = qp_cpu.solve_batched(tpl, disc, sc["sigma"], X, U, sc["x_init"], sc["x_final"], tr, nthreads=threads,
+                            warm=warm if WARM else None, wstate=wstate)
+    if os.environ.get("DUMP"):
+        np.savez(os.environ["DUMP"], disc=disc, X=X, U=U, tr=tr, iters=o["iters"], warm=warm,
+                 wstate=w_in if WARM else np.zeros(1), step=s)
     it, st = o["iters"] % 100, o["status"]
     gz = o["iters"] // 100
     cost = it + float(os.environ.get("GZ_COST", "0.25")) * gz
@@ -42,6 +52,7 @@ for s in range(steps):
     ok = (st != 2)[:, None, None]
     X, U = np.where(ok, o["X"], X), np.where(ok, o["U"], U)
     cost = (U[:, :-1] ** 2).sum(axis=(1, 2))
-    tr = tr * np.where(cost > prev, 0.5, 1.0) * np.where(st == 2, 0.5, 1.0)
+    tr = tr * np.where(cost > prev * (1 + 1e-9), 0.5, 1.0) * np.where(st == 2, 0.5, 1.0)
     prev = cost
+    warm = (st <= 0).astype(np.int32)
 print(f"sum of per-step max iterations: {sum(tot)} (mean {np.mean(tot):.2f}); mean max cost {np.mean(tot_cost):.2f}")
