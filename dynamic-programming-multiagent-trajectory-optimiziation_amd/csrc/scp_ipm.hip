@@ -346,8 +346,8 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
     const double* xfin = a.x_final + agent * NX;
     const bool fin = T.has_final != 0;
 
-    __shared__ double sP[NXA * NXA], sPv[NXA], sPA[NXA * NXA],
-        sPB[NXA * NUA], sQxx[NXA * NXA], sQux[NUA * NXA], sQuu[NUA * NUA], sK[NUA * NXA], sV[NXA], sQ[NZ],
+    __shared__ double sP[NXA * NXA], sPv[NXA], sPAB[NXA * (NXA + NUA)], sQxx[NXA * NXA], sQuxC[NUA * NXA],
+        sQuu[NUA * NUA], sKC[NUA * NXA], sV[NXA], sQ[NZ],
         sXi[2][NXA], sU[NUA], sMisc[32];
     // sMisc: 0..NX-1 r_init, 8..8+NX-1 y0+, 16.. scalars
     auto pinned = [&](int t, int i) -> bool {  // i: z index
@@ -660,35 +660,43 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
 
     // ------------------------------------------------------------------ stage packets
     // The Riccati sweeps are sequential over nodes, so every global load inside a stage is exposed
-    // latency.  Each sweep instead gathers the next stage's operands (a packet of segments of the node
-    // blocks) into registers at the top of the current stage and parks them in an LDS ring slot at its
-    // end; the stage itself reads only LDS.  Loads are unconditional (node clamped to [0, K-1], lanes
-    // past the packet re-read its first element into the slot tail) and the sweeps use LDS-only wave
-    // barriers, so nothing drains the prefetch.
-    constexpr int PK_F = NZ * NZ + NXA * NXA + NXA * NUA;                                   // factor
+    // latency.  Each sweep instead gathers the next stage's operands (a packet of node-block elements)
+    // into registers at the top of the current stage and parks them in an LDS ring slot at its end; the
+    // stage itself reads only LDS.  Each lane's packet elements are mapped to (node delta, node-block
+    // offset) once per sweep, so a stage's gather is PF loads at stage-invariant offsets.  Loads are
+    // unconditional (node clamped to [0, K-1], lanes past the packet re-read an element into the slot
+    // tail) and the sweeps use LDS-only wave barriers, so nothing drains the prefetch.
+    constexpr int NAB = NXA + NUA;
+    constexpr int PK_F = NZ * NZ + NXA * NAB;                                               // factor
     constexpr int PK_B = NXA * NXA + NXA + NZ + NXA * NXA + NXA * NUA + NUA * NUA + NUA * NXA;  // LQ backward
     constexpr int PK_W = NUA + NUA * NXA + NXA + NXA * NXA + NXA * NUA + NXA + NXA * NXA;   // LQ forward
     constexpr int PK_MAX = PK_F > PK_B ? (PK_F > PK_W ? PK_F : PK_W) : (PK_B > PK_W ? PK_B : PK_W);
     constexpr int PF = (PK_MAX + WAVE - 1) / WAVE;
     __shared__ double sRing[2][PF * WAVE];
+    __shared__ double sSink[WAVE];  // LDS stores of lanes without an output element
     double pf[PF];
-    // segments: {node offset (0 or +1), node-block offset, length}
-    auto gather = [&](int t, const int (&dn)[7], const int (&off)[7], const int (&len)[7], int nseg) {
+    // segments: {node offset (0 or +1), node-block offset, length} -> per-lane element map
+    auto seg_map = [&](const int (&dn)[7], const int (&off)[7], const int (&len)[7], int nseg, int (&fo)[PF],
+                       int (&fd)[PF]) {
         #pragma unroll
         for (int c = 0; c < PF; ++c) {
             const int e = lane + c * WAVE;
-            long long addr = 0;
-            int acc = 0;
+            int o = off[0], d = dn[0], acc = 0;
             #pragma unroll
             for (int sg = 0; sg < 7; ++sg) {
-                if (sg < nseg && e >= acc && e < acc + len[sg]) {
-                    int tn = t + dn[sg];
-                    tn = tn < 0 ? 0 : (tn > K - 1 ? K - 1 : tn);
-                    addr = (long long)tn * Ly.stride + off[sg] + (e - acc);
-                }
+                if (sg < nseg && e >= acc && e < acc + len[sg]) { o = off[sg] + (e - acc); d = dn[sg]; }
                 if (sg < nseg) acc += len[sg];
             }
-            pf[c] = ws[addr];
+            fo[c] = o;
+            fd[c] = d;
+        }
+    };
+    auto gather = [&](int t, const int (&fo)[PF], const int (&fd)[PF]) {
+        #pragma unroll
+        for (int c = 0; c < PF; ++c) {
+            int tn = t + fd[c];
+            tn = tn < 0 ? 0 : (tn > K - 1 ? K - 1 : tn);
+            pf[c] = ws[(long long)tn * Ly.stride + fo[c]];
         }
     };
     auto park = [&](int slot) {
@@ -697,72 +705,115 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
     };
 
     // ------------------------------------------------------------------ Riccati factor (uses o_H)
+    // Stage packet: H (NZ x NZ) | [At Bt] column-major (column j of [At Bt] is NXA contiguous doubles),
+    // so every product of the stage is a dot product of two contiguous LDS vectors.  Four straight-line
+    // phases per stage, each lane's operand offsets decoded once per sweep (the packet slot alternates,
+    // the offsets within it do not); no divergent branches:
+    //   1: PAB = P [At Bt]                       (column-major, NXA x NAB)
+    //   2: Qxx = H_xx + At'PA (upper triangle), Qux = H_ux + Bt'PA (column-major), Quu = H_uu + Bt'PB
+    //   3: Quu = L D L' in registers (every lane); K = -Quu^-1 Qux, lane c < NXA solves column c
+    //   4: P = Qxx + Qux'K (symmetric: the upper element for both halves)
+    // Every accumulation runs in the order of oracle/scp_cpu.py's restatement (and of the previous
+    // element-loop form of this sweep): sequential k, starting from the H element.
     auto factor = [&]() __attribute__((always_inline)) {
-        const int dn[7] = {0, 0, 0, 0, 0, 0, 0};
-        const int off[7] = {Ly.o_H, Ly.o_At, Ly.o_Bt, 0, 0, 0, 0};
-        const int len[7] = {NZ * NZ, NXA * NXA, NXA * NUA, 0, 0, 0, 0};
+        constexpr int R1 = (NXA * NAB + WAVE - 1) / WAVE;
+        constexpr int E2 = NXA * NXA + NXA * NUA + NUA * NUA, R2 = (E2 + WAVE - 1) / WAVE;
+        constexpr int R4 = (NXA * NXA + WAVE - 1) / WAVE;
+        int fo[PF], fd[PF];
+        #pragma unroll
+        for (int c = 0; c < PF; ++c) {
+            const int e = lane + c * WAVE;
+            fd[c] = 0;
+            if (e < NZ * NZ) {
+                fo[c] = Ly.o_H + e;
+            } else if (e < PK_F) {
+                const int c2 = e - NZ * NZ, j = c2 / NXA, k = c2 - j * NXA;
+                fo[c] = j < NXA ? Ly.o_At + k * NXA + j : Ly.o_Bt + k * NUA + (j - NXA);
+            } else {
+                fo[c] = Ly.o_H;
+            }
+        }
+        // phase 1: out PAB[o] (o = j NXA + i) = P row i . [At Bt] column j
+        int l1[R1], r1[R1];
+        double* o1[R1];
+        #pragma unroll
+        for (int r = 0; r < R1; ++r) {
+            const int o = lane + r * WAVE;
+            const bool ok = o < NXA * NAB;
+            const int oo = ok ? o : 0, j = oo / NXA, i = oo - j * NXA;
+            l1[r] = i * NXA;
+            r1[r] = NZ * NZ + j * NXA;
+            o1[r] = ok ? sPAB + oo : sSink + lane;
+        }
+        // phase 2: column a of [At Bt] . PAB column b, + H[hi][hj]; pin classes (0 state, 1 input, 2 nu)
+        int a2[R2], b2[R2], h2[R2], ci2[R2], cj2[R2], kd2[R2];
+        double* o2[R2];
+        #pragma unroll
+        for (int r = 0; r < R2; ++r) {
+            const int o = lane + r * WAVE;
+            int a = 0, b = 0, hi = 0, hj = 0, ci = 0, cj = 0, kd = 0;
+            double* out = sSink + lane;
+            if (o < NXA * NXA) {  // Qxx (p, q) = (min, max)
+                const int i = o / NXA, j = o - i * NXA, p = i < j ? i : j, q = i < j ? j : i;
+                a = p; b = q; hi = p; hj = q; out = sQxx + o;
+            } else if (o < NXA * NXA + NXA * NUA) {  // Qux column-major: element (i, j) at j NUA + i
+                const int o2_ = o - NXA * NXA, j = o2_ / NUA, i = o2_ - j * NUA;
+                a = NXA + i; b = j; hi = NXA + i; hj = j; ci = i < NU ? 1 : 2; kd = 1; out = sQuxC + o2_;
+            } else if (o < E2) {  // Quu (i, j)
+                const int o3 = o - NXA * NXA - NXA * NUA, i = o3 / NUA, j = o3 - i * NUA;
+                a = NXA + i; b = NXA + j; hi = NXA + i; hj = NXA + j;
+                ci = i < NU ? 1 : 2; cj = j < NU ? 1 : 2; kd = i == j ? 3 : 2; out = sQuu + o3;
+            }
+            a2[r] = NZ * NZ + a * NXA; b2[r] = b * NXA; h2[r] = hi * NZ + hj;
+            ci2[r] = ci; cj2[r] = cj; kd2[r] = kd; o2[r] = out;
+        }
+        const bool kl = lane < NXA;
+        const int kc = kl ? lane : 0;
         for (int e = lane; e < NXA * NXA; e += WAVE) sP[e] = 0.0;
-        gather(K - 1, dn, off, len, 3);
+        gather(K - 1, fo, fd);
         park(0);
         wsync();
         for (int t = K - 1; t >= 0; --t) {
             const int slot = (K - 1 - t) & 1;
-            gather(t - 1, dn, off, len, 3);
-            const double* sH = sRing[slot];
-            const double* sAt = sH + NZ * NZ;
-            const double* sBt = sAt + NXA * NXA;
+            gather(t - 1, fo, fd);
+            const double* pk = sRing[slot];
             const bool dyn = t < K - 1;
-            if (dyn) {
-                for (int e = lane; e < NXA * (NXA + NUA); e += WAVE) {
-                    const int i = e / (NXA + NUA), j = e % (NXA + NUA);
-                    double v = 0.0;
-                    if (j < NXA) {
-                        for (int k = 0; k < NXA; ++k) v += sP[i * NXA + k] * sAt[k * NXA + j];
-                        sPA[i * NXA + j] = v;
-                    } else {
-                        for (int k = 0; k < NXA; ++k) v += sP[i * NXA + k] * sBt[k * NUA + j - NXA];
-                        sPB[i * NUA + j - NXA] = v;
-                    }
-                }
-                wsync();
+            const bool pinU = (t == 0 && T.pin_u_first) || (t == K - 1 && T.pin_u_last);
+            const bool pinN = t == K - 1 || (fin && t == K - 2);
+            #pragma unroll
+            for (int r = 0; r < R1; ++r) {
+                double v = 0.0;
+                #pragma unroll
+                for (int k = 0; k < NXA; ++k) v += sP[l1[r] + k] * pk[r1[r] + k];
+                *o1[r] = v;
             }
-            for (int e = lane; e < NXA * NXA + NUA * NXA + NUA * NUA; e += WAVE) {
-                if (e < NXA * NXA) {
-                    const int i = e / NXA, j = e % NXA;
-                    double v = sH[i * NZ + j];
-                    if (dyn)
-                        for (int k = 0; k < NXA; ++k) v += sAt[k * NXA + i] * sPA[k * NXA + j];
-                    sQxx[e] = v;
-                } else if (e < NXA * NXA + NUA * NXA) {
-                    const int o = e - NXA * NXA, i = o / NXA, j = o % NXA;
-                    double v = sH[(NXA + i) * NZ + j];
-                    if (dyn)
-                        for (int k = 0; k < NXA; ++k) v += sBt[k * NUA + i] * sPA[k * NXA + j];
-                    sQux[o] = pinned(t, NXA + i) ? 0.0 : v;
-                } else {
-                    const int o = e - NXA * NXA - NUA * NXA, i = o / NUA, j = o % NUA;
-                    double v = sH[(NXA + i) * NZ + NXA + j];
-                    if (dyn)
-                        for (int k = 0; k < NXA; ++k) v += sBt[k * NUA + i] * sPB[k * NUA + j];
-                    if (pinned(t, NXA + i) || pinned(t, NXA + j)) v = (i == j) ? 1.0 : 0.0;
-                    sQuu[o] = v;
-                }
+            wsync();
+            #pragma unroll
+            for (int r = 0; r < R2; ++r) {
+                double v = pk[h2[r]];
+                double d = v;
+                #pragma unroll
+                for (int k = 0; k < NXA; ++k) d += pk[a2[r] + k] * sPAB[b2[r] + k];
+                v = dyn ? d : v;
+                const bool pi = ci2[r] == 1 ? pinU : (ci2[r] == 2 ? pinN : false);
+                const bool pj = cj2[r] == 1 ? pinU : (cj2[r] == 2 ? pinN : false);
+                if (kd2[r] == 1) v = pi ? 0.0 : v;
+                if (kd2[r] >= 2) v = (pi || pj) ? (kd2[r] == 3 ? 1.0 : 0.0) : v;
+                *o2[r] = v;
             }
             wsync();
             double Lm[NUA * NUA];
             #pragma unroll
             for (int e = 0; e < NUA * NUA; ++e) Lm[e] = sQuu[e];
             ldl_factor<NUA>(Lm, NUA);
-            {  // every lane solves (lanes >= NXA on a copy of column 0, stored to the junk slot)
-                const bool kl = lane < NXA;
-                const int c = kl ? lane : 0;
+            {  // every lane solves (lanes >= NXA on a copy of column 0, stored to the sinks)
                 double x[NUA];
                 #pragma unroll
-                for (int i = 0; i < NUA; ++i) x[i] = -sQux[i * NXA + c];
+                for (int i = 0; i < NUA; ++i) x[i] = -sQuxC[kc * NUA + i];
                 ldl_solve<NUA>(Lm, NUA, x);
                 #pragma unroll
                 for (int i = 0; i < NUA; ++i) {
-                    if (kl) sK[i * NXA + lane] = x[i];
+                    *(kl ? sKC + kc * NUA + i : sSink + lane) = x[i];
                     *(kl ? nb(t) + Ly.o_K + i * NXA + lane : jnk) = x[i];
                 }
                 double lv = 0.0;  // element `lane` of the factor (select chain: no dynamic register index)
@@ -772,14 +823,15 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             }
             wsync();
             #pragma unroll
-            for (int rep = 0; rep < (NXA * NXA + WAVE - 1) / WAVE; ++rep) {
+            for (int rep = 0; rep < R4; ++rep) {
                 const int e = lane + rep * WAVE;
                 const bool ok = e < NXA * NXA;
                 const int ee = ok ? e : 0;
                 const int i = ee / NXA, j = ee % NXA, p = i < j ? i : j, q = i < j ? j : i;
                 double v = sQxx[p * NXA + q];
-                for (int k = 0; k < NUA; ++k) v += sQux[k * NXA + p] * sK[k * NXA + q];
-                if (ok) sP[e] = v;
+                #pragma unroll
+                for (int k = 0; k < NUA; ++k) v += sQuxC[p * NUA + k] * sKC[q * NUA + k];
+                *(ok ? sP + e : sSink + lane) = v;
                 *(ok ? nb(t) + Ly.o_Pr + e : jnk) = v;
             }
             park(slot ^ 1);
@@ -799,12 +851,14 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             const int dn[7] = {1, 0, 0, 0, 0, 0, 0};
             const int off[7] = {Ly.o_Pr, Ly.o_rp, Ly.o_f, Ly.o_At, Ly.o_Bt, Ly.o_LD, Ly.o_K};
             const int len[7] = {NXA * NXA, NXA, NZ, NXA * NXA, NXA * NUA, NUA * NUA, NUA * NXA};
-            gather(K - 1, dn, off, len, 7);
+            int fo[PF], fd[PF];
+            seg_map(dn, off, len, 7, fo, fd);
+            gather(K - 1, fo, fd);
             park(0);
             wsync();
             for (int t = K - 1; t >= 0; --t) {
                 const int slot = (K - 1 - t) & 1;
-                gather(t - 1, dn, off, len, 7);
+                gather(t - 1, fo, fd);
                 const double* pk = sRing[slot];
                 const bool dyn = t < K - 1;
                 if (lane < NXA) {
@@ -891,13 +945,15 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             const int dn[7] = {0, 0, 0, 0, 0, 1, 1};
             const int off[7] = {Ly.o_kv, Ly.o_K, Ly.o_rp, Ly.o_At, Ly.o_Bt, Ly.o_pv, Ly.o_Pr};
             const int len[7] = {NUA, NUA * NXA, NXA, NXA * NXA, NXA * NUA, NXA, NXA * NXA};
-            gather(0, dn, off, len, 7);
+            int fo[PF], fd[PF];
+            seg_map(dn, off, len, 7, fo, fd);
+            gather(0, fo, fd);
             park(0);
             wsync();
             int cur = 0;
             for (int t = 0; t < K; ++t) {
                 const int slot = t & 1;
-                gather(t + 1, dn, off, len, 7);
+                gather(t + 1, fo, fd);
                 const double* pk = sRing[slot];
                 double* B = nb(t);
                 {
