@@ -52,7 +52,7 @@ struct SCPLay {
     int RH, NS, Q, RL, ROWS, stride;
     int o_rows, o_q, o_P, o_At, o_Bt, o_ct, o_z, o_sig, o_s, o_lam, o_wl, o_sw, o_lt, o_H, o_f, o_rd, o_rc, o_rsig,
         o_t, o_rho, o_rhs, o_dz, o_dsig, o_ds, o_dl, o_dsa, o_dla, o_y, o_yp, o_rp, o_K, o_Pr, o_pv, o_kv, o_LD, o_nh,
-        o_zb, o_sgb;
+        o_zb, o_sgb, o_Acl, o_g, o_w, o_e;
 };
 
 // augmented game states: u~_k = u_{k-1} (m), th~_k = th_{k-1} (1 when the model has a heading)
@@ -111,6 +111,10 @@ __host__ __device__ inline SCPLay scp_layout(const scvx_scp_template& T) {
     L.o_nh = take(1);
     L.o_zb = take(NZ);       // best iterate (z, soft slacks) once the reduced tolerances hold
     L.o_sgb = take(L.NS);
+    L.o_Acl = take(NXA * NXA);  // closed-loop Acl = At + Bt K (row-major), LQ chain offsets g, w, e
+    L.o_g = take(NXA);
+    L.o_w = take(NXA);
+    L.o_e = take(NXA);
     L.stride = (o + 7) & ~7;
     if (L.stride < 64) L.stride = 64;  // the junk block after the K node blocks holds one slot per lane
     return L;
@@ -145,6 +149,13 @@ __device__ __forceinline__ void ldl_solve(const double (&Lm)[D * D], int nn, dou
     for (int i = 0; i < nn; ++i) x[i] *= Lm[i * D + i];
     for (int i = nn - 1; i >= 0; --i)
         for (int k = i + 1; k < nn; ++k) x[i] -= Lm[k * D + i] * x[k];
+}
+
+// keep a value opaque to the optimiser: per-sweep decoded offsets derived from it are then computed
+// where the sweep starts instead of being hoisted out of the IPM loop (and held live across it)
+__device__ __forceinline__ int scp_opaque(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
 }
 
 // ---- second-order cone algebra (dimension Q = m + 1 <= 4), hyperbolic-rotation NT scaling
@@ -346,9 +357,8 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
     const double* xfin = a.x_final + agent * NX;
     const bool fin = T.has_final != 0;
 
-    __shared__ double sP[NXA * NXA], sPv[NXA], sPAB[NXA * (NXA + NUA)], sQxx[NXA * NXA], sQuxC[NUA * NXA],
-        sQuu[NUA * NUA], sKC[NUA * NXA], sV[NXA], sQ[NZ],
-        sXi[2][NXA], sU[NUA], sMisc[32];
+    __shared__ double sP[NXA * NXA], sPAB[NXA * (NXA + NUA)], sQxx[NXA * NXA], sQuxC[NUA * NXA],
+        sQuu[NUA * NUA], sKC[NUA * NXA], sXi[NXA], sMisc[32];
     // sMisc: 0..NX-1 r_init, 8..8+NX-1 y0+, 16.. scalars
     auto pinned = [&](int t, int i) -> bool {  // i: z index
         if (i >= ZU && i < ZN) return (t == 0 && T.pin_u_first) || (t == K - 1 && T.pin_u_last);
@@ -675,22 +685,6 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
     __shared__ double sRing[2][PF * WAVE];
     __shared__ double sSink[WAVE];  // LDS stores of lanes without an output element
     double pf[PF];
-    // segments: {node offset (0 or +1), node-block offset, length} -> per-lane element map
-    auto seg_map = [&](const int (&dn)[7], const int (&off)[7], const int (&len)[7], int nseg, int (&fo)[PF],
-                       int (&fd)[PF]) {
-        #pragma unroll
-        for (int c = 0; c < PF; ++c) {
-            const int e = lane + c * WAVE;
-            int o = off[0], d = dn[0], acc = 0;
-            #pragma unroll
-            for (int sg = 0; sg < 7; ++sg) {
-                if (sg < nseg && e >= acc && e < acc + len[sg]) { o = off[sg] + (e - acc); d = dn[sg]; }
-                if (sg < nseg) acc += len[sg];
-            }
-            fo[c] = o;
-            fd[c] = d;
-        }
-    };
     auto gather = [&](int t, const int (&fo)[PF], const int (&fd)[PF]) {
         #pragma unroll
         for (int c = 0; c < PF; ++c) {
@@ -716,6 +710,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
     // Every accumulation runs in the order of oracle/scp_cpu.py's restatement (and of the previous
     // element-loop form of this sweep): sequential k, starting from the H element.
     auto factor = [&]() __attribute__((always_inline)) {
+        const int lane = scp_opaque(threadIdx.x);
         constexpr int R1 = (NXA * NAB + WAVE - 1) / WAVE;
         constexpr int E2 = NXA * NXA + NXA * NUA + NUA * NUA, R2 = (E2 + WAVE - 1) / WAVE;
         constexpr int R4 = (NXA * NXA + WAVE - 1) / WAVE;
@@ -838,75 +833,140 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             wsync();
         }
         __syncthreads();
+        // closed-loop Acl_t = At_t + Bt_t K_t (row-major), the LQ chains' matrices: lane-parallel over nodes
+        for (int t = lane; t < K - 1; t += WAVE) {
+            double* B = nb(t);
+            double Kt[NUA * NXA];
+            #pragma unroll
+            for (int e = 0; e < NUA * NXA; ++e) Kt[e] = B[Ly.o_K + e];
+            #pragma unroll
+            for (int i = 0; i < NXA; ++i) {
+                double bi[NUA];
+                #pragma unroll
+                for (int k = 0; k < NUA; ++k) bi[k] = B[Ly.o_Bt + i * NUA + k];
+                #pragma unroll
+                for (int j = 0; j < NXA; ++j) {
+                    double v = B[Ly.o_At + i * NXA + j];
+                    #pragma unroll
+                    for (int k = 0; k < NUA; ++k) v += bi[k] * Kt[k * NXA + j];
+                    B[Ly.o_Acl + i * NXA + j] = v;
+                }
+            }
+        }
+        __syncthreads();
     };
 
     // ------------------------------------------------------------------ LQ solve
     // In: o_f (per node), o_rp (t < K-1), sMisc[0..NX) = r_init.  Out: o_dz, o_yp (costates y+),
     // sMisc[8..8+NX) = y0+.
+    // Closed-loop form: with Acl_t = At_t + Bt_t K_t (the factor's output) the backward recursion
+    //   v = P_{t+1} rp_t + p_{t+1}; q = f + [At Bt]'v; k_t = -Quu^-1 q_u; p_t = q_x + K_t'q_u
+    // is p_t = Acl_t' p_{t+1} + g_t with g_t = f_x + K_t'f_u + Acl_t' P_{t+1} rp_t (K_t's pinned rows are 0),
+    // and the forward one xi_{t+1} = Acl_t xi_t + e_t with e_t = rp_t + Bt_t k_t.  Only these two NXA-vector
+    // recursions are sequential: each step is one NXA-term dot product per lane (lane i: element i), the
+    // previous vector broadcast by 64-bit DPP row_newbcast, operands prefetched four steps ahead.  g_t,
+    // k_t, e_t and the outputs u_t, y+_t are lane-parallel passes over the nodes.
     auto lqsolve = [&]() __attribute__((always_inline)) {
-        // backward: v = P_{t+1} rp_t + p_{t+1}; qx = fx + At'v; qu = fu + Bt'v; k = -Quu^-1 qu; p = qx + K'qu
-        constexpr int B_PR = 0, B_RP = B_PR + NXA * NXA, B_F = B_RP + NXA, B_AT = B_F + NZ, B_BT = B_AT + NXA * NXA,
-                      B_LD = B_BT + NXA * NUA, B_K = B_LD + NUA * NUA;
-        {
-            const int dn[7] = {1, 0, 0, 0, 0, 0, 0};
-            const int off[7] = {Ly.o_Pr, Ly.o_rp, Ly.o_f, Ly.o_At, Ly.o_Bt, Ly.o_LD, Ly.o_K};
-            const int len[7] = {NXA * NXA, NXA, NZ, NXA * NXA, NXA * NUA, NUA * NUA, NUA * NXA};
-            int fo[PF], fd[PF];
-            seg_map(dn, off, len, 7, fo, fd);
-            gather(K - 1, fo, fd);
-            park(0);
-            wsync();
-            for (int t = K - 1; t >= 0; --t) {
-                const int slot = (K - 1 - t) & 1;
-                gather(t - 1, fo, fd);
-                const double* pk = sRing[slot];
-                const bool dyn = t < K - 1;
-                if (lane < NXA) {
-                    double v = 0.0;
-                    if (dyn) {
-                        v = sPv[lane];
-                        for (int k = 0; k < NXA; ++k) v += pk[B_PR + lane * NXA + k] * pk[B_RP + k];
-                    }
-                    sV[lane] = v;
-                }
-                wsync();
-                if (lane < NZ) {
-                    double v = pk[B_F + lane];
-                    if (dyn) {
-                        if (lane < NXA)
-                            for (int k = 0; k < NXA; ++k) v += pk[B_AT + k * NXA + lane] * sV[k];
-                        else
-                            for (int k = 0; k < NXA; ++k) v += pk[B_BT + k * NUA + lane - NXA] * sV[k];
-                    }
-                    if (pinned(t, lane)) v = 0.0;
-                    sQ[lane] = v;
-                }
-                wsync();
-                {
-                    double Lm[NUA * NUA], x[NUA];
-                    #pragma unroll
-                    for (int e = 0; e < NUA * NUA; ++e) Lm[e] = pk[B_LD + e];
-                    #pragma unroll
-                    for (int i = 0; i < NUA; ++i) x[i] = -sQ[NXA + i];
-                    ldl_solve<NUA>(Lm, NUA, x);
-                    // (select x[lane] without dynamic register indexing)
-                    double xv = 0.0;
-                    #pragma unroll
-                    for (int i = 0; i < NUA; ++i) xv = (i == lane) ? x[i] : xv;
-                    *(lane < NUA ? nb(t) + Ly.o_kv + lane : jnk) = xv;
-                }
-                double pn;
-                {
-                    const int li = lane < NXA ? lane : 0;
-                    pn = sQ[li];
-                    for (int k = 0; k < NUA; ++k) pn += pk[B_K + k * NXA + li] * sQ[NXA + k];
-                    *(lane < NXA ? nb(t) + Ly.o_pv + lane : jnk) = pn;
-                }
-                wsync();
-                if (lane < NXA) sPv[lane] = pn;
-                park(slot ^ 1);
-                wsync();
+        const int li = scp_opaque(lane < NXA ? lane : 0);
+        // ---- backward pre-pass: w_t = P_{t+1} rp_t, g_t
+        for (int t = lane; t < K; t += WAVE) {
+            double* B = nb(t);
+            const bool dyn = t < K - 1;
+            double w[NXA], g[NXA], fu[NUA];
+            #pragma unroll
+            for (int j = 0; j < NUA; ++j) fu[j] = B[Ly.o_f + NXA + j];
+            #pragma unroll
+            for (int i = 0; i < NXA; ++i) {
+                double v = B[Ly.o_f + i];
+                #pragma unroll
+                for (int j = 0; j < NUA; ++j) v += B[Ly.o_K + j * NXA + i] * fu[j];
+                g[i] = v;
             }
+            if (dyn) {
+                const double* Bn = nb(t + 1);
+                double rp[NXA];
+                #pragma unroll
+                for (int k = 0; k < NXA; ++k) rp[k] = B[Ly.o_rp + k];
+                #pragma unroll
+                for (int i = 0; i < NXA; ++i) {
+                    double v = 0.0;
+                    #pragma unroll
+                    for (int k = 0; k < NXA; ++k) v += Bn[Ly.o_Pr + i * NXA + k] * rp[k];
+                    w[i] = v;
+                    B[Ly.o_w + i] = v;
+                }
+                #pragma unroll
+                for (int i = 0; i < NXA; ++i) {
+                    double v = g[i];
+                    #pragma unroll
+                    for (int k = 0; k < NXA; ++k) v += B[Ly.o_Acl + k * NXA + i] * w[k];
+                    g[i] = v;
+                }
+            }
+            #pragma unroll
+            for (int i = 0; i < NXA; ++i) B[Ly.o_g + i] = g[i];
+        }
+        __syncthreads();
+        // ---- backward chain p_t = Acl_t' p_{t+1} + g_t  (lane i < NXA: element i; column i of Acl_t)
+        {
+            double ca[4][NXA], cg[4];
+            auto ld = [&](int t, double (&c)[NXA], double& gv) __attribute__((always_inline)) {
+                const double* B = nb(t > 0 ? t : 0);
+                #pragma unroll
+                for (int k = 0; k < NXA; ++k) c[k] = B[Ly.o_Acl + k * NXA + li];
+                gv = B[Ly.o_g + li];
+            };
+            double p = nb(K - 1)[Ly.o_g + li];
+            *(lane < NXA ? nb(K - 1) + Ly.o_pv + lane : jnk) = p;
+            ld(K - 2, ca[0], cg[0]);
+            ld(K - 3, ca[1], cg[1]);
+            ld(K - 4, ca[2], cg[2]);
+            ld(K - 5, ca[3], cg[3]);
+            auto step = [&](int t, double (&c)[NXA], double gv, double (&nc)[NXA], double& ng) __attribute__((always_inline)) {
+                double v = gv;
+                #pragma unroll
+                for (int k = 0; k < NXA; ++k) v += c[k] * row_bcast_d(p, k);
+                p = v;
+                *(lane < NXA ? nb(t) + Ly.o_pv + lane : jnk) = v;
+                ld(t - 4, nc, ng);  // stage t-4 into the slot just consumed
+            };
+            int t = K - 2;
+            while (true) {
+                step(t, ca[0], cg[0], ca[0], cg[0]); if (--t < 0) break;
+                step(t, ca[1], cg[1], ca[1], cg[1]); if (--t < 0) break;
+                step(t, ca[2], cg[2], ca[2], cg[2]); if (--t < 0) break;
+                step(t, ca[3], cg[3], ca[3], cg[3]); if (--t < 0) break;
+            }
+        }
+        __syncthreads();
+        // ---- backward post-pass: k_t = -Quu^-1 (f_u + Bt'(p_{t+1} + w_t)); e_t = rp_t + Bt k_t
+        for (int t = lane; t < K; t += WAVE) {
+            double* B = nb(t);
+            const bool dyn = t < K - 1;
+            double v[NXA], x[NUA], Lm[NUA * NUA];
+            #pragma unroll
+            for (int k = 0; k < NXA; ++k) v[k] = dyn ? nb(t + 1)[Ly.o_pv + k] + B[Ly.o_w + k] : 0.0;
+            #pragma unroll
+            for (int j = 0; j < NUA; ++j) {
+                double q = B[Ly.o_f + NXA + j];
+                if (dyn)
+                    #pragma unroll
+                    for (int k = 0; k < NXA; ++k) q += B[Ly.o_Bt + k * NUA + j] * v[k];
+                x[j] = pinned(t, NXA + j) ? 0.0 : -q;
+            }
+            #pragma unroll
+            for (int e = 0; e < NUA * NUA; ++e) Lm[e] = B[Ly.o_LD + e];
+            ldl_solve<NUA>(Lm, NUA, x);
+            #pragma unroll
+            for (int j = 0; j < NUA; ++j) B[Ly.o_kv + j] = x[j];
+            if (dyn)
+                #pragma unroll
+                for (int i = 0; i < NXA; ++i) {
+                    double e = B[Ly.o_rp + i];
+                    #pragma unroll
+                    for (int j = 0; j < NUA; ++j) e += B[Ly.o_Bt + i * NUA + j] * x[j];
+                    B[Ly.o_e + i] = e;
+                }
         }
         __syncthreads();
         // stage 0: x part fixed (-r_init), g part free: P_gg dg = -(p_g + P_gx dx)
@@ -926,63 +986,76 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             ldl_solve<SCP_NG>(Lm, SCP_NG, g);
             #pragma unroll
             for (int i = 0; i < NX; ++i)
-                if (lane == i) sXi[0][lane] = dx[i];
+                if (lane == i) sXi[lane] = dx[i];
             for (int i = 0; i < SCP_NG; ++i)
-                if (lane == NX + i) sXi[0][lane] = g[i];
-            if (lane >= E0 && lane < NXA) sXi[0][lane] = 0.0;  // u~_0, th~_0: no predecessor, no cost
+                if (lane == NX + i) sXi[lane] = g[i];
+            if (lane >= E0 && lane < NXA) sXi[lane] = 0.0;  // u~_0, th~_0: no predecessor, no cost
             __syncthreads();
             if (lane < NX) {
                 double v = B0[Ly.o_pv + lane];
-                for (int k = 0; k < NXA; ++k) v += B0[Ly.o_Pr + lane * NXA + k] * sXi[0][k];
+                for (int k = 0; k < NXA; ++k) v += B0[Ly.o_Pr + lane * NXA + k] * sXi[k];
                 sMisc[8 + lane] = v;
             }
         }
         __syncthreads();
-        // forward: u = kv + K xi; xi+ = rp + At xi + Bt u; y+ = p_{t+1} + P_{t+1} xi+
+        // ---- forward chain xi_{t+1} = Acl_t xi_t + e_t  (lane i < NXA: element i; row i of Acl_t)
         {
-            constexpr int W_KV = 0, W_K = W_KV + NUA, W_RP = W_K + NUA * NXA, W_AT = W_RP + NXA,
-                          W_BT = W_AT + NXA * NXA, W_PV1 = W_BT + NXA * NUA, W_PR1 = W_PV1 + NXA;
-            const int dn[7] = {0, 0, 0, 0, 0, 1, 1};
-            const int off[7] = {Ly.o_kv, Ly.o_K, Ly.o_rp, Ly.o_At, Ly.o_Bt, Ly.o_pv, Ly.o_Pr};
-            const int len[7] = {NUA, NUA * NXA, NXA, NXA * NXA, NXA * NUA, NXA, NXA * NXA};
-            int fo[PF], fd[PF];
-            seg_map(dn, off, len, 7, fo, fd);
-            gather(0, fo, fd);
-            park(0);
-            wsync();
-            int cur = 0;
-            for (int t = 0; t < K; ++t) {
-                const int slot = t & 1;
-                gather(t + 1, fo, fd);
-                const double* pk = sRing[slot];
-                double* B = nb(t);
-                {
-                    const int lu = lane < NUA ? lane : 0;
-                    double v = pk[W_KV + lu];
-                    for (int k = 0; k < NXA; ++k) v += pk[W_K + lu * NXA + k] * sXi[cur][k];
-                    if (lane < NUA) sU[lane] = v;
-                    *(lane < NUA ? B + Ly.o_dz + NXA + lane : jnk) = v;
+            double ca[4][NXA], ce[4];
+            auto ld = [&](int t, double (&c)[NXA], double& ev) __attribute__((always_inline)) {
+                const double* B = nb(t < K - 2 ? t : K - 2);
+                #pragma unroll
+                for (int k = 0; k < NXA; ++k) c[k] = B[Ly.o_Acl + li * NXA + k];
+                ev = B[Ly.o_e + li];
+            };
+            double xi = sXi[li];
+            *(lane < NXA ? nb(0) + Ly.o_dz + lane : jnk) = xi;
+            ld(0, ca[0], ce[0]);
+            ld(1, ca[1], ce[1]);
+            ld(2, ca[2], ce[2]);
+            ld(3, ca[3], ce[3]);
+            auto step = [&](int t, double (&c)[NXA], double ev, double (&nc)[NXA], double& ne) __attribute__((always_inline)) {
+                double v = ev;
+                #pragma unroll
+                for (int k = 0; k < NXA; ++k) v += c[k] * row_bcast_d(xi, k);
+                xi = v;
+                *(lane < NXA ? nb(t + 1) + Ly.o_dz + lane : jnk) = v;
+                ld(t + 4, nc, ne);
+            };
+            int t = 0;
+            while (true) {
+                if (t > K - 2) break;
+                step(t, ca[0], ce[0], ca[0], ce[0]); if (++t > K - 2) break;
+                step(t, ca[1], ce[1], ca[1], ce[1]); if (++t > K - 2) break;
+                step(t, ca[2], ce[2], ca[2], ce[2]); if (++t > K - 2) break;
+                step(t, ca[3], ce[3], ca[3], ce[3]); ++t;
+            }
+        }
+        __syncthreads();
+        // ---- forward post-pass: u_t = k_t + K_t xi_t; y+_t = p_{t+1} + P_{t+1} xi_{t+1}
+        for (int t = lane; t < K; t += WAVE) {
+            double* B = nb(t);
+            double xi[NXA];
+            #pragma unroll
+            for (int k = 0; k < NXA; ++k) xi[k] = B[Ly.o_dz + k];
+            #pragma unroll
+            for (int j = 0; j < NUA; ++j) {
+                double v = B[Ly.o_kv + j];
+                #pragma unroll
+                for (int k = 0; k < NXA; ++k) v += B[Ly.o_K + j * NXA + k] * xi[k];
+                B[Ly.o_dz + NXA + j] = v;
+            }
+            if (t < K - 1) {
+                const double* Bn = nb(t + 1);
+                double x1[NXA];
+                #pragma unroll
+                for (int k = 0; k < NXA; ++k) x1[k] = Bn[Ly.o_dz + k];
+                #pragma unroll
+                for (int i = 0; i < NXA; ++i) {
+                    double v = Bn[Ly.o_pv + i];
+                    #pragma unroll
+                    for (int k = 0; k < NXA; ++k) v += Bn[Ly.o_Pr + i * NXA + k] * x1[k];
+                    B[Ly.o_yp + i] = v;
                 }
-                *(lane < NXA ? B + Ly.o_dz + lane : jnk) = sXi[cur][lane < NXA ? lane : 0];
-                wsync();
-                if (t < K - 1) {
-                    if (lane < NXA) {
-                        double v = pk[W_RP + lane];
-                        for (int k = 0; k < NXA; ++k) v += pk[W_AT + lane * NXA + k] * sXi[cur][k];
-                        for (int k = 0; k < NUA; ++k) v += pk[W_BT + lane * NUA + k] * sU[k];
-                        sXi[cur ^ 1][lane] = v;
-                    }
-                    wsync();
-                    cur ^= 1;
-                    {
-                        const int li = lane < NXA ? lane : 0;
-                        double v = pk[W_PV1 + li];
-                        for (int k = 0; k < NXA; ++k) v += pk[W_PR1 + li * NXA + k] * sXi[cur][k];
-                        *(lane < NXA ? B + Ly.o_yp + lane : jnk) = v;
-                    }
-                }
-                park(slot ^ 1);
-                wsync();
             }
         }
         __syncthreads();
