@@ -329,8 +329,8 @@ __device__ __forceinline__ void rows_update(double* __restrict__ sl, double* __r
     for (int r = r0; r < r1; ++r) { sl[r] += al * ds[r]; lam[r] += al * dl[r]; }
 }
 
-template <int NX, int NU, int NE>
-__global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restrict__ ws_all, const double* __restrict__ disc_all) {
+template <int NX, int NU, int NE, int NW>
+__global__ __launch_bounds__(64 * NW) void scp_ipm_kernel(SCPArgs a, double* __restrict__ ws_all, const double* __restrict__ disc_all) {
     // workspace and disc come in as kernel pointer arguments (known global address space): read out
     // of the by-value struct they would be FLAT accesses, which also count against lgkmcnt, so every
     // LDS wait would drain the outstanding global loads
@@ -339,8 +339,30 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
     // game terms (NE > 0): E0..E0+NU-1 = u~, E0+NU = th~ (when T.theta_idx >= 0)
     constexpr int QM = NU + 1;
     const scvx_scp_template& T = a.T;
+    __shared__ double sRed[NW];
+    // reductions over the agent's threads (result uniform across its waves)
+    auto blk_red = [&](double v, int op) -> double {
+        v = op == 0 ? wave_sum(v) : (op == 1 ? wave_max(v) : wave_min(v));
+        if constexpr (NW > 1) {
+            if ((threadIdx.x & (WAVE - 1)) == 0) sRed[threadIdx.x / WAVE] = v;
+            __syncthreads();
+            double r = sRed[0];
+            #pragma unroll
+            for (int w = 1; w < NW; ++w) r = op == 0 ? r + sRed[w] : (op == 1 ? fmax(r, sRed[w]) : fmin(r, sRed[w]));
+            __syncthreads();
+            v = r;
+        }
+        return v;
+    };
+    auto blk_sum = [&](double v) { return blk_red(v, 0); };
+    auto blk_max = [&](double v) { return blk_red(v, 1); };
+    auto blk_min = [&](double v) { return blk_red(v, 2); };
     const bool sfix = NE > 0 && T.sigma_fixed != 0;
-    const int K = T.K, lane = threadIdx.x, pd = T.pos_dim;
+    // NW waves per agent: node phases over all NW * 64 threads (thread tid: nodes tid, tid + NT, ...); the
+    // sequential sweeps (factor, LQ chains) on wave 0 while the others wait at the next block barrier
+    constexpr int NT = NW * WAVE;
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid / WAVE;
+    const int K = T.K, pd = T.pos_dim;
     const long long agent = blockIdx.x;
     const SCPLay Ly = scp_layout(T);
     const int RH = Ly.RH, NS = Ly.NS, Q = Ly.Q, RL = Ly.RL, NLP = RH + 2 * NS;
@@ -372,21 +394,21 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
     // ------------------------------------------------------------------ setup (rows, dynamics)
     // objective scale: every cost term / cs (oracle/scp_cpu.py build_nodes)
     double csl = 0.0;
-    for (int t = lane; t < K; t += WAVE) {
+    for (int t = tid; t < K; t += NT) {
         for (int j = 0; j < T.n_nbr; ++j)
             for (int i = 0; i < pd; ++i) {
                 const long long o = ((agent * T.n_nbr + j) * K + t) * pd + i;
                 csl = fmax(csl, fabs(a.nbr_Lam[o] - T.rho * a.nbr_Y[o]));
             }
     }
-    double cs = wave_max(csl);
+    double cs = blk_max(csl);
     cs = fmax(cs, fmax(1.0, fmax(T.w_nu, T.w_sigma)));
     if (T.n_obs > 0) cs = fmax(cs, T.w_slack);
     if (T.n_nbr > 0) cs = fmax(cs, fmax(T.w_coll, T.rho));
     const double ics = 1.0 / cs;
     const double w_obs = T.w_slack * ics, w_col = T.w_coll * ics;
     double hmax = 0.0, qmax = 0.0, degl = 0.0;
-    for (int t = lane; t < K; t += WAVE) {
+    for (int t = tid; t < K; t += NT) {
         double* B = nb(t);
         double xb[NX], ub[NU];
         #pragma unroll
@@ -655,12 +677,12 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
         }
     }
     if (lane < NX) hmax = fmax(hmax, fabs(xinit[lane]));
-    const double pscale = 1.0 + wave_max(hmax);
-    double dsc = wave_max(qmax);
+    const double pscale = 1.0 + blk_max(hmax);
+    double dsc = blk_max(qmax);
     if (T.n_obs > 0) dsc = fmax(dsc, w_obs);
     if (T.n_nbr > 0) dsc = fmax(dsc, w_col);
     const double dscale = 1.0 + dsc;
-    const double deg = wave_sum(degl);
+    const double deg = blk_sum(degl);
     __syncthreads();
 
     auto soft_w = [&](int r) -> double { return r < T.n_obs ? w_obs : w_col; };
@@ -710,6 +732,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
     // Every accumulation runs in the order of oracle/scp_cpu.py's restatement (and of the previous
     // element-loop form of this sweep): sequential k, starting from the H element.
     auto factor = [&]() __attribute__((always_inline)) {
+      if (wid == 0) {  // the sweep: wave 0
         const int lane = scp_opaque(threadIdx.x);
         constexpr int R1 = (NXA * NAB + WAVE - 1) / WAVE;
         constexpr int E2 = NXA * NXA + NXA * NUA + NUA * NUA, R2 = (E2 + WAVE - 1) / WAVE;
@@ -832,9 +855,10 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             park(slot ^ 1);
             wsync();
         }
+      }
         __syncthreads();
         // closed-loop Acl_t = At_t + Bt_t K_t (row-major), the LQ chains' matrices: lane-parallel over nodes
-        for (int t = lane; t < K - 1; t += WAVE) {
+        for (int t = tid; t < K - 1; t += NT) {
             double* B = nb(t);
             double Kt[NUA * NXA];
             #pragma unroll
@@ -869,7 +893,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
     auto lqsolve = [&]() __attribute__((always_inline)) {
         const int li = scp_opaque(lane < NXA ? lane : 0);
         // ---- backward pre-pass: w_t = P_{t+1} rp_t, g_t
-        for (int t = lane; t < K; t += WAVE) {
+        for (int t = tid; t < K; t += NT) {
             double* B = nb(t);
             const bool dyn = t < K - 1;
             double w[NXA], g[NXA], fu[NUA];
@@ -908,7 +932,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
         }
         __syncthreads();
         // ---- backward chain p_t = Acl_t' p_{t+1} + g_t  (lane i < NXA: element i; column i of Acl_t)
-        {
+        if (wid == 0) {
             double ca[4][NXA], cg[4];
             auto ld = [&](int t, double (&c)[NXA], double& gv) __attribute__((always_inline)) {
                 const double* B = nb(t > 0 ? t : 0);
@@ -940,7 +964,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
         }
         __syncthreads();
         // ---- backward post-pass: k_t = -Quu^-1 (f_u + Bt'(p_{t+1} + w_t)); e_t = rp_t + Bt k_t
-        for (int t = lane; t < K; t += WAVE) {
+        for (int t = tid; t < K; t += NT) {
             double* B = nb(t);
             const bool dyn = t < K - 1;
             double v[NXA], x[NUA], Lm[NUA * NUA];
@@ -999,7 +1023,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
         }
         __syncthreads();
         // ---- forward chain xi_{t+1} = Acl_t xi_t + e_t  (lane i < NXA: element i; row i of Acl_t)
-        {
+        if (wid == 0) {
             double ca[4][NXA], ce[4];
             auto ld = [&](int t, double (&c)[NXA], double& ev) __attribute__((always_inline)) {
                 const double* B = nb(t < K - 2 ? t : K - 2);
@@ -1032,7 +1056,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
         }
         __syncthreads();
         // ---- forward post-pass: u_t = k_t + K_t xi_t; y+_t = p_{t+1} + P_{t+1} xi_{t+1}
-        for (int t = lane; t < K; t += WAVE) {
+        for (int t = tid; t < K; t += NT) {
             double* B = nb(t);
             double xi[NXA];
             #pragma unroll
@@ -1071,7 +1095,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
     };
 
     // ------------------------------------------------------------------ starting point (W = I)
-    for (int t = lane; t < K; t += WAVE) {
+    for (int t = tid; t < K; t += NT) {
         double* B = nb(t);
         const int nh = (int)B[Ly.o_nh];
         double Hu[NZ * NZ], f[NZ];
@@ -1121,12 +1145,12 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             #pragma unroll
             for (int i = 0; i < NXA; ++i) B[Ly.o_rp + i] = B[Ly.o_ct + i];
     }
-    if (lane < NX) sMisc[lane] = -xinit[lane];
+    if (tid < NX) sMisc[tid] = -xinit[tid];
     __syncthreads();
     factor();
     lqsolve();
     double mins = INFINITY, minl = INFINITY;
-    for (int t = lane; t < K; t += WAVE) {
+    for (int t = tid; t < K; t += NT) {
         double* B = nb(t);
         const int nh = (int)B[Ly.o_nh];
         double z[NZ];
@@ -1163,9 +1187,9 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
         for (int i = 0; i < NXA; ++i) B[Ly.o_y + i] = 0.0;
     }
     {
-        const double as = wave_min(mins), al = wave_min(minl);
+        const double as = blk_min(mins), al = blk_min(minl);
         const double sh_s = fmax(0.0, 1.0 - as), sh_l = fmax(0.0, 1.0 - al);
-        for (int t = lane; t < K; t += WAVE) {
+        for (int t = tid; t < K; t += NT) {
             double* B = nb(t);
             const int nh = (int)B[Ly.o_nh];
             for (int r = 0; r < NLP; ++r) {
@@ -1199,7 +1223,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
     for (it = 0; it < T.max_iter; ++it) {
         // ---- residuals (node-parallel); rp needs xi~_{t+1}
         double gapl = 0.0, pobjl = 0.0, presl = 0.0, dresl = 0.0;
-        for (int t = lane; t < K; t += WAVE) {
+        for (int t = tid; t < K; t += NT) {
             double* B = nb(t);
             const int nh = (int)B[Ly.o_nh];
             double z[NZ], rd[NZ];
@@ -1283,7 +1307,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
                 if (!pinned(t, i)) dresl = fmax(dresl, fabs(rd[i]));
         }
         SCP_TR(0)
-        const double gap = wave_sum(gapl), pobj = wave_sum(pobjl), pres = wave_max(presl), dres = wave_max(dresl);
+        const double gap = blk_sum(gapl), pobj = blk_sum(pobjl), pres = blk_max(presl), dres = blk_max(dresl);
         if (!(gap == gap) || !(pres == pres) || !(dres == dres)) { status = 2; break; }
         if (pres < T.tol * pscale && dres < T.tol * dscale && gap < T.tol * fmax(1.0, fabs(pobj))) { status = 0; break; }
         // ECOS-style reduced tolerances: an iterate meeting them is reported "optimal_inaccurate"
@@ -1305,7 +1329,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             const double score = fmax(fmax(pres / pscale, dres / dscale), gap / fmax(1.0, fabs(pobj)));
             if (near_ok && score < score_best) {  // snapshot (uniform branch: the scores are wave reductions)
                 score_best = score;
-                for (int t = lane; t < K; t += WAVE) {
+                for (int t = tid; t < K; t += NT) {
                     double* B = nb(t);
                     #pragma unroll
                     for (int i = 0; i < NZ; ++i) B[Ly.o_zb + i] = B[Ly.o_z + i];
@@ -1314,9 +1338,9 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             }
         }
         const double mu = gap / deg;
-        if (lane < NX) sMisc[lane] = nb(0)[Ly.o_z + lane] - xinit[lane];  // r_init
+        if (tid < NX) sMisc[tid] = nb(0)[Ly.o_z + tid] - xinit[tid];  // r_init
         // ---- scaling and node Hessians
-        for (int t = lane; t < K; t += WAVE) {
+        for (int t = tid; t < K; t += NT) {
             double* B = nb(t);
             const int nh = (int)B[Ly.o_nh];
             double Hu[NZ * NZ];
@@ -1391,7 +1415,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
 
         // ---- one Newton direction: corrector = false -> affine (predictor)
         auto direction = [&](bool corr, double sgmu) __attribute__((always_inline)) -> double {
-            for (int t = lane; t < K; t += WAVE) {
+            for (int t = tid; t < K; t += NT) {
                 double* B = nb(t);
                 const int nh = (int)B[Ly.o_nh];
                 double f[NZ];
@@ -1452,7 +1476,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             SCP_TR(4)
             // recover slack steps, step length
             double amax = INFINITY;
-            for (int t = lane; t < K; t += WAVE) {
+            for (int t = tid; t < K; t += NT) {
                 double* B = nb(t);
                 const int nh = (int)B[Ly.o_nh];
                 double dz[NZ];
@@ -1502,14 +1526,14 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
                     amax = fmin(amax, fmin(Soc<QM>::step(sv, ds, Q), Soc<QM>::step(lv, dl, Q)));
                 }
             }
-            const double am = wave_min(amax);
+            const double am = blk_min(amax);
             SCP_TR(5)
             return am;
         };
 
         const double aa = fmin(1.0, direction(false, 0.0));
         double mual = 0.0;
-        for (int t = lane; t < K; t += WAVE) {
+        for (int t = tid; t < K; t += NT) {
             double* B = nb(t);
             const int nh = (int)B[Ly.o_nh];
             rows_mu(B + Ly.o_s, B + Ly.o_lam, B + Ly.o_ds, B + Ly.o_dl, 0, nh, aa, mual);
@@ -1518,14 +1542,14 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             // SOC: keep ds_a, dl_a raw (scaled inside direction())
             rows_copy2(B + Ly.o_ds, B + Ly.o_dl, B + Ly.o_dsa, B + Ly.o_dla, RL);
         }
-        const double mu_a = wave_sum(mual) / deg;
+        const double mu_a = blk_sum(mual) / deg;
         const double sg = (mu_a / mu) * (mu_a / mu) * (mu_a / mu);
         __syncthreads();
         const double al = fmin(1.0, 0.99 * direction(true, sg * mu));
         // ---- breakdown guard: a non-finite direction (Riccati overflow in the end-game) ends the
         // solve on the current, finite iterate instead of corrupting it
         double badl = (al > 0.0) ? 0.0 : 1.0;
-        for (int t = lane; t < K; t += WAVE) {
+        for (int t = tid; t < K; t += NT) {
             const double* B = nb(t);
             const int nh = (int)B[Ly.o_nh];
             double acc = 0.0;
@@ -1544,13 +1568,13 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
         #pragma unroll
         for (int i = 0; i < NX; ++i)
             if (!(fabs(sMisc[8 + i]) < INFINITY)) badl = 1.0;
-        if (wave_max(badl) > 0.0) {
+        if (blk_max(badl) > 0.0) {
             if (regv < 1e-5) { regv *= 100.0; __syncthreads(); continue; }   // retry, stiffer
             status = near_ok ? 1 : 2;
             break;
         }
         // ---- update
-        for (int t = lane; t < K; t += WAVE) {
+        for (int t = tid; t < K; t += NT) {
             double* B = nb(t);
             const int nh = (int)B[Ly.o_nh];
             #pragma unroll
@@ -1569,14 +1593,14 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
         SCP_TR(6)
     }
 #ifdef SCP_TRACE
-    if (agent == 0 && lane == 0)
+    if (agent == 0 && tid == 0)
         printf("SCP_TRACE it=%d res=%lld hess=%lld factor=%lld dirnode=%lld lqsolve=%lld step=%lld upd=%lld\n", it,
                tr_acc[0], tr_acc[1], tr_acc[2], tr_acc[3], tr_acc[4], tr_acc[5], tr_acc[6]);
 #endif
 
     if (status == 1 && it == T.max_iter && !near_ok) status = 2;   // cap reached far from optimal
     if (restore) {
-        for (int t = lane; t < K; t += WAVE) {
+        for (int t = tid; t < K; t += NT) {
             double* B = nb(t);
             #pragma unroll
             for (int i = 0; i < NZ; ++i) B[Ly.o_z + i] = B[Ly.o_zb + i];
@@ -1587,7 +1611,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
     // ------------------------------------------------------------------ outputs
     double sigv = sfix ? sref : nb(0)[Ly.o_z + SIG];
     double numaxl = 0.0, softl = 0.0, admml = 0.0;
-    for (int t = lane; t < K; t += WAVE) {
+    for (int t = tid; t < K; t += NT) {
         double* B = nb(t);
         double u[NU], x[NX];
         #pragma unroll
@@ -1630,7 +1654,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
     }
     __syncthreads();
     // nu_{K-2} from the dynamics (x_{K-1} = x_final)
-    if (fin && K >= 2 && lane == 0) {
+    if (fin && K >= 2 && tid == 0) {
         const int t = K - 2;
         const double* dk = disc + (long long)t * DSTR;
         const double* xk = a.X + (agent * K + t) * NX;
@@ -1651,7 +1675,7 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
     double gamel = 0.0;
     if (NE > 0) {  // the game cost at the solution (game_model.py:87-100)
         __syncthreads();
-        for (int t = lane; t < K; t += WAVE) {
+        for (int t = tid; t < K; t += NT) {
             const double* x = a.X + (agent * K + t) * NX;
             const double* u = a.U + (agent * K + t) * NU;
             #pragma unroll
@@ -1672,8 +1696,8 @@ __global__ __launch_bounds__(64) void scp_ipm_kernel(SCPArgs a, double* __restri
             }
         }
     }
-    const double numax = wave_max(numaxl), soft = wave_sum(softl), admm = wave_sum(admml), game = wave_sum(gamel);
-    if (lane == 0) {
+    const double numax = blk_max(numaxl), soft = blk_sum(softl), admm = blk_sum(admml), game = blk_sum(gamel);
+    if (tid == 0) {
         a.sigma[agent] = sigv;
         a.obj[agent] = T.w_nu * numax + soft + T.w_sigma * sigv + admm + game;
         a.status[agent] = status;
@@ -1737,19 +1761,29 @@ static int scp_launch(const scvx_scp_template* T, int N, const double* disc, con
     a.ws_agent = (long long)scp_layout(*T).stride * (T->K + 1);
     hipStream_t st = (hipStream_t)stream;
     const int ne = scp_ne(*T);
+    // two waves per agent (node phases in one pass over K <= 128 nodes) when the launch leaves SIMDs idle:
+    // the kernel holds a SIMD's whole register file, so at most one wave per SIMD runs
+    static int simds = 0;
+    if (!simds) {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+            simds = 4 * cus;
+        if (simds <= 0) simds = 1024;
+    }
+    const bool two = T->K > WAVE && 2LL * N <= simds;
     if (T->model_id == SCVX_MODEL_UNICYCLE && T->n_x == 3 && T->n_u == 2) {
         if (T->has_soc) return set_error(SCVX_EUNSUPPORTED, "scp: SOC rows need n_u + 1 <= 4");
         if (ne == 0)
-            hipLaunchKernelGGL((scp_ipm_kernel<3, 2, 0>), dim3(N), dim3(WAVE), 0, st, a, a.ws, a.disc);
+            { if (two) hipLaunchKernelGGL((scp_ipm_kernel<3, 2, 0, 2>), dim3(N), dim3(2 * WAVE), 0, st, a, a.ws, a.disc); else hipLaunchKernelGGL((scp_ipm_kernel<3, 2, 0, 1>), dim3(N), dim3(WAVE), 0, st, a, a.ws, a.disc); }
         else if (ne == 3)
-            hipLaunchKernelGGL((scp_ipm_kernel<3, 2, 3>), dim3(N), dim3(WAVE), 0, st, a, a.ws, a.disc);
+            { if (two) hipLaunchKernelGGL((scp_ipm_kernel<3, 2, 3, 2>), dim3(N), dim3(2 * WAVE), 0, st, a, a.ws, a.disc); else hipLaunchKernelGGL((scp_ipm_kernel<3, 2, 3, 1>), dim3(N), dim3(WAVE), 0, st, a, a.ws, a.disc); }
         else
             return set_error(SCVX_EUNSUPPORTED, "scp game: unicycle needs theta_idx = 2");
     } else if (T->model_id == SCVX_MODEL_SINGLE_INTEGRATOR && T->n_x == 3 && T->n_u == 3) {
         if (ne == 0)
-            hipLaunchKernelGGL((scp_ipm_kernel<3, 3, 0>), dim3(N), dim3(WAVE), 0, st, a, a.ws, a.disc);
+            { if (two) hipLaunchKernelGGL((scp_ipm_kernel<3, 3, 0, 2>), dim3(N), dim3(2 * WAVE), 0, st, a, a.ws, a.disc); else hipLaunchKernelGGL((scp_ipm_kernel<3, 3, 0, 1>), dim3(N), dim3(WAVE), 0, st, a, a.ws, a.disc); }
         else if (ne == 3)
-            hipLaunchKernelGGL((scp_ipm_kernel<3, 3, 3>), dim3(N), dim3(WAVE), 0, st, a, a.ws, a.disc);
+            { if (two) hipLaunchKernelGGL((scp_ipm_kernel<3, 3, 3, 2>), dim3(N), dim3(2 * WAVE), 0, st, a, a.ws, a.disc); else hipLaunchKernelGGL((scp_ipm_kernel<3, 3, 3, 1>), dim3(N), dim3(WAVE), 0, st, a, a.ws, a.disc); }
         else
             return set_error(SCVX_EUNSUPPORTED, "scp game: single integrator has no heading (theta_idx = -1)");
     } else {

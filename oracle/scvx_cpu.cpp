@@ -962,6 +962,14 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out, const double*
             }
         pobj += cprox / osc;   // the proximal term's constant: the gap test is relative to the true objective
         if (std::getenv("SCVX_DEBUG")) std::fprintf(stderr, "it %d pres %.3e dres %.3e mu %.3e pobj %.6e\n", it, pres, dres, mu, pobj);
+        if (const char* dn = std::getenv("SCVX_DEBUG_NODE")) {   // diagnostics: one node's iterate and rows
+            const int t = std::atoi(dn);
+            const Node& N = ag.nd[t];
+            std::fprintf(stderr, "   node %d z:", t);
+            for (int j = 0; j < N.nv; ++j) std::fprintf(stderr, " %.4e", N.z[j]);
+            std::fprintf(stderr, "\n");
+            for (int r = 0; r < N.nr; ++r) std::fprintf(stderr, "     r %d s %.3e lam %.3e\n", r, N.s[r], N.lam[r]);
+        }
         if (!std::isfinite(pres + dres + mu)) { status = SCVX_STATUS_NUMERICAL; break; }
         const double pnorm = std::max(1.0, nb + nxv + nsl), dnorm = std::max(1.0 / osc, nq + nxv / osc + nzd);  // caller's units / osc
         if (pres <= tol * pnorm && dres <= tol * dnorm && gap * osc <= tol * std::max(1.0, std::fabs(pobj * osc))) {
