@@ -1716,6 +1716,8 @@ extern "C" size_t scvx_scp_workspace_bytes(const scvx_scp_template* T, int N) {
     return sizeof(double) * (size_t)N * (size_t)L.stride * (size_t)(T->K + 1);  // + the per-lane junk block
 }
 
+static int g_scp_waves = 0;  // scvx_scp_set_waves_per_agent: 0 automatic, 1 or 2 forced
+
 static int scp_launch(const scvx_scp_template* T, int N, const double* disc, const double* Xref, const double* Uref,
                       const double* sigma_ref, const double* tr, const double* x_init, const double* x_final,
                       const double* nbr_pos, const double* nbr_Y, const double* nbr_Lam, const double* X_prev,
@@ -1770,7 +1772,7 @@ static int scp_launch(const scvx_scp_template* T, int N, const double* disc, con
             simds = 4 * cus;
         if (simds <= 0) simds = 1024;
     }
-    const bool two = T->K > WAVE && 2LL * N <= simds;
+    const bool two = g_scp_waves == 2 || (g_scp_waves == 0 && T->K > WAVE && 2LL * N <= simds);
     if (T->model_id == SCVX_MODEL_UNICYCLE && T->n_x == 3 && T->n_u == 2) {
         if (T->has_soc) return set_error(SCVX_EUNSUPPORTED, "scp: SOC rows need n_u + 1 <= 4");
         if (ne == 0)
@@ -1790,6 +1792,12 @@ static int scp_launch(const scvx_scp_template* T, int N, const double* disc, con
         return set_error(SCVX_EUNSUPPORTED, "scp: model (unicycle n=3 m=2, single integrator n=3 m=3)");
     }
     return check_launch("scp_ipm_kernel");
+}
+
+extern "C" int scvx_scp_set_waves_per_agent(int waves) {
+    if (waves < 0 || waves > 2) return set_error(SCVX_EINVAL, "scp: waves per agent must be 0, 1 or 2");
+    g_scp_waves = waves;
+    return SCVX_OK;
 }
 
 extern "C" int scvx_scp_solve_batched(const scvx_scp_template* T, int N, const double* disc, const double* Xref,

@@ -310,6 +310,12 @@ int scvx_scp_solve_batched(const scvx_scp_template* tpl, int N, const double* di
  * N agents (depends on the game fields: the game kernel carries extra Riccati states). */
 size_t scvx_scp_workspace_bytes(const scvx_scp_template* tpl, int N);
 
+/* Waves per agent of the SCP kernels (scvx_scp_solve_batched / scvx_scp_game_solve_batched): 0 (default) =
+ * automatic -- two when K > 64 and the launch leaves SIMDs idle (2 N <= 4 x CUs), so the node phases of a
+ * K <= 128 agent run in one pass; 1 or 2 forces the mapping (parity tests of both paths).  Process-wide.
+ * Returns SCVX_OK, or SCVX_EINVAL for another value.  (No reference counterpart: a launch parameter.) */
+int scvx_scp_set_waves_per_agent(int waves);
+
 /* ------------------------------------------------------------------------------------------
  * Batched Nash best response: AgentBestResponse.setup/solve (SCvx/optimization/agent_best_response.py:
  * 35-113, si_agent_best_response.py:36-127) = the SCProblem above (without ADMM terms) plus the

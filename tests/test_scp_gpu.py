@@ -76,6 +76,38 @@ def test_scproblem_matches_reference_formulation(cuda, model, K):
         assert X.shape == (K, 3) and nu.shape == (K - 1, 3)
 
 
+@pytest.mark.parametrize("model,admm", [("unicycle", False), ("si", False), ("unicycle", True)])
+def test_one_and_two_waves_per_agent(cuda, model, admm):
+    """K = 100 > 64 nodes: the same agents through the one-wave mapping (node phases in two passes; what a
+    launch that fills every SIMD uses) and the two-wave mapping (scvx_scp_set_waves_per_agent; what a
+    single-agent launch uses).  Both at the dense oracle's optimal value (1e-7, feasibility 1e-7); their
+    reductions sum in different orders, so they agree to the stopping tolerance, not bit for bit."""
+    import torch
+    import scvx_hip
+    from oracle import scp_dense as sd
+    probs = instances(model, 100, 3, admm=admm, seed=5)
+    out = {}
+    try:
+        for w in (1, 2):
+            scvx_hip.check(scvx_hip.lib().scvx_scp_set_waves_per_agent(w), "scvx_scp_set_waves_per_agent")
+            out[w] = solve_gpu(probs, torch, cuda)
+    finally:
+        scvx_hip.lib().scvx_scp_set_waves_per_agent(0)
+    assert scvx_hip.lib().scvx_scp_set_waves_per_agent(3) != 0   # only 0, 1, 2
+    for a, p in enumerate(probs):
+        ref = sd.solve_scproblem(p, tol=1e-10)
+        objs = []
+        for w in (1, 2):
+            g = out[w]
+            assert g["status"][a] in (0, 1), (w, g["status"])
+            X, U, nu, sig = g["X"][a], g["U"][a], g["nu"][a], float(g["sigma"][a])
+            obj = sd.scp_objective(p, X, U, nu, sig)
+            assert abs(obj - ref["obj"]) <= 1e-7 * abs(ref["obj"]), (w, a, obj, ref["obj"])
+            assert sd.scp_violation(p, X, U, nu, sig) < 1e-7
+            objs.append(obj)
+        assert abs(objs[0] - objs[1]) <= 1e-7 * abs(ref["obj"])
+
+
 @pytest.mark.parametrize("model", ["unicycle", "si"])
 def test_agent_solver_admm_matches_reference_formulation(cuda, model):
     import torch
