@@ -411,9 +411,13 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
         for (int e = 0; e < n; ++e) dst[e] = wb.ld(vfb, FBB + (b0 + e) * 8);
     };
+    // (n = 12 classes: not held -- their 144-element blocks would occupy the register file and spill;
+    // the compiler then interleaves the loads with their uses instead)
     auto hold = [&](double* v, int n) __attribute__((always_inline)) {
+        if constexpr (NX <= 8) {
 #pragma unroll
-        for (int e = 0; e < n; ++e) asm volatile("" : "+v"(v[e]));
+            for (int e = 0; e < n; ++e) asm volatile("" : "+v"(v[e]));
+        }
     };
     auto pst = [&](int e, double v) __attribute__((always_inline)) { wb.st(vpk, PKB + e * 8, v); };
 
@@ -849,6 +853,51 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
         // Pi_0 -> persistent; LU with partial pivoting of M (lane 0, registers)
         for (int e = lane; e < NX * NX; e += WAVE) lds[V_PI0 + e] = lds[C::F_PIP + (e % NX) * NX + e / NX];
+        if constexpr (NX > 8) {
+            // n = 12 classes: the same LU column-parallel (lane j < NX owns column j of M; pivot column k
+            // broadcast by readlane) -- the lane-0 form holds NX x NX doubles in registers and spills.  Every
+            // element sees the same operations in the same order as the lane-0 form below.
+            if (fin) {
+                const int j = lane < NX ? lane : 0;
+                double col[NX];
+#pragma unroll
+                for (int i = 0; i < NX; ++i) col[i] = lds[V_M + i * NX + j];
+#pragma unroll
+                for (int k = 0; k < NX; ++k) {
+                    double ck[NX];
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) ck[i] = readlane_d(col[i], k);
+                    int p = k;
+                    double best = fabs(ck[k]);
+#pragma unroll
+                    for (int i = k + 1; i < NX; ++i) {
+                        const double v = fabs(ck[i]);
+                        if (v > best) { best = v; p = i; }
+                    }
+                    if (lane == 0) lds[V_PIV + k] = (double)p;
+#pragma unroll
+                    for (int i = k + 1; i < NX; ++i) {
+                        const double m = qp_mask(i, p);
+                        const double dlt = m * (col[i] - col[k]);
+                        col[k] += dlt;
+                        col[i] -= dlt;
+                    }
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) ck[i] = readlane_d(col[i], k);
+                    const double d = ck[k];
+                    if (lane == 0 && (d == 0.0 || d != d)) lds[V_FLAG] = 2.0;
+                    const double inv = d != 0.0 ? 1.0 / d : 0.0;
+#pragma unroll
+                    for (int i = k + 1; i < NX; ++i) {
+                        const double f = ck[i] * inv;
+                        col[i] = (j == k) ? f : ((j > k) ? col[i] - f * col[k] : col[i]);
+                    }
+                }
+                if (lane < NX)
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) lds[V_M + i * NX + j] = col[i];
+            }
+        } else {
         if (fin && lane == 0) {
             double Mr[NX * NX];
 #pragma unroll
@@ -886,6 +935,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             }
 #pragma unroll
             for (int e = 0; e < NX * NX; ++e) lds[V_M + e] = Mr[e];
+        }
         }
         wsync();
         return lds[V_FLAG] == 0.0;
