@@ -76,16 +76,18 @@ def test_scproblem_matches_reference_formulation(cuda, model, K):
         assert X.shape == (K, 3) and nu.shape == (K - 1, 3)
 
 
-@pytest.mark.parametrize("model,admm", [("unicycle", False), ("si", False), ("unicycle", True)])
-def test_one_and_two_waves_per_agent(cuda, model, admm):
-    """K = 100 > 64 nodes: the same agents through the one-wave mapping (node phases in two passes; what a
+@pytest.mark.parametrize("model,admm,K", [("unicycle", False, 100), ("si", False, 100), ("unicycle", True, 100),
+                                          ("unicycle", False, 200)])
+def test_one_and_two_waves_per_agent(cuda, model, admm, K):
+    """K > 64 nodes: the same agents through the one-wave mapping (node phases in two or more passes; what a
     launch that fills every SIMD uses) and the two-wave mapping (scvx_scp_set_waves_per_agent; what a
-    single-agent launch uses).  Both at the dense oracle's optimal value (1e-7, feasibility 1e-7); their
-    reductions sum in different orders, so they agree to the stopping tolerance, not bit for bit."""
+    single-agent launch uses; K = 200 takes two passes of 128 threads).  Both at the dense oracle's optimal
+    value (1e-7, feasibility 1e-7); their reductions sum in different orders, so they agree to the
+    stopping tolerance, not bit for bit."""
     import torch
     import scvx_hip
     from oracle import scp_dense as sd
-    probs = instances(model, 100, 3, admm=admm, seed=5)
+    probs = instances(model, K, 3 if K <= 100 else 2, admm=admm, seed=5)
     out = {}
     try:
         for w in (1, 2):
