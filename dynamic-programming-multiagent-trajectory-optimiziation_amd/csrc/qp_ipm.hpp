@@ -315,6 +315,48 @@ __device__ __forceinline__ void qp_phase(double* lds, const QPRep (&d)[NREP], do
     }
 }
 
+// Compact repetition (n = 12 classes): the base / accumulate flags packed in F (bits 0-1: base kind 0 none,
+// 1 every stage, 2 last stage; bit 2: accumulating output) instead of three doubles, and the accumulating
+// outputs keep their LDS target in O (written every stage, overwritten by the register sum after the
+// sweep; nothing reads V_M / V_XE during it).  20 repetitions x 6 instead of 11 registers at NX = 12.
+struct QPRepC {
+    int L, R, B, O, G, F;
+};
+__device__ __forceinline__ QPRepC qp_decode_c(const int (&d)[4], int one, int lsink, int jnk) {
+    QPRepC q;
+    q.L = d[0] & 0x7FFF;
+    q.R = d[1] & 0x7FFF;
+    const int bk = d[3] >> 16;
+    q.B = bk ? (d[3] & 0x7FFF) : one;
+    const int O = d[2];
+    const bool on = O >= 0, acc = on && ((O >> 15) & 1);
+    q.O = on ? (O & 0x7FFF) : lsink;
+    const int g = on ? (O >> 17) - 1 : -1;
+    q.G = (g >= 0 ? g : jnk) * 8;
+    q.F = bk | (acc ? 4 : 0);
+    return q;
+}
+// as qp_phase; outputs [ALO, AHI) of the phase may accumulate (only those repetitions keep a register sum)
+template <int KK, int NREP, int ALO, int AHI>
+__device__ __forceinline__ void qp_phase_c(double* lds, const QPRepC (&d)[NREP], double blast, const QPBuf& wb,
+                                           int fbo, double (&areg)[NREP]) {
+    double val[NREP];
+#pragma unroll
+    for (int r = 0; r < NREP; ++r) {
+        const int bk = d[r].F & 3;
+        const double bm = (bk == 1 ? 1.0 : 0.0) + blast * (bk == 2 ? 1.0 : 0.0);
+        val[r] = fma(lds[d[r].B], bm, qp_dot<KK>(lds, d[r].L, d[r].R));
+    }
+#pragma unroll
+    for (int r = 0; r < NREP; ++r) {
+        lds[d[r].O] = val[r];
+        if constexpr (true) {
+            if (WAVE * r < AHI && WAVE * r + WAVE > ALO) areg[r] = fma((d[r].F & 4) ? 1.0 : 0.0, val[r], areg[r]);
+        }
+        wb.st(d[r].G, fbo, val[r]);
+    }
+}
+
 template <class C>
 __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     constexpr int NX = C::NX, NU = C::NU, NZ = C::NZ, NQ = C::NQ, NR = C::NR, NG = C::NG, NS = C::NS,
@@ -615,7 +657,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             }
         }
         // decoded once per sweep; accumulating outputs (xe, M) are summed in registers
-        QPRep q1[R1], q2[R2], q4[R4];
+        constexpr bool CMP = NX > 8;   // compact repetitions (QPRepC) for the n = 12 classes
+        using Rep = typename std::conditional<CMP, QPRepC, QPRep>::type;
+        Rep q1[R1], q2[R2], q4[R4];
         double a1[R1], a2[R2], a4[R4];
         // virtual control: the M contributions -Pi'' G^-1 Pi' of every stage (registers, like a4)
         constexpr int R0 = (NX * NX + WAVE - 1) / WAVE;
@@ -623,11 +667,23 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
         for (int r = 0; r < R0; ++r) amv[r] = 0.0;
 #pragma unroll
-        for (int r = 0; r < R1; ++r) { q1[r] = qp_decode(d1[r], V_ONE, C::F_SINK, C::B_JNK); a1[r] = 0.0; }
+        for (int r = 0; r < R1; ++r) {
+            if constexpr (CMP) q1[r] = qp_decode_c(d1[r], V_ONE, C::F_SINK, C::B_JNK);
+            else q1[r] = qp_decode(d1[r], V_ONE, C::F_SINK, C::B_JNK);
+            a1[r] = 0.0;
+        }
 #pragma unroll
-        for (int r = 0; r < R2; ++r) { q2[r] = qp_decode(d2[r], V_ONE, C::F_SINK, C::B_JNK); a2[r] = 0.0; }
+        for (int r = 0; r < R2; ++r) {
+            if constexpr (CMP) q2[r] = qp_decode_c(d2[r], V_ONE, C::F_SINK, C::B_JNK);
+            else q2[r] = qp_decode(d2[r], V_ONE, C::F_SINK, C::B_JNK);
+            a2[r] = 0.0;
+        }
 #pragma unroll
-        for (int r = 0; r < R4; ++r) { q4[r] = qp_decode(d4[r], V_ONE, C::F_SINK, C::B_JNK); a4[r] = 0.0; }
+        for (int r = 0; r < R4; ++r) {
+            if constexpr (CMP) q4[r] = qp_decode_c(d4[r], V_ONE, C::F_SINK, C::B_JNK);
+            else q4[r] = qp_decode(d4[r], V_ONE, C::F_SINK, C::B_JNK);
+            a4[r] = 0.0;
+        }
         for (int e = lane; e < NX * NX; e += WAVE) { lds[C::F_PP + e] = 0.0; lds[C::F_PIP + e] = 0.0; lds[V_M + e] = 0.0; }
         if (lane < NX) lds[V_XE + lane] = 0.0;
         if (lane == 0) lds[V_FLAG] = 0.0;
@@ -725,10 +781,12 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 wsync();
             }
             // ---- phase 1: T1 = P'A, T2 = P'Bt, W1 = A'Pi', W2 = Bt'Pi', u = P'e, xe += Pi''e
-            qp_phase<NX, R1>(lds, q1, blast, wb, fbo, a1);
+            if constexpr (CMP) qp_phase_c<NX, R1, E1 - NX, E1>(lds, q1, blast, wb, fbo, a1);
+            else qp_phase<NX, R1>(lds, q1, blast, wb, fbo, a1);
             wsync();
             // ---- phase 2: Qh = Q + A'T1, Sh = S' + Bt'T1, Rh = R + Bt'T2
-            qp_phase<NX, R2>(lds, q2, blast, wb, fbo, a2);
+            if constexpr (CMP) qp_phase_c<NX, R2, 0, 0>(lds, q2, blast, wb, fbo, a2);
+            else qp_phase<NX, R2>(lds, q2, blast, wb, fbo, a2);
             wsync();
             // ---- phase 3: Rh = L D L' in registers (every lane); [K | kappa] = -Rh^-1 [Sh | W2]
             {
@@ -808,7 +866,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             }
             wsync();
             // ---- phase 4: P = Qh + Sh'K, Pi = W1 + Sh'kappa, M += W2'kappa, Acl = A + Bt K
-            qp_phase<NU, R4>(lds, q4, blast, wb, fbo, a4);
+            if constexpr (CMP) qp_phase_c<NU, R4, 2 * NX * NX, 3 * NX * NX>(lds, q4, blast, wb, fbo, a4);
+            else qp_phase<NU, R4>(lds, q4, blast, wb, fbo, a4);
             if (ts > 0) pf_store(ts - 1, cb);
             wsync();
             if constexpr (C::NV > 0) {
@@ -836,12 +895,21 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
         if (bad) lds[V_FLAG] = 1.0;  // any lane (all agree)
         // the register-accumulated outputs (xe, M) to their LDS homes
+        if constexpr (CMP) {
 #pragma unroll
-        for (int r = 0; r < R1; ++r)
-            if (d1[r][2] >= 0 && ((d1[r][2] >> 15) & 1)) lds[d1[r][2] & 0x7FFF] = a1[r];
+            for (int r = 0; r < R1; ++r)
+                if (WAVE * r < E1 && WAVE * r + WAVE > E1 - NX && (q1[r].F & 4)) lds[q1[r].O] = a1[r];
 #pragma unroll
-        for (int r = 0; r < R4; ++r)
-            if (d4[r][2] >= 0 && ((d4[r][2] >> 15) & 1)) lds[d4[r][2] & 0x7FFF] = a4[r];
+            for (int r = 0; r < R4; ++r)
+                if (WAVE * r < 3 * NX * NX && WAVE * r + WAVE > 2 * NX * NX && (q4[r].F & 4)) lds[q4[r].O] = a4[r];
+        } else {
+#pragma unroll
+            for (int r = 0; r < R1; ++r)
+                if (d1[r][2] >= 0 && ((d1[r][2] >> 15) & 1)) lds[d1[r][2] & 0x7FFF] = a1[r];
+#pragma unroll
+            for (int r = 0; r < R4; ++r)
+                if (d4[r][2] >= 0 && ((d4[r][2] >> 15) & 1)) lds[d4[r][2] & 0x7FFF] = a4[r];
+        }
         wsync();
         if constexpr (C::NV > 0) {
 #pragma unroll
