@@ -362,6 +362,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     constexpr int NX = C::NX, NU = C::NU, NZ = C::NZ, NQ = C::NQ, NR = C::NR, NG = C::NG, NS = C::NS,
                   NO = C::NO, NC = C::NC, NB = C::NB, PKT = C::PKT, NV = C::NV, NVA = C::NVA;
     constexpr int NGA = NG > 0 ? NG : 1, NSA = NS > 0 ? NS : 1, NBA = NB > 0 ? NB : 1;
+    // solve-chain prefetch depth: two stages for the n = 12 classes (4 x 12 held doubles would spill)
+    constexpr int CPF = NX > 8 ? 2 : QP_CPF;
     extern __shared__ double lds[];
     const scvx_qp_template& T = a.T;
     const int K = T.K, lane = threadIdx.x, t = lane;
@@ -1081,25 +1083,25 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             lds[V_CH + (K - 1) * NX + lane] = p;
             // QP_CPF register buffers: operands loaded QP_CPF stages ahead (a global load under
             // full-chip load takes ~2,000 cycles; 8 stages measured no faster than 4 and spilled more)
-            double ab[QP_CPF][NX], gb[QP_CPF];
+            double ab[CPF][NX], gb[CPF];
 #pragma unroll
-            for (int b = 0; b < QP_CPF; ++b) ldA(K - 2 - b, ab[b], gb[b]);
+            for (int b = 0; b < CPF; ++b) ldA(K - 2 - b, ab[b], gb[b]);
             int ts = K - 2;
             auto step = [&](double* a, double& g) __attribute__((always_inline)) {
                 p = chain(p, a, g);
                 lds[V_CH + ts * NX + lane] = p;
-                ldA(ts - QP_CPF, a, g);
+                ldA(ts - CPF, a, g);
                 --ts;
             };
             // groups of QP_CPF steps with no exit inside the loop body (a mid-body exit makes the
             // compiler's vmcnt tracking fall back to vmcnt(0) and drain the prefetches), then the
             // remaining steps continuing the buffer rotation
-            while (ts >= QP_CPF - 1) {
+            while (ts >= CPF - 1) {
 #pragma unroll
-                for (int b = 0; b < QP_CPF; ++b) step(ab[b], gb[b]);
+                for (int b = 0; b < CPF; ++b) step(ab[b], gb[b]);
             }
 #pragma unroll
-            for (int b = 0; b < QP_CPF - 1; ++b)
+            for (int b = 0; b < CPF - 1; ++b)
                 if (ts >= 0) step(ab[b], gb[b]);
         }
         wsync();
@@ -1288,22 +1290,22 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             };
             double x = lds[V_XI0 + lane];
             lds[V_CH + lane] = x;
-            double ab[QP_CPF][NX], fb[QP_CPF];
+            double ab[CPF][NX], fb[CPF];
 #pragma unroll
-            for (int b = 0; b < QP_CPF; ++b) ldA(b, ab[b], fb[b]);
+            for (int b = 0; b < CPF; ++b) ldA(b, ab[b], fb[b]);
             int ts = 0;
             auto step = [&](double* a, double& f) __attribute__((always_inline)) {
                 x = chain(x, a, f);
                 lds[V_CH + (ts + 1) * NX + lane] = x;
-                ldA(ts + QP_CPF, a, f);
+                ldA(ts + CPF, a, f);
                 ++ts;
             };
-            while (ts <= K - 1 - QP_CPF) {  // QP_CPF steps per trip, no exit inside (see the backward chain)
+            while (ts <= K - 1 - CPF) {  // CPF steps per trip, no exit inside (see the backward chain)
 #pragma unroll
-                for (int b = 0; b < QP_CPF; ++b) step(ab[b], fb[b]);
+                for (int b = 0; b < CPF; ++b) step(ab[b], fb[b]);
             }
 #pragma unroll
-            for (int b = 0; b < QP_CPF - 1; ++b)
+            for (int b = 0; b < CPF - 1; ++b)
                 if (ts < K - 1) step(ab[b], fb[b]);
         }
         wsync();
