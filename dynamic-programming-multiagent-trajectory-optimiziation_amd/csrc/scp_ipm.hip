@@ -381,6 +381,7 @@ __global__ __launch_bounds__(64 * NW) void scp_ipm_kernel(SCPArgs a, double* __r
 
     __shared__ double sP[NXA * NXA], sPAB[NXA * (NXA + NUA)], sQxx[NXA * NXA], sQuxC[NUA * NXA],
         sQuu[NUA * NUA], sKC[NUA * NXA], sXi[NXA], sMisc[32];
+    __shared__ double sPv[NXA], sV[NXA], sQ[NZ], sU[NUA], sXw[2][NXA];  // sweep-form LQ solve (NW = 1)
     // sMisc: 0..NX-1 r_init, 8..8+NX-1 y0+, 16.. scalars
     auto pinned = [&](int t, int i) -> bool {  // i: z index
         if (i >= ZU && i < ZN) return (t == 0 && T.pin_u_first) || (t == K - 1 && T.pin_u_last);
@@ -707,6 +708,22 @@ __global__ __launch_bounds__(64 * NW) void scp_ipm_kernel(SCPArgs a, double* __r
     __shared__ double sRing[2][PF * WAVE];
     __shared__ double sSink[WAVE];  // LDS stores of lanes without an output element
     double pf[PF];
+    // segments: {node offset (0 or +1), node-block offset, length} -> per-lane element map (sweep-form LQ)
+    auto seg_map = [&](const int (&dn)[7], const int (&off)[7], const int (&len)[7], int nseg, int (&fo)[PF],
+                       int (&fd)[PF]) {
+        #pragma unroll
+        for (int c = 0; c < PF; ++c) {
+            const int e = lane + c * WAVE;
+            int o = off[0], d = dn[0], acc = 0;
+            #pragma unroll
+            for (int sg = 0; sg < 7; ++sg) {
+                if (sg < nseg && e >= acc && e < acc + len[sg]) { o = off[sg] + (e - acc); d = dn[sg]; }
+                if (sg < nseg) acc += len[sg];
+            }
+            fo[c] = o;
+            fd[c] = d;
+        }
+    };
     auto gather = [&](int t, const int (&fo)[PF], const int (&fd)[PF]) {
         #pragma unroll
         for (int c = 0; c < PF; ++c) {
@@ -858,6 +875,7 @@ __global__ __launch_bounds__(64 * NW) void scp_ipm_kernel(SCPArgs a, double* __r
       }
         __syncthreads();
         // closed-loop Acl_t = At_t + Bt_t K_t (row-major), the LQ chains' matrices: lane-parallel over nodes
+        if constexpr (NW > 1)
         for (int t = tid; t < K - 1; t += NT) {
             double* B = nb(t);
             double Kt[NUA * NXA];
@@ -875,6 +893,158 @@ __global__ __launch_bounds__(64 * NW) void scp_ipm_kernel(SCPArgs a, double* __r
                     for (int k = 0; k < NUA; ++k) v += bi[k] * Kt[k * NXA + j];
                     B[Ly.o_Acl + i * NXA + j] = v;
                 }
+            }
+        }
+        __syncthreads();
+    };
+
+    // ------------------------------------------------------------------ LQ solve, sweep form (one wave per agent)
+    // The element-parallel Riccati sweeps of rounds 1-2 (the recursion below stage by stage, the stage
+    // operands gathered a stage ahead into an LDS ring): used when the launch fills every SIMD (NW = 1),
+    // where the closed-loop form's lane-parallel passes (P, Acl and K of every node re-read under
+    // full-chip contention) measured slower (batched game launch 61.9 vs 70.9 ms).
+    // In: o_f (per node), o_rp (t < K-1), sMisc[0..NX) = r_init.  Out: o_dz, o_yp (costates y+),
+    // sMisc[8..8+NX) = y0+.
+    auto lqsolve_sweep = [&]() __attribute__((always_inline)) {
+        // backward: v = P_{t+1} rp_t + p_{t+1}; qx = fx + At'v; qu = fu + Bt'v; k = -Quu^-1 qu; p = qx + K'qu
+        constexpr int B_PR = 0, B_RP = B_PR + NXA * NXA, B_F = B_RP + NXA, B_AT = B_F + NZ, B_BT = B_AT + NXA * NXA,
+                      B_LD = B_BT + NXA * NUA, B_K = B_LD + NUA * NUA;
+        {
+            const int dn[7] = {1, 0, 0, 0, 0, 0, 0};
+            const int off[7] = {Ly.o_Pr, Ly.o_rp, Ly.o_f, Ly.o_At, Ly.o_Bt, Ly.o_LD, Ly.o_K};
+            const int len[7] = {NXA * NXA, NXA, NZ, NXA * NXA, NXA * NUA, NUA * NUA, NUA * NXA};
+            int fo[PF], fd[PF];
+            seg_map(dn, off, len, 7, fo, fd);
+            gather(K - 1, fo, fd);
+            park(0);
+            wsync();
+            for (int t = K - 1; t >= 0; --t) {
+                const int slot = (K - 1 - t) & 1;
+                gather(t - 1, fo, fd);
+                const double* pk = sRing[slot];
+                const bool dyn = t < K - 1;
+                if (lane < NXA) {
+                    double v = 0.0;
+                    if (dyn) {
+                        v = sPv[lane];
+                        for (int k = 0; k < NXA; ++k) v += pk[B_PR + lane * NXA + k] * pk[B_RP + k];
+                    }
+                    sV[lane] = v;
+                }
+                wsync();
+                if (lane < NZ) {
+                    double v = pk[B_F + lane];
+                    if (dyn) {
+                        if (lane < NXA)
+                            for (int k = 0; k < NXA; ++k) v += pk[B_AT + k * NXA + lane] * sV[k];
+                        else
+                            for (int k = 0; k < NXA; ++k) v += pk[B_BT + k * NUA + lane - NXA] * sV[k];
+                    }
+                    if (pinned(t, lane)) v = 0.0;
+                    sQ[lane] = v;
+                }
+                wsync();
+                {
+                    double Lm[NUA * NUA], x[NUA];
+                    #pragma unroll
+                    for (int e = 0; e < NUA * NUA; ++e) Lm[e] = pk[B_LD + e];
+                    #pragma unroll
+                    for (int i = 0; i < NUA; ++i) x[i] = -sQ[NXA + i];
+                    ldl_solve<NUA>(Lm, NUA, x);
+                    // (select x[lane] without dynamic register indexing)
+                    double xv = 0.0;
+                    #pragma unroll
+                    for (int i = 0; i < NUA; ++i) xv = (i == lane) ? x[i] : xv;
+                    *(lane < NUA ? nb(t) + Ly.o_kv + lane : jnk) = xv;
+                }
+                double pn;
+                {
+                    const int li = lane < NXA ? lane : 0;
+                    pn = sQ[li];
+                    for (int k = 0; k < NUA; ++k) pn += pk[B_K + k * NXA + li] * sQ[NXA + k];
+                    *(lane < NXA ? nb(t) + Ly.o_pv + lane : jnk) = pn;
+                }
+                wsync();
+                if (lane < NXA) sPv[lane] = pn;
+                park(slot ^ 1);
+                wsync();
+            }
+        }
+        __syncthreads();
+        // stage 0: x part fixed (-r_init), g part free: P_gg dg = -(p_g + P_gx dx)
+        {
+            const double* B0 = nb(0);
+            double dx[NX];
+            #pragma unroll
+            for (int i = 0; i < NX; ++i) dx[i] = -sMisc[i];
+            double Lm[SCP_NG * SCP_NG], g[SCP_NG];
+            for (int i = 0; i < SCP_NG; ++i) {
+                double v = B0[Ly.o_pv + NX + i];
+                for (int k = 0; k < NX; ++k) v += B0[Ly.o_Pr + (NX + i) * NXA + k] * dx[k];
+                g[i] = -v;
+                for (int j = 0; j < SCP_NG; ++j) Lm[i * SCP_NG + j] = B0[Ly.o_Pr + (NX + i) * NXA + NX + j];
+            }
+            ldl_factor<SCP_NG>(Lm, SCP_NG);
+            ldl_solve<SCP_NG>(Lm, SCP_NG, g);
+            #pragma unroll
+            for (int i = 0; i < NX; ++i)
+                if (lane == i) sXw[0][lane] = dx[i];
+            for (int i = 0; i < SCP_NG; ++i)
+                if (lane == NX + i) sXw[0][lane] = g[i];
+            if (lane >= E0 && lane < NXA) sXw[0][lane] = 0.0;  // u~_0, th~_0: no predecessor, no cost
+            __syncthreads();
+            if (lane < NX) {
+                double v = B0[Ly.o_pv + lane];
+                for (int k = 0; k < NXA; ++k) v += B0[Ly.o_Pr + lane * NXA + k] * sXw[0][k];
+                sMisc[8 + lane] = v;
+            }
+        }
+        __syncthreads();
+        // forward: u = kv + K xi; xi+ = rp + At xi + Bt u; y+ = p_{t+1} + P_{t+1} xi+
+        {
+            constexpr int W_KV = 0, W_K = W_KV + NUA, W_RP = W_K + NUA * NXA, W_AT = W_RP + NXA,
+                          W_BT = W_AT + NXA * NXA, W_PV1 = W_BT + NXA * NUA, W_PR1 = W_PV1 + NXA;
+            const int dn[7] = {0, 0, 0, 0, 0, 1, 1};
+            const int off[7] = {Ly.o_kv, Ly.o_K, Ly.o_rp, Ly.o_At, Ly.o_Bt, Ly.o_pv, Ly.o_Pr};
+            const int len[7] = {NUA, NUA * NXA, NXA, NXA * NXA, NXA * NUA, NXA, NXA * NXA};
+            int fo[PF], fd[PF];
+            seg_map(dn, off, len, 7, fo, fd);
+            gather(0, fo, fd);
+            park(0);
+            wsync();
+            int cur = 0;
+            for (int t = 0; t < K; ++t) {
+                const int slot = t & 1;
+                gather(t + 1, fo, fd);
+                const double* pk = sRing[slot];
+                double* B = nb(t);
+                {
+                    const int lu = lane < NUA ? lane : 0;
+                    double v = pk[W_KV + lu];
+                    for (int k = 0; k < NXA; ++k) v += pk[W_K + lu * NXA + k] * sXw[cur][k];
+                    if (lane < NUA) sU[lane] = v;
+                    *(lane < NUA ? B + Ly.o_dz + NXA + lane : jnk) = v;
+                }
+                *(lane < NXA ? B + Ly.o_dz + lane : jnk) = sXw[cur][lane < NXA ? lane : 0];
+                wsync();
+                if (t < K - 1) {
+                    if (lane < NXA) {
+                        double v = pk[W_RP + lane];
+                        for (int k = 0; k < NXA; ++k) v += pk[W_AT + lane * NXA + k] * sXw[cur][k];
+                        for (int k = 0; k < NUA; ++k) v += pk[W_BT + lane * NUA + k] * sU[k];
+                        sXw[cur ^ 1][lane] = v;
+                    }
+                    wsync();
+                    cur ^= 1;
+                    {
+                        const int li = lane < NXA ? lane : 0;
+                        double v = pk[W_PV1 + li];
+                        for (int k = 0; k < NXA; ++k) v += pk[W_PR1 + li * NXA + k] * sXw[cur][k];
+                        *(lane < NXA ? B + Ly.o_yp + lane : jnk) = v;
+                    }
+                }
+                park(slot ^ 1);
+                wsync();
             }
         }
         __syncthreads();
@@ -1148,7 +1318,7 @@ __global__ __launch_bounds__(64 * NW) void scp_ipm_kernel(SCPArgs a, double* __r
     if (tid < NX) sMisc[tid] = -xinit[tid];
     __syncthreads();
     factor();
-    lqsolve();
+    if constexpr (NW == 1) lqsolve_sweep(); else lqsolve();
     double mins = INFINITY, minl = INFINITY;
     for (int t = tid; t < K; t += NT) {
         double* B = nb(t);
@@ -1472,7 +1642,7 @@ __global__ __launch_bounds__(64 * NW) void scp_ipm_kernel(SCPArgs a, double* __r
             }
             __syncthreads();
             SCP_TR(3)
-            lqsolve();
+            if constexpr (NW == 1) lqsolve_sweep(); else lqsolve();
             SCP_TR(4)
             // recover slack steps, step length
             double amax = INFINITY;
