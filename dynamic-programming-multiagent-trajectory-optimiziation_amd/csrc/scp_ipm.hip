@@ -16,12 +16,14 @@
 // Riccati initial state with g_0 free.  Soft rows (obstacles, ADMM collision rows) keep their slack,
 // eliminated per row.  Every cost term is divided by an objective scale cs so the duals are O(1).
 //
-// Mapping: one agent per 64-lane workgroup.  Node phases are lane-parallel (node t on lane t % 64);
-// the Riccati factor and the two solve sweeps are sequential over nodes and element-parallel over
-// lanes, with the stage matrices in LDS.  Per-node data (rows in z coordinates, iterates, scaling,
-// factor outputs) lives in an agent-private workspace block per node.  Problems are small (K <= 256,
-// |z| <= 13): this kernel targets the reference's single-agent SCVXSolver / few-agent ADMM use, not
-// the batched headline path (csrc/qp_ipm.hpp).
+// Mapping: one agent per workgroup of NW waves (NW = 2 when K > 64 and the launch leaves SIMDs idle, e.g.
+// a single-agent SCVXSolver or Nash call; 1 otherwise).  Node phases are parallel over the nodes (thread
+// tid: nodes tid, tid + 64 NW, ...); the Riccati factor sweep is sequential over nodes and
+// element-parallel over wave 0's lanes, with the stage matrices in LDS.  The LQ solve is the same sweep
+// form for NW = 1 and the closed-loop form (two NXA-vector chains, the rest lane-parallel) for NW = 2.
+// Per-node data (rows in z coordinates, iterates, scaling, factor outputs) lives in an agent-private
+// workspace block per node.  Problems are small (K <= 256, |z| <= 16): this kernel serves the
+// reference's SCVXSolver / ADMM / Nash subproblems, not the batched headline path (csrc/qp_ipm.hpp).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
