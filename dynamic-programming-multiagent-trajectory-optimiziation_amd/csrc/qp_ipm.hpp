@@ -693,7 +693,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         // packets stream through one LDS slot (a stage's packet is overwritten by the next one after its
         // last read), loads issued 3 stages ahead (register buffers pf[0..2], so the stage loop is
         // unrolled by 3 to keep their indices static)
-        double pf[3][PFN];
+        // prefetch distance: 3 stages; 2 for the n = 12 classes (9 doubles per buffer, register pressure)
+        constexpr int FPD = NX > 8 ? 2 : 3;
+        double pf[FPD][PFN];
         // lane's global packet element per prefetch slot (structural zeros read past the end: 0)
         int pfo[PFN];
 #pragma unroll
@@ -713,11 +715,18 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 lds[e < PKT ? C::F_RING + e : C::F_SINK] = b[k];
             }
         };
-        pf_load(K - 1, pf[0]);
-        pf_load(K - 2, pf[1]);
-        pf_load(K - 3, pf[2]);
-        pf_store(K - 1, pf[0]);
-        pf_load(K - 4, pf[0]);
+        if constexpr (FPD == 3) {
+            pf_load(K - 1, pf[0]);
+            pf_load(K - 2, pf[1]);
+            pf_load(K - 3, pf[2]);
+            pf_store(K - 1, pf[0]);
+            pf_load(K - 4, pf[0]);
+        } else {
+            pf_load(K - 1, pf[0]);
+            pf_load(K - 2, pf[1]);
+            pf_store(K - 1, pf[0]);
+            pf_load(K - 3, pf[0]);
+        }
         wsync();
         bool bad = false;
         // one stage; buffer `nb` receives stage ts-3 (issued now), buffer `cb` holds stage ts-1
@@ -725,7 +734,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             const bool last = ts == K - 1;
             const double blast = last ? 1.0 : 0.0;
             const int fbo = FBB + ts * C::FBS * 8;  // byte offset of this stage's output block (uniform)
-            pf_load(ts - 3, nb);  // unconditional: stage K-1 re-issues K-4, ts-3 < 0 reads zeros
+            pf_load(ts - FPD, nb);  // unconditional: stage K-1 re-issues K-1-FPD, ts-FPD < 0 reads zeros
             if constexpr (C::NV > 0) {
                 // ---- phase 0 (virtual control nu_ts): G = diag(D) + P', then [G^-1 Pi' | G^-1 | G^-1 P'] by
                 // Gauss-Jordan without pivoting (G is SPD): lane c < 4 NX owns column c of [G | Pi' | I | P'];
@@ -885,15 +894,26 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         };
         // stage K-1's packet is in LDS, K-2 in pf[1], K-3 in pf[2], K-4 in pf[0]
         int ts = K - 1;
-        stage(ts, pf[0], pf[1]);  // (its load of K-4 went out before the loop)
-        --ts;
-        while (ts >= 0) {
-            stage(ts, pf[1], pf[2]);
-            if (--ts < 0) break;
-            stage(ts, pf[2], pf[0]);
-            if (--ts < 0) break;
+        if constexpr (FPD == 3) {
+            stage(ts, pf[0], pf[1]);  // (its load of K-4 went out before the loop)
+            --ts;
+            while (ts >= 0) {
+                stage(ts, pf[1], pf[2]);
+                if (--ts < 0) break;
+                stage(ts, pf[2], pf[0]);
+                if (--ts < 0) break;
+                stage(ts, pf[0], pf[1]);
+                --ts;
+            }
+        } else {  // LDS: K-1, pf[1]: K-2, pf[0]: K-3 (in flight)
             stage(ts, pf[0], pf[1]);
             --ts;
+            while (ts >= 0) {
+                stage(ts, pf[1], pf[0]);
+                if (--ts < 0) break;
+                stage(ts, pf[0], pf[1]);
+                --ts;
+            }
         }
         if (bad) lds[V_FLAG] = 1.0;  // any lane (all agree)
         // the register-accumulated outputs (xe, M) to their LDS homes
