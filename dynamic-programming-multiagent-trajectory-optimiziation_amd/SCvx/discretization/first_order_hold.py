@@ -89,6 +89,34 @@ class FirstOrderHold:
             dst[...] = src.cpu().numpy()
         return self.A_bar, self.B_bar, self.C_bar, self.S_bar, self.z_bar
 
+    # ---- caller-side batching (no reference counterpart; the reference integrates one agent per call)
+    def calculate_discretization_device(self, Xd, Ud, sd):
+        """Device-resident batch: Xd (M, K, n_x), Ud (M, K, n_u), sd (M,) float64 tensors on this object's
+        device -> the packed per-interval matrices (M, K-1, n_x (n_x + 2 n_u + 2)) as a device tensor, one
+        launch and no host transfer (unpack with scvx_hip.unpack_disc)."""
+        if isinstance(self._name, str):
+            return scvx_hip.foh_batched(self._name, Xd, Ud, sd, nsub=self._nsub, params=self._params)
+        return self._name.foh(Xd, Ud, sd, nsub=self._nsub, params=self._params)
+
+    def calculate_discretization_batched(self, Xs, Us, sigmas):
+        """calculate_discretization for M agents in one launch and one host round trip each way (a loop of
+        M single-agent calls pays M of both).  Xs: M arrays (n_x, K), Us: M arrays (n_u, K), sigmas: M
+        scalars.  Returns a list of M (A_bar, B_bar, C_bar, S_bar, z_bar) tuples of NEW arrays (the
+        single-agent method's output buffers are not touched)."""
+        import torch
+        M = len(Xs)
+        if len(Us) != M or len(sigmas) != M:
+            raise ValueError("calculate_discretization_batched: Xs, Us and sigmas must have the same length")
+        if M == 0:
+            return []
+        Xd = torch.as_tensor(np.ascontiguousarray(np.stack([np.asarray(x, float).T for x in Xs])), device=self._device)
+        Ud = torch.as_tensor(np.ascontiguousarray(np.stack([np.asarray(u, float).T for u in Us])), device=self._device)
+        sd = torch.as_tensor(np.asarray(sigmas, float).reshape(M), device=self._device)
+        disc = self.calculate_discretization_device(Xd, Ud, sd)
+        unpack = scvx_hip.unpack_disc if isinstance(self._name, str) else None
+        outs = [o.cpu().numpy() for o in (unpack(disc, self._name) if unpack else self._name.unpack_disc(disc))]
+        return [tuple(np.array(o[a]) for o in outs) for a in range(M)]
+
     def integrate_nonlinear_piecewise(self, X_lin, U, sigma):
         Xd, Ud, sd = self._to_dev(X_lin, U, sigma)
         out = self._roll(Xd, Ud, sd, True)

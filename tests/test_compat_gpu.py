@@ -25,6 +25,39 @@ def _model(name):
             "quad": QuadrotorModel}[name]()
 
 
+@pytest.mark.parametrize("name", ["unicycle", "quad"])
+def test_first_order_hold_batched_helper(cuda, name):
+    """calculate_discretization_batched (one launch for M agents) returns exactly what M single-agent
+    calculate_discretization calls return (the kernel integrates every agent independently), as new
+    arrays, and leaves the object's own output buffers alone; the device-resident form matches too."""
+    import torch
+    from SCvx.discretization.first_order_hold import FirstOrderHold
+    import scvx_hip
+    model = _model(name)
+    K, M = 30, 5
+    rng = np.random.default_rng(11)
+    Xs = [0.1 * rng.standard_normal((model.n_x, K)) for _ in range(M)]
+    Us = [0.1 * rng.standard_normal((model.n_u, K)) for _ in range(M)]
+    sigmas = list(1.0 + rng.uniform(0, 2, M))
+    foh = FirstOrderHold(model, K)
+    single = [tuple(o.copy() for o in foh.calculate_discretization(X, U, s)) for X, U, s in zip(Xs, Us, sigmas)]
+    keep = foh.A_bar.copy()
+    batched = foh.calculate_discretization_batched(Xs, Us, sigmas)
+    assert len(batched) == M
+    for a in range(M):
+        for got, want in zip(batched[a], single[a]):
+            assert got.shape == want.shape
+            np.testing.assert_array_equal(got, want)
+        assert batched[a][0] is not foh.A_bar
+    np.testing.assert_array_equal(foh.A_bar, keep)
+    Xd = torch.tensor(np.ascontiguousarray(np.stack([x.T for x in Xs])), device=cuda)
+    Ud = torch.tensor(np.ascontiguousarray(np.stack([u.T for u in Us])), device=cuda)
+    disc = foh.calculate_discretization_device(Xd, Ud, torch.tensor(sigmas, dtype=torch.float64, device=cuda))
+    A_dev = scvx_hip.unpack_disc(disc, name)[0].cpu().numpy()
+    np.testing.assert_array_equal(A_dev[2], single[2][0])
+    assert foh.calculate_discretization_batched([], [], []) == []
+
+
 @pytest.mark.parametrize("path", GOLD, ids=[os.path.basename(p) for p in GOLD])
 def test_first_order_hold_dropin(cuda, path):
     from SCvx.discretization.first_order_hold import FirstOrderHold
