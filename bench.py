@@ -157,45 +157,67 @@ def host_info():
     return info
 
 
-def cpu_baseline(sc, n_sample, threads, min_seconds=8.0, tol=1e-9):
-    """Time the CPU restatement (oracle) on n_sample agents: FOH + QP for one SCvx iteration,
-    repeated until about min_seconds of wall time (a bounded sample of the same workload).
-    Returns SCvx iterations/s scaled to the N=1024-agent workload."""
+def cpu_jacobi(sc, n_sample, threads, warmup, steps, tol=1e-8, max_seconds=30.0):
+    """The CPU restatement of the timed region, like for like: the same warm-started Jacobi loop as the GPU
+    line (JacobiSCvx with the bench's settings) on the first n_sample agents -- per step the FOH
+    (oracle/foh_ref.c), the QP twin (oracle/scvx_cpu.cpp, the kernel's algorithm, started from the previous
+    step's primal-dual point exactly as the kernel's warm rule: warm = last status == 0) and the per-agent
+    trust-region bookkeeping of csrc/jacobi.hip (tie margin 1e-9).  `warmup` untimed steps, then up to `steps`
+    timed steps (fewer if max_seconds runs out first).  Returns (SCvx iterations/s scaled to the N=1024-agent
+    workload, timed steps, seconds, mean IPM iterations per agent over the timed steps)."""
     from oracle import foh_oracle, qp_cpu
     tpl = qp_cpu.make_template(6, 3, K, box=BOX, obs=sc["obs"], w_obs=1e6, u_max=U_MAX, tol=tol, max_iter=60)
-    reps = 0
-    t0 = time.perf_counter()
-    while True:
-        disc = np.zeros((n_sample, K - 1, 6 * (6 + 6 + 2)))
-        for a in range(n_sample):
-            outs = foh_oracle.foh("di", sc["X"][a].T, sc["U"][a].T, sc["sigma"][a])
-            disc[a] = np.hstack([o.T for o in outs])
-        qp_cpu.solve_batched(tpl, disc, sc["sigma"][:n_sample], sc["X"][:n_sample], sc["U"][:n_sample],
-                             sc["x_init"][:n_sample], sc["x_final"][:n_sample], np.full(n_sample, TR0),
-                             nthreads=threads)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= min_seconds:
-            break
-    return reps * (n_sample / N_AGENTS) / el, reps, el
+    n = n_sample
+    X, U = sc["X"][:n].copy(), sc["U"][:n].copy()
+    sig, xi, xf = sc["sigma"][:n], sc["x_init"][:n], sc["x_final"][:n]
+    tr = np.full(n, TR0)
+    prev = np.full(n, np.inf)
+    wstate = np.zeros((n, qp_cpu.warm_doubles(tpl)))
+    warm = None
+    disc = np.zeros((n, K - 1, 6 * (6 + 6 + 2)))
+    timed, t_el, it_sum = 0, 0.0, 0
+    for k in range(warmup + steps):
+        t0 = time.perf_counter()
+        for a in range(n):
+            disc[a] = foh_oracle.foh_disc("di", X[a], U[a], sig[a])
+        o = qp_cpu.solve_batched(tpl, disc, sig, X, U, xi, xf, tr, nthreads=threads, warm=warm, wstate=wstate)
+        ok = o["status"] != 2
+        X = np.where(ok[:, None, None], o["X"], X)
+        U = np.where(ok[:, None, None], o["U"], U)
+        cost = (U[:, :-1] ** 2).sum(axis=(1, 2))
+        tr = np.where(cost > prev * (1.0 + 1e-9), 0.5 * tr, tr)
+        tr = np.where(ok, tr, 0.5 * tr)
+        prev = cost
+        warm = (o["status"] == 0).astype(np.int32)
+        if k >= warmup:
+            t_el += time.perf_counter() - t0
+            timed += 1
+            it_sum += int(o["iters"].sum())
+            if t_el >= max_seconds:
+                break
+    return timed * (n / N_AGENTS) / t_el, timed, t_el, it_sum / (timed * n)
 
 
-def cpu_baselines(sc, n_sample, tol):
-    """All-core and single-core CPU figures of the restatement.  "All cores" is every CPU this process may
-    run on: nproc, capped by the cgroup CPU quota when one is set (the GPU box grants 16 CPUs of a
-    256-thread host; more OpenMP threads than that only time-slice)."""
+def cpu_baselines(sc, n_sample, tol, warmup, steps):
+    """All-core and single-core CPU figures of the restatement on the GPU line's own loop (cpu_jacobi).  "All
+    cores" is every CPU this process may run on: nproc, capped by the cgroup CPU quota when one is set (the GPU
+    box grants 16 CPUs of a 256-thread host; more OpenMP threads than that only time-slice)."""
     info = host_info()
     quota = info.get("cgroup_cpu_quota")
     threads = max(1, min(info["nproc"], int(quota))) if quota else info["nproc"]
-    v_all, reps, el = cpu_baseline(sc, n_sample, threads, tol=tol)
+    v_all, steps_all, el, it_all = cpu_jacobi(sc, n_sample, threads, warmup, steps, tol=tol)
     n1 = min(n_sample, 64)
-    v_one, reps1, el1 = cpu_baseline(sc, n1, 1, tol=tol)
+    v_one, steps1, el1, it1 = cpu_jacobi(sc, n1, 1, warmup, steps, tol=tol)
     return dict(value=v_all, unit="SCvx-iterations/s (N=1024-agent equivalent)", cores=threads, kind="port",
-                sample=f"{reps} x one SCvx iteration of {n_sample} of the {N_AGENTS} agents (FOH C + structured IPM "
-                       f"C++, -O3 x86-64-v3, OpenMP over agents on {threads} threads = the CPUs this process may use: "
-                       f"nproc {info['nproc']}, cgroup quota {quota}), {el:.1f} s wall",
-                single_core={"value": v_one, "cores": 1,
-                             "sample": f"{reps1} x one SCvx iteration of {n1} agents on 1 thread, {el1:.1f} s wall"},
+                sample=f"warm-started steady state, steps {warmup + 1}-{warmup + steps_all} of the GPU line's Jacobi "
+                       f"loop ({warmup} untimed warm-up steps first) on {n_sample} of the {N_AGENTS} agents: FOH C + "
+                       f"the kernel's IPM in C++ with the same warm start and trust-region bookkeeping, -O3 x86-64-v3, "
+                       f"OpenMP over agents on {threads} threads = the CPUs this process may use (nproc "
+                       f"{info['nproc']}, cgroup quota {quota}); {el:.1f} s timed",
+                ipm_iters_per_agent=it_all,
+                single_core={"value": v_one, "cores": 1, "ipm_iters_per_agent": it1,
+                             "sample": f"steps {warmup + 1}-{warmup + steps1} of the same loop on {n1} agents, 1 thread, "
+                                       f"{el1:.1f} s timed"},
                 host=info)
 
 
@@ -604,7 +626,7 @@ def main():
     if rank == 0:
         cpu = None
         if not args.no_cpu and args.config == "c3":
-            cpu = cpu_baselines(sc, min(args.cpu_sample, N), tol=args.tol)
+            cpu = cpu_baselines(sc, min(args.cpu_sample, N), tol=args.tol, warmup=args.warmup, steps=args.steps)
         if args.config == "c3":
             value, scaling = world * args.steps / el, "weak"
             metric = "SCvx-iterations/sec, N agents x K=50 nodes (N=1024 per GPU)"

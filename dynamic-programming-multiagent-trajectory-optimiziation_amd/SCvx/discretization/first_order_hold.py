@@ -43,12 +43,14 @@ def device_model(model):
 
 def builtin_model(model, what):
     """The built-in device model name of `model`, for the kernels that are compiled per model class
-    (the SCP subproblem, the inter-sample search): a runtime-compiled user model is rejected loudly."""
-    dm = device_model(model)
-    if not isinstance(dm, str):
+    (the SCP subproblem, the inter-sample search): any other model is rejected loudly, before anything is
+    traced or compiled for it."""
+    name = "" if getattr(model, "scvx_device_model", None) is not None else \
+        (getattr(model, "scvx_model", "") or _BY_CLASS.get(type(model).__name__, ""))
+    if not name:
         raise NotImplementedError(f"{what}: compiled for the built-in models {sorted(scvx_hip.MODEL_DIMS)}; "
                                   f"{type(model).__name__} runs on the runtime-compiled FOH path only")
-    return dm
+    return device_model(model)   # validates the name and the dimensions
 
 
 class FirstOrderHold:
@@ -90,13 +92,20 @@ class FirstOrderHold:
         return self.A_bar, self.B_bar, self.C_bar, self.S_bar, self.z_bar
 
     # ---- caller-side batching (no reference counterpart; the reference integrates one agent per call)
-    def calculate_discretization_device(self, Xd, Ud, sd):
+    def calculate_discretization_device(self, Xd, Ud, sd, out=None):
         """Device-resident batch: Xd (M, K, n_x), Ud (M, K, n_u), sd (M,) float64 tensors on this object's
         device -> the packed per-interval matrices (M, K-1, n_x (n_x + 2 n_u + 2)) as a device tensor, one
-        launch and no host transfer (unpack with scvx_hip.unpack_disc)."""
+        launch and no host transfer (unpack with self.unpack_disc); `out` is an optional buffer to reuse."""
         if isinstance(self._name, str):
-            return scvx_hip.foh_batched(self._name, Xd, Ud, sd, nsub=self._nsub, params=self._params)
-        return self._name.foh(Xd, Ud, sd, nsub=self._nsub, params=self._params)
+            return scvx_hip.foh_batched(self._name, Xd, Ud, sd, nsub=self._nsub, params=self._params, out=out)
+        return self._name.foh(Xd, Ud, sd, nsub=self._nsub, params=self._params, out=out)
+
+    def unpack_disc(self, disc):
+        """Packed device disc [..., K-1, n(n+2m+2)] -> (A_bar, B_bar, C_bar, S_bar, z_bar) views in the
+        reference's F-order column layout."""
+        if isinstance(self._name, str):
+            return scvx_hip.unpack_disc(disc, self._name)
+        return self._name.unpack_disc(disc)
 
     def calculate_discretization_batched(self, Xs, Us, sigmas):
         """calculate_discretization for M agents in one launch and one host round trip each way (a loop of
@@ -113,8 +122,7 @@ class FirstOrderHold:
         Ud = torch.as_tensor(np.ascontiguousarray(np.stack([np.asarray(u, float).T for u in Us])), device=self._device)
         sd = torch.as_tensor(np.asarray(sigmas, float).reshape(M), device=self._device)
         disc = self.calculate_discretization_device(Xd, Ud, sd)
-        unpack = scvx_hip.unpack_disc if isinstance(self._name, str) else None
-        outs = [o.cpu().numpy() for o in (unpack(disc, self._name) if unpack else self._name.unpack_disc(disc))]
+        outs = [o.cpu().numpy() for o in self.unpack_disc(disc)]
         return [tuple(np.array(o[a]) for o in outs) for a in range(M)]
 
     def integrate_nonlinear_piecewise(self, X_lin, U, sigma):

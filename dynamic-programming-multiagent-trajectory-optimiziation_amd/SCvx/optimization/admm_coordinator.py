@@ -41,8 +41,8 @@ def discretize_batched(discretizers, X_list, U_list, sigma):
     X = torch.as_tensor(np.stack([np.asarray(x, float).T for x in X_list]), device=dev)
     U = torch.as_tensor(np.stack([np.asarray(u, float).T for u in U_list]), device=dev)
     s = torch.full((len(X_list),), float(sigma), dtype=torch.float64, device=dev)
-    disc = scvx_hip.foh_batched(d0._name, X.contiguous(), U.contiguous(), s, nsub=d0._nsub, params=d0._params)
-    host = [t.cpu().numpy() for t in scvx_hip.unpack_disc(disc, d0._name)]
+    disc = d0.calculate_discretization_device(X.contiguous(), U.contiguous(), s)
+    host = [t.cpu().numpy() for t in d0.unpack_disc(disc)]
     return [tuple(np.ascontiguousarray(h[a]) for h in host) for a in range(len(X_list))]
 
 
@@ -105,7 +105,7 @@ class ADMMCoordinator:
         out = None
         t0 = time.time()
         for it in range(self.max_iter):
-            disc = scvx_hip.foh_batched(d0._name, X, U, sig, nsub=d0._nsub, params=d0._params, out=disc)
+            disc = d0.calculate_discretization_device(X, U, sig, out=disc)
             Xr, Ur = (X0, U0) if self.trust_ref_is_initial else (X, U)
             if self.mode == "jacobi":
                 pos = X[nbr_l][..., :pd].contiguous()                # every agent sees the previous round

@@ -99,7 +99,7 @@ class NashSolver:
                 print(f"\n--- Outer iteration {it} ---")
             self._it = it
             Xp = X.clone()                                          # X_prev_all
-            disc = scvx_hip.foh_batched(d0._name, X, U, sig, nsub=d0._nsub, params=d0._params, out=disc)
+            disc = d0.calculate_discretization_device(X, U, sig, out=disc)
             if self.mode == "jacobi":
                 max_change = self._jacobi_round(specs, disc, X, U, Xp, sig, tr, x_init, x_final, nbr, pd, last, slabs)
             else:

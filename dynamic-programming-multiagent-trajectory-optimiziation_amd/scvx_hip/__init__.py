@@ -254,6 +254,9 @@ class QPSolver:
         self.iters = torch.empty(N, dtype=torch.int32, device=device)
         self._dummy = torch.zeros(1, dtype=torch.float64, device=device)
         self._dummy_i = torch.zeros(1, dtype=torch.int32, device=device)
+        # slots [0, _state_n) hold a solve's primal-dual state (solve(n=...) always fills a leading prefix):
+        # a warm flag on any other slot would start the IPM from uninitialised workspace, so it is cleared
+        self._state_n = 0
 
     def _check_shapes(self, disc, sigma, Xref, Uref, x_init, x_final, tr, coll_rows, coll_count, N=None):
         """Host-side shape checks: the kernel indexes every buffer with the template's compile-time
@@ -296,6 +299,9 @@ class QPSolver:
             return {k: v[:0] for k, v in self._outputs().items()}
         if warm is not None and tuple(warm.shape) != (n,):
             raise ValueError(f"QPSolver.solve: warm has shape {tuple(warm.shape)}, expected ({n},)")
+        if warm is not None and n > self._state_n:   # slots never solved by this solver start cold
+            warm = warm.clone()
+            warm[self._state_n:] = 0
         rc = lib().scvx_qp_solve_batched(
             ctypes.byref(self.ctpl), n, _dev(disc, name="disc"), _dev(sigma, name="sigma"),
             _dev(Xref, name="Xref"), _dev(Uref, name="Uref"), _dev(x_init, name="x_init"), _dev(xf, name="x_final"),
@@ -304,6 +310,7 @@ class QPSolver:
             _dev(self.iters, torch.int32), _dev(warm, torch.int32, "warm") if warm is not None else None,
             _dev(self.workspace), ctypes.c_size_t(self.workspace.numel() * 8), _stream(stream))
         check(rc, "scvx_qp_solve_batched")
+        self._state_n = max(self._state_n, n)
         out = self._outputs()
         return out if n == self.N else {k: v[:n] for k, v in out.items()}
 

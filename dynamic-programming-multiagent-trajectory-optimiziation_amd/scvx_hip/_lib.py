@@ -9,6 +9,9 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SCVX_HIP_LIB") or os.path.join(HERE, "libscvx_hip.so")  # override: diagnostics builds
 
+# the C-ABI revision these bindings are written for (SCVX_HIP_VERSION of include/scvx_hip.h): a library of
+# another revision would take these argument lists with shifted pointers, so lib() refuses it
+SCVX_HIP_VERSION = 3
 SCVX_MAX_BOX, SCVX_MAX_OBS, SCVX_MAX_NBR = 4, 16, 32
 SCVX_IS_MAX_PROJ, SCVX_IS_MAX_STATE = 3, 12
 MODEL_IDS = {"di": 0, "unicycle": 1, "si": 2, "quad": 3}
@@ -92,6 +95,9 @@ def lib():
         L = ctypes.CDLL(LIB_PATH)
         vp, i32, dbl, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_size_t
         L.scvx_version.restype = i32
+        if L.scvx_version() != SCVX_HIP_VERSION:
+            raise ImportError(f"{LIB_PATH} implements C-ABI revision {L.scvx_version()}, these bindings revision "
+                              f"{SCVX_HIP_VERSION}: rebuild it (`make -C {os.path.dirname(HERE)}`)")
         L.scvx_last_error.restype = ctypes.c_char_p
         L.scvx_foh_batched.argtypes = [i32, vp, i32, i32, vp, vp, vp, i32, vp, vp]
         L.scvx_integrate_nonlinear_batched.argtypes = [i32, vp, i32, i32, vp, vp, vp, i32, i32, vp, vp]

@@ -233,6 +233,19 @@ class _NumpyShim:
         return self._over[name] if name in self._over else getattr(self._np, name)
 
 
+def _is_math_name(k, v):
+    """True when the global `k` holds numpy's or math's own object of that name (e.g. `from numpy import sin`,
+    a lambdify namespace, `from math import e`); a user value that merely shares the name (a restitution
+    coefficient `e = 0.8`, an exponent `power = 2.0`) is not re-bound."""
+    import math
+    import numpy as np
+    for mod in (np, math):
+        ref = getattr(mod, k, None)
+        if ref is not None and v is ref:
+            return True
+    return False
+
+
 def _retrace(fn):
     import numpy as np
     bound = getattr(fn, "__self__", None)
@@ -242,7 +255,7 @@ def _retrace(fn):
     for k, v in list(ns.items()):
         if v is np:
             ns[k] = shim
-        elif k in shim._over:
+        elif k in shim._over and _is_math_name(k, v):
             ns[k] = shim._over[k]
     ns["float"] = lambda a=0.0: a   # float(expr) of a traced scalar stays symbolic
     g = types.FunctionType(fn.__code__, ns, fn.__name__, fn.__defaults__, fn.__closure__)

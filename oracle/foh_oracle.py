@@ -57,6 +57,21 @@ def foh(model, X, U, sigma, nsub=1, params=None):
     return tuple(np.ascontiguousarray(out[:, o[i]:o[i + 1]].T) for i in range(5))
 
 
+def foh_disc(model, X, U, sigma, nsub=1, params=None):
+    """X (K,n), U (K,m) agent-major -> disc (K-1, n(n+2m+2)), per interval vec_F(A) | vec_F(B) | vec_F(C) | S | z
+    (the layout of include/scvx_hip.h scvx_foh_batched)."""
+    n, m = MODEL_DIMS[model]
+    K = X.shape[0]
+    prm = np.ascontiguousarray(QUAD_PARAMS if params is None else params, dtype=np.float64)
+    Xc = np.ascontiguousarray(X, dtype=np.float64)
+    Uc = np.ascontiguousarray(U, dtype=np.float64)
+    out = np.zeros((K - 1, n * n + 2 * n * m + 2 * n))
+    rc = lib().oracle_foh(MODEL_IDS[model], _p(prm), n, m, K, _p(Xc), _p(Uc), float(sigma), nsub, _p(out))
+    if rc != 0:
+        raise ValueError("oracle_foh failed")
+    return out
+
+
 def integrate_nonlinear(model, X, U, sigma, piecewise, nsub=16, params=None):
     n, m = MODEL_DIMS[model]
     K = X.shape[1]

@@ -23,6 +23,8 @@ UNPINNED (no reference solver available offline); the reference formulation is w
 """
 import numpy as np
 
+from .cone import soc_max_step
+
 
 # ----------------------------------------------------------------------------------------------
 # generic dense conic QP interior-point solver
@@ -127,22 +129,7 @@ def _max_step(dims, x, dx):
         a = min(a, np.min(-x[:nl][neg] / dx[:nl][neg]))
     i = nl
     for k in dims["q"]:
-        xx, dd = x[i:i + k], dx[i:i + k]
-        qa, qb, qc = _soc_J(dd), 2.0 * (xx[0] * dd[0] - xx[1:] @ dd[1:]), _soc_J(xx)
-        roots = []
-        if abs(qa) < 1e-300:
-            if qb < 0:
-                roots.append(-qc / qb)
-        else:
-            disc = qb * qb - 4 * qa * qc
-            if disc >= 0:
-                sq = np.sqrt(disc)
-                roots += [(-qb - sq) / (2 * qa), (-qb + sq) / (2 * qa)]
-        for r in roots:
-            if r > 0:
-                a = min(a, r)
-        if dd[0] < 0:
-            a = min(a, -xx[0] / dd[0])
+        a = min(a, soc_max_step(x[i:i + k], dx[i:i + k]))
         i += k
     return a
 
@@ -185,26 +172,31 @@ def solve_conic_qp(P, q, A, b, G, h, dims, tol=1e-11, maxit=80, verbose=False):
         if pres < tol * pscale and dres < tol * dscale and s @ z < tol * max(1.0, abs(pobj)):
             status = "optimal"
             break
-        W, Wi = _nt_scaling(dims, s, z)
-        Wi2 = Wi @ Wi
-        lam = W @ z
+        try:
+            # an overflowing or invalid direction (a conditioning floor) ends the run: status stays "max_iter"
+            with np.errstate(over="raise", invalid="raise"):
+                W, Wi = _nt_scaling(dims, s, z)
+                Wi2 = Wi @ Wi
+                lam = W @ z
 
-        def solve_dir(rcomp):
-            rho = _jdiv(dims, lam, rcomp)
-            t = Wi @ rho + Wi2 @ rc
-            dx, dy = kkt_solve(Wi2, -rd - G.T @ t, -rp)
-            dz = Wi @ rho + Wi2 @ (rc + G @ dx)
-            ds = -rc - G @ dx
-            return dx, dy, ds, dz
+                def solve_dir(rcomp):
+                    rho = _jdiv(dims, lam, rcomp)
+                    t = Wi @ rho + Wi2 @ rc
+                    dx, dy = kkt_solve(Wi2, -rd - G.T @ t, -rp)
+                    dz = Wi @ rho + Wi2 @ (rc + G @ dx)
+                    ds = -rc - G @ dx
+                    return dx, dy, ds, dz
 
-        lam2 = _jprod(dims, lam, lam)
-        dxa, dya, dsa, dza = solve_dir(-lam2)
-        alpha = min(1.0, _max_step(dims, s, dsa), _max_step(dims, z, dza))
-        mu_a = ((s + alpha * dsa) @ (z + alpha * dza)) / deg
-        sig = (mu_a / mu) ** 3
-        corr = _jprod(dims, Wi @ dsa, W @ dza)
-        dx, dy, ds, dz = solve_dir(-lam2 - corr + sig * mu * e)
-        alpha = min(1.0, 0.99 * min(_max_step(dims, s, ds), _max_step(dims, z, dz)))
+                lam2 = _jprod(dims, lam, lam)
+                dxa, dya, dsa, dza = solve_dir(-lam2)
+                alpha = min(1.0, _max_step(dims, s, dsa), _max_step(dims, z, dza))
+                mu_a = ((s + alpha * dsa) @ (z + alpha * dza)) / deg
+                sig = (mu_a / mu) ** 3
+                corr = _jprod(dims, Wi @ dsa, W @ dza)
+                dx, dy, ds, dz = solve_dir(-lam2 - corr + sig * mu * e)
+                alpha = min(1.0, 0.99 * min(_max_step(dims, s, ds), _max_step(dims, z, dz)))
+        except (FloatingPointError, np.linalg.LinAlgError):
+            break
         x, y, s, z = x + alpha * dx, y + alpha * dy, s + alpha * ds, z + alpha * dz
     return dict(x=x, y=y, s=s, z=z, status=status, iters=it)
 

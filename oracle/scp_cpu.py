@@ -473,6 +473,12 @@ class SCPSolver:
     # ---- Riccati LQ solve: min sum 1/2 dz'H dz + f'dz s.t. xi~_{k+1} = At xi~ + Bt u~ + rp_k,
     # xi_0 (x part) = -r_init, g_0 free, pinned inputs zero.  Returns dz, costates y+ (K-1), y0+.
     def _lq(self, Hs, fs, rp, r_init):
+        # a breakdown (overflowing Riccati factor at an extreme barrier scaling) yields non-finite directions,
+        # which solve() detects and handles like the kernel (regularised retry, then the reduced-accuracy exit)
+        with np.errstate(over="ignore", invalid="ignore", divide="ignore"):
+            return self._lq_raw(Hs, fs, rp, r_init)
+
+    def _lq_raw(self, Hs, fs, rp, r_init):
         L, K, nodes = self.L, self.K, self.nodes
         nx, n = L.nxa, L.n
         Ps, ps, Ks, ks = [None] * K, [None] * K, [None] * K, [None] * K

@@ -23,6 +23,8 @@ import numpy as np
 import scipy.sparse as sp
 import scipy.sparse.linalg as spla
 
+from .cone import soc_max_step
+
 WEIGHT_COLLISION_SLACK = 1e5  # SCvx/optimization/admm_utils.py:5
 
 
@@ -83,19 +85,7 @@ def _max_step(dims, x, dx):
     if np.any(neg):
         a = min(a, np.min(-x[:nl][neg] / dx[:nl][neg]))
     for i, k in _cone_blocks(dims):
-        xx, dd = x[i:i + k], dx[i:i + k]
-        # largest t with (xx + t dd) in Q: solve the quadratic J(xx + t dd) = 0
-        qa = dd[0] ** 2 - dd[1:] @ dd[1:]
-        qb = 2 * (xx[0] * dd[0] - xx[1:] @ dd[1:])
-        qc = xx[0] ** 2 - xx[1:] @ xx[1:]
-        roots = np.roots([qa, qb, qc]) if abs(qa) > 1e-300 else ([-qc / qb] if qb != 0 else [])
-        for r in np.atleast_1d(roots):
-            if np.isreal(r) and np.real(r) > 0:
-                t = float(np.real(r))
-                if xx[0] + t * dd[0] >= -1e-14:
-                    a = min(a, t)
-        if dd[0] < 0:
-            a = min(a, -xx[0] / dd[0])
+        a = min(a, soc_max_step(x[i:i + k], dx[i:i + k]))
     return a
 
 
@@ -185,29 +175,32 @@ def solve_conic_qp_sparse(P, q, A, b, G, h, dims, tol=1e-10, maxit=100, osc=1.0,
         if it - best[1] > 15:
             break
         try:
-            W, Wi = _nt_scaling(dims, s, z)
-            Wi2 = Wi @ Wi
-            lam = W @ z
-            lu = factor(Wi2)
+            # an overflowing or invalid direction (the Newton system at a conditioning floor) is a breakdown:
+            # the best iterate so far is returned below, as ECOS does
+            with np.errstate(over="raise", invalid="raise"):
+                W, Wi = _nt_scaling(dims, s, z)
+                Wi2 = Wi @ Wi
+                lam = W @ z
+                lu = factor(Wi2)
 
-            def direction(rcomp):
-                rho = _jdiv(dims, lam, rcomp)
-                t = Wi @ rho + Wi2 @ rc
-                dx, dy = ksolve(lu, -rd - G.T @ t, -rp)
-                dz = Wi @ rho + Wi2 @ (rc + G @ dx)
-                ds = -rc - G @ dx
-                return dx, dy, ds, dz
+                def direction(rcomp):
+                    rho = _jdiv(dims, lam, rcomp)
+                    t = Wi @ rho + Wi2 @ rc
+                    dx, dy = ksolve(lu, -rd - G.T @ t, -rp)
+                    dz = Wi @ rho + Wi2 @ (rc + G @ dx)
+                    ds = -rc - G @ dx
+                    return dx, dy, ds, dz
 
-            lam2 = _jprod(dims, lam, lam)
-            dxa, dya, dsa, dza = direction(-lam2)
-            alpha = min(1.0, _max_step(dims, s, dsa), _max_step(dims, z, dza))
-            mu_a = ((s + alpha * dsa) @ (z + alpha * dza)) / deg
-            sig = (mu_a / mu) ** 3
-            corr = _jprod(dims, Wi @ dsa, W @ dza)
-            dx, dy, ds, dz = direction(-lam2 - corr + sig * mu * e)
-            alpha = min(1.0, 0.99 * min(_max_step(dims, s, ds), _max_step(dims, z, dz)))
-            if not (np.isfinite(alpha) and np.all(np.isfinite(dx)) and np.all(np.isfinite(dz))):
-                raise FloatingPointError("non-finite direction")
+                lam2 = _jprod(dims, lam, lam)
+                dxa, dya, dsa, dza = direction(-lam2)
+                alpha = min(1.0, _max_step(dims, s, dsa), _max_step(dims, z, dza))
+                mu_a = ((s + alpha * dsa) @ (z + alpha * dza)) / deg
+                sig = (mu_a / mu) ** 3
+                corr = _jprod(dims, Wi @ dsa, W @ dza)
+                dx, dy, ds, dz = direction(-lam2 - corr + sig * mu * e)
+                alpha = min(1.0, 0.99 * min(_max_step(dims, s, ds), _max_step(dims, z, dz)))
+                if not (np.isfinite(alpha) and np.all(np.isfinite(dx)) and np.all(np.isfinite(dz))):
+                    raise FloatingPointError("non-finite direction")
         except (RuntimeError, FloatingPointError):   # boundary round-off (SOC J < 0) or a singular
             break                                     # factor: the best iterate is returned below
         x, y, s, z = x + alpha * dx, y + alpha * dy, s + alpha * ds, z + alpha * dz
@@ -444,6 +437,9 @@ def solve_scproblem(prob, tol=1e-10, maxit=100):
                s_prime=g("sp").reshape(-1, K), S=g("S").reshape(-1, K),
                obj=float(0.5 * x @ (P @ x) + q @ x + idx["const"]), status=sol["status"], iters=sol["iters"],
                cert=kkt_certificate(P, q, A, b, G, h, dims, sol))
+    # duality gap of the returned point relative to its objective (caller's units): an optimal_inaccurate
+    # answer (the best iterate at a conditioning floor) is as good as this says
+    out["rel_gap"] = abs(float(sol["s"] @ sol["z"])) / max(1.0, abs(float(0.5 * x @ (P @ x) + q @ x)))
     return out
 
 

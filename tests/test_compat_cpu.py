@@ -138,6 +138,9 @@ def test_library_exports_every_header_symbol():
     t.K = 100
     assert L.scvx_qp_solve_batched(ctypes.byref(t), 1, *([None] * 17), None, 0, None) == -2
     assert L.scvx_version() >= 3   # v2: w_nu / w_prox template fields, the nu output; v3: scvx_rtc_*
+    # the bindings' revision is the header's, and the loaded library's (lib() refuses any other)
+    hv = int(re.search(r"#define SCVX_HIP_VERSION (\d+)", hdr).group(1))
+    assert _lib.SCVX_HIP_VERSION == hv == L.scvx_version()
 
 
 def test_first_order_hold_rejects_models_without_device_dynamics():

@@ -60,6 +60,9 @@ def _check_against_oracle(p, X, U, nu, sigma, obj_kernel, w_u2):
     from oracle import nash_ref, scp_dense as sd
     ref = nash_ref.best_response(p)
     assert ref["status"] in ("optimal", "optimal_inaccurate"), ref["status"]
+    # the checker's own certificate: a best-iterate exit must still be a near-exact KKT point
+    assert ref["rel_gap"] <= 1e-8 and ref["cert"]["primal"] <= 1e-9 and ref["cert"]["stationarity"] <= 1e-9, \
+        (ref["rel_gap"], ref["cert"])
     obj = sd.scp_objective(p, X, U, nu, sigma)
     assert abs(obj - ref["obj"]) <= 1e-6 * abs(ref["obj"]), (obj, ref["obj"])
     assert abs(obj_kernel - obj) <= 1e-7 * abs(obj), (obj_kernel, obj)        # kernel-reported objective

@@ -123,6 +123,21 @@ def test_retrace_of_dropin_models():
     assert dq.f_exprs[:3] == ["x[3]", "x[4]", "x[5]"]
 
 
+def test_retrace_keeps_user_globals_that_share_a_math_name():
+    """A model module's own constants named like a numpy / math object (a restitution `e = 0.8`, an exponent
+    `power = 3.0`) stay the user's values; only numpy's and math's objects are re-bound to sympy."""
+    import math
+    from scvx_hip.rtc import _retrace
+    g = {"np": np, "e": 0.8, "power": 3.0, "sin": np.sin, "pi": math.pi}
+    exec("def f(x, u):\n    return np.array([x[1], -e * x[0] ** power + sin(pi * u[0])])", g)
+    xs, us = sp.symbols("x0:2", real=True), sp.symbols("u0:1", real=True)
+    got = np.asarray(_retrace(g["f"])(list(xs), list(us)), dtype=object)
+    for x0, u0 in ((0.7, 0.3), (-1.3, 2.1)):
+        want = -0.8 * x0 ** 3 + math.sin(math.pi * u0)
+        assert abs(float(got[1].subs({xs[0]: x0, us[0]: u0})) - want) < 1e-12
+    assert got[1].has(sp.sin) and got[1].has(sp.pi)
+
+
 def test_untraceable_model_is_rejected():
     from scvx_hip.rtc import DeviceModel
 

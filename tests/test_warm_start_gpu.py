@@ -60,3 +60,27 @@ def test_warm_start_reaches_the_cold_optimum(cuda):
         X, U = ow["X"], ow["U"]      # the Jacobi update (every agent solved)
         warm = (ow["status"] == 0).to(torch.int32)
     assert np.mean(its_warm) < 0.6 * np.mean(its_cold), (its_warm, its_cold)
+
+
+def test_warm_flag_on_a_never_solved_slot_starts_cold(cuda):
+    """QPSolver.solve(warm=...) on slots this solver has not solved yet: their workspace holds no primal-dual
+    state, so they start cold (the same result as warm=None), bit for bit."""
+    import torch
+    from scvx_hip import workloads
+    N, K = 64, 50
+    sc = workloads.synthetic_di(N, K=K, seed=1, obstacles=8)
+    spec = scvx_hip.QPSpec(model="di", K=K, box=BOX, obs=sc["obs"], w_obs=1e6, u_max=1.0, tol=1e-8, max_iter=60)
+    X, U, sig = _t(sc["X"], cuda), _t(sc["U"], cuda), _t(sc["sigma"], cuda)
+    xi, xf, tr = _t(sc["x_init"], cuda), _t(sc["x_final"], cuda), _t(np.full(N, 0.25), cuda)
+    disc = scvx_hip.foh_batched("di", X, U, sig)
+    ref = {k: v.clone() for k, v in scvx_hip.QPSolver(spec, N, device=cuda).solve(disc, sig, X, U, xi, xf, tr).items()}
+    s = scvx_hip.QPSolver(spec, N, device=cuda)
+    s.workspace.fill_(float("nan"))                      # what an uninitialised slot could hold
+    half = s.solve(disc[:N // 2], sig[:N // 2], X[:N // 2], U[:N // 2], xi[:N // 2], xf[:N // 2], tr[:N // 2],
+                   n=N // 2, warm=torch.ones(N // 2, dtype=torch.int32, device=cuda))
+    assert torch.equal(half["X"], ref["X"][:N // 2]) and torch.equal(half["status"], ref["status"][:N // 2])
+    out = s.solve(disc, sig, X, U, xi, xf, tr, warm=torch.zeros(N, dtype=torch.int32, device=cuda) + 1)
+    # slots >= N/2 were never solved: cold; slots < N/2 warm-start from the identical subproblem's optimum
+    assert torch.equal(out["X"][N // 2:], ref["X"][N // 2:])
+    assert (out["status"] == 0).all()
+    assert out["iters"][:N // 2].float().mean() < ref["iters"][:N // 2].float().mean()

@@ -1,0 +1,97 @@
+"""Diagnostics (not a test): the bench's C4 loop (bench.make_coupled("c4"), world 1) step by step --
+per step the global trust radius, status counts, exit-code histogram of the status-1 solves, IPM
+iterations, warm-started count; for the steps with the most status-1 solves, the IPM trace of a few
+status-1 agents replayed from a snapshot of the solver workspace (the exact warm-started solve), their
+cold re-solve on the GPU, and an npz dump of the subproblems (gpurun_out/c4_drift_*.npz) for the
+dense oracle / CPU twin on the host.
+usage: python tools/c4_drift.py [steps] [dump_steps, comma separated]"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "dynamic-programming-multiagent-trajectory-optimiziation_amd"))
+sys.path.insert(0, REPO)
+
+
+def main(steps=25, dump_steps="12,18", n_dump=4, cap=64):
+    import torch
+    import bench
+    import scvx_hip
+    from scvx_hip.scvx import CouplingSpec, JacobiSCvx
+    steps = int(steps)
+    dump_steps = {int(s) for s in str(dump_steps).split(",") if s}
+    dev = torch.device("cuda:0")
+    sc, w, cfg = bench.make_coupled("c4", 1, 0, dev)
+    ws = int(os.environ.get("WARM_STATUS", "0"))
+    spec = scvx_hip.QPSpec(model="di", K=bench.K, box=cfg["box"], obs=cfg["obs"], w_obs=1e6, j_max=cfg["j_max"],
+                           w_coll=1e4, tol=1e-8, max_iter=60)
+    drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], bench.TR0, coupling=CouplingSpec(R=cfg["R"]),
+                     tr_rule="global", warm_max_status=ws)
+    lib = scvx_hip.lib()
+    X, U = w["X"].clone(), w["U"].clone()
+    N = X.shape[0]
+    codes = torch.zeros(N, dtype=torch.float64, device=dev)
+    cold = scvx_hip.QPSolver(spec, N, device=dev)
+    for k in range(steps):
+        trp = drv.tr.clone()
+        warm_in = None if drv.warm is None else drv.warm.clone()
+        snap = drv.solver.workspace.clone() if k in dump_steps else None
+        lib.scvx_qp_set_trace(ctypes.c_void_p(codes.data_ptr()), -1, 0)
+        Xn, Un, o = drv.step(X, U)
+        torch.cuda.synchronize()
+        lib.scvx_qp_set_trace(None, 0, 0)
+        # the main solve's own outputs (drv.solver buffers; `o` is after the full-row check re-solve)
+        st = drv.solver.status.cpu().numpy()
+        it = drv.solver.iters.cpu().numpy()
+        cd = codes.cpu().numpy().astype(int)
+        nw = 0 if warm_in is None else int(warm_in.sum().item())
+        s1 = np.nonzero(st == 1)[0]
+        print(f"step {k}: tr {trp[0].item():.5g} warm {nw} status {np.bincount(st, minlength=3).tolist()} "
+              f"codes(st1) {dict(zip(*np.unique(cd[s1], return_counts=True)))} iters mean {it.mean():.2f} max {it.max()} "
+              f"mean(st1) {it[s1].mean() if s1.size else 0:.1f} warm(st1) "
+              f"{int(warm_in[s1].sum().item()) if (warm_in is not None and s1.size) else 0} check {drv.last_check}",
+              flush=True)
+        if k in dump_steps and s1.size:
+            pick = s1[:: max(1, s1.size // n_dump)][:n_dump]
+            rows, count = drv.rows.clone(), drv.count.clone()
+            # cold re-solve of the same subproblems
+            oc = cold.solve(drv.disc, drv.sigma, X, U, drv.x_init, drv.x_final, trp, rows, count)
+            stc, itc = oc["status"].cpu().numpy(), oc["iters"].cpu().numpy()
+            print(f"   cold re-solve of step {k}: status {np.bincount(stc, minlength=3).tolist()} on the st1 agents "
+                  f"{np.bincount(stc[s1], minlength=3).tolist()} iters mean {itc.mean():.2f} (st1 {itc[s1].mean():.1f})",
+                  flush=True)
+            objw = drv.solver.obj.cpu().numpy()
+            objc = oc["obj"].cpu().numpy()
+            for a in pick:
+                buf = torch.zeros(8 * cap + 32, dtype=torch.float64, device=dev)
+                ws_now = drv.solver.workspace.clone()
+                drv.solver.workspace.copy_(snap)
+                lib.scvx_qp_set_trace(ctypes.c_void_p(buf.data_ptr()), int(a), cap)
+                orp = drv.solver.solve(drv.disc, drv.sigma, X, U, drv.x_init, drv.x_final, trp, rows, count, warm=warm_in)
+                torch.cuda.synchronize()
+                lib.scvx_qp_set_trace(None, 0, 0)
+                bb = buf.cpu().numpy()
+                print(f"   agent {a}: warm {int(warm_in[a].item()) if warm_in is not None else 0} replay status "
+                      f"{orp['status'][a].item()} iters {orp['iters'][a].item()} code {bb[8 * cap + 3]:.0f} "
+                      f"obj warm {objw[a]:.12e} cold {objc[a]:.12e} (cold status {stc[a]}, iters {itc[a]})", flush=True)
+                b = bb[:8 * cap].reshape(cap, 8)
+                for i in range(min(int(orp["iters"][a].item()) + 1, cap)):
+                    print("     it %2d pres %.2e dres %.2e gap %.2e pobj %.12e aa %.3f al %.3f sg %.2e mu %.2e"
+                          % ((i,) + tuple(b[i])), flush=True)
+                drv.solver.workspace.copy_(ws_now)
+            os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+            np.savez(os.path.join(REPO, "gpurun_out", f"c4_drift_step{k}.npz"), agents=pick,
+                     disc=drv.disc[pick].cpu().numpy(), sigma=drv.sigma[pick].cpu().numpy(),
+                     X=X[pick].cpu().numpy(), U=U[pick].cpu().numpy(), x_init=drv.x_init[pick].cpu().numpy(),
+                     x_final=drv.x_final[pick].cpu().numpy(), tr=trp[pick].cpu().numpy(),
+                     rows=rows[pick].cpu().numpy(), count=count[pick].cpu().numpy(),
+                     obj_warm=objw[pick], obj_cold=objc[pick], st_cold=stc[pick],
+                     Xw=drv.solver.X[pick].cpu().numpy(), Uw=drv.solver.U[pick].cpu().numpy())
+        X, U = Xn.clone(), Un.clone()
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
