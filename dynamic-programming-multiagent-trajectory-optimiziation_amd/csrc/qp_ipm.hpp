@@ -102,6 +102,15 @@ constexpr long long qp_ws_doubles(int nx, int nu, int nb, int ns, int ng, int K,
 constexpr int QP_OOB = 0x40000000;
 // warm start: floor of every slack and dual of the previous iterate (scaled units; oracle/scvx_cpu.cpp)
 constexpr double QP_WARM_ETA = 1e-3;
+// fraction-to-boundary of the end game (affine step >= 0.99).  In the warm-started Jacobi loop almost every
+// solve is an end game from its first iteration: each step is a full Newton step up to this fraction, so
+// the gap falls by 1 / (1 - QP_TAU_END) per iteration.  0.999 took the C3 bulk 5 iterations, 1 - 1e-5 takes
+// it 3 (oracle/scvx_cpu.cpp, the same rule; 1 - 1e-6 lengthened the tail: measured on the twin over the
+// bench's 25 steps)
+constexpr double QP_TAU_END = 0.99999;
+// chunked solve chains (NX <= 8): the K-1 transitions are cut into QP_NCH chunks, one per 8-lane group; a
+// chunk holds at most QP_CLM transitions (K <= 64)
+constexpr int QP_NCH = 8, QP_CLM = 8;
 
 // VC_ = 1: the virtual-control class (scvx_qp_template.w_nu > 0): nu_t in every dynamics row, priced
 // w_nu ||nu_t||_1 through its epigraph -e <= nu <= e.  nu is eliminated inside each Riccati stage
@@ -212,8 +221,10 @@ struct QPCfg {
                          L_R2F = L_XI0 + NX, L_YI = L_R2F + NX, L_YF = L_YI + NX, L_DYI = L_YF + NX,
                          L_DYF = L_DYI + NX, L_PIV = L_DYF + NX, L_ONE = L_PIV + NX, L_FLAG = L_ONE + 1,
                          L_ST = qp_even(L_FLAG + 4), L_S = L_ST + 16, L_L = L_S + NR * 64, L_VAR = L_L + NR * 64;
-    // row slacks s / duals lambda [r][lane]; then K-sized: chain offsets g/f [K][NX], chain vectors [K+1][NX]
-    static constexpr int lds_doubles(int K) { return L_VAR + K * NX + (K + 1) * NX; }
+    // row slacks s / duals lambda [r][lane]; then K-sized: chain offsets g/f [K][NX], chain vectors [K+1][NX];
+    // then (chunked solve chains, NX <= 8) the chunk transition matrices Phi_c [QP_NCH][NX][NX]
+    static constexpr bool CHK = NX <= 8;
+    static constexpr int lds_doubles(int K) { return L_VAR + K * NX + (K + 1) * NX + (CHK ? QP_NCH * NX * NX : 0); }
     static_assert(4 * NV <= WAVE, "virtual control: one Gauss-Jordan column per lane");
 };
 
@@ -468,7 +479,21 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     constexpr int V_M = C::L_M, V_PI0 = C::L_PI0, V_XE = C::L_XE, V_XI0 = C::L_XI0, V_R2F = C::L_R2F,
                   V_YI = C::L_YI, V_YF = C::L_YF, V_DYI = C::L_DYI, V_DYF = C::L_DYF, V_PIV = C::L_PIV,
                   V_ONE = C::L_ONE, V_FLAG = C::L_FLAG, V_ST = C::L_ST, V_S = C::L_S, V_L = C::L_L;
-    const int V_G = C::L_VAR, V_CH = V_G + K * NX;
+    const int V_G = C::L_VAR, V_CH = V_G + K * NX, V_PHI = V_CH + (K + 1) * NX;
+    // chunked chains (C::CHK): transitions t = 0..K-2 in chunks of CL; lane = 8 ch + ce carries element ce of
+    // chunk ch, whose transitions are [cs0, cs1)
+    const int KS = K - 1, CL = (KS + QP_NCH - 1) / QP_NCH, NCH = (KS + CL - 1) / CL;
+    // (a phase re-derives these from qp_opaque(lane) through chunk_coords(): the address arithmetic is then
+    // rebuilt inside the phase, not hoisted out of the IPM loop and held -- or spilled -- across it)
+    struct ChunkC { int ch, ce, cs0, cs1; bool act; };
+    auto chunk_coords = [&]() __attribute__((always_inline)) -> ChunkC {
+        ChunkC r;
+        const int l = qp_opaque(lane);
+        r.ch = l >> 3; r.ce = l & 7;
+        r.cs0 = min(r.ch * CL, KS); r.cs1 = min(r.cs0 + CL, KS);
+        r.act = r.ce < NX && r.cs0 < r.cs1;
+        return r;
+    };
     // region timers of the traced agent (diagnostics): cycles since the previous stamp -> V_ST[i]
     const bool stamp_on = a.trace && agent == a.trace_agent;
     long long tprev = 0;
@@ -1028,6 +1053,42 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
         }
         wsync();
+        if constexpr (C::CHK) {
+            const ChunkC cc = chunk_coords();
+            const int ch = cc.ch, ce = cc.ce, cs0 = cc.cs0, cs1 = cc.cs1;
+            const bool cact = cc.act;
+            // chunk transition matrices Phi_c = Acl_{s1-1} ... Acl_{s0} (the chain matrices B_CH of the chunk's
+            // transitions, just stored by the sweep): lane (ch, ce) keeps row ce, Phi <- Acl_t Phi with the rows of
+            // Phi broadcast inside the 8-lane group; the solve chains of this factor read them from LDS
+            double ar[QP_CLM][NX], ph[NX];
+#pragma unroll
+            for (int j = 0; j < QP_CLM; ++j) {
+                const int tj = cs0 + j;
+                const int vo = (cact && j < CL && tj < cs1) ? (C::B_CH + ce * NX) * 8 + tj * C::FBS * 8 : QP_OOB;
+#pragma unroll
+                for (int k = 0; k < NX; ++k) ar[j][k] = wb.ld(vo + k * 8, FBB);
+            }
+#pragma unroll
+            for (int c = 0; c < NX; ++c) ph[c] = (c == ce) ? 1.0 : 0.0;
+#pragma unroll
+            for (int j = 0; j < QP_CLM; ++j) {
+                if (j < CL) {
+                    double nw[NX];
+#pragma unroll
+                    for (int c = 0; c < NX; ++c) nw[c] = 0.0;
+#pragma unroll
+                    for (int k = 0; k < NX; ++k)
+#pragma unroll
+                        for (int c = 0; c < NX; ++c) nw[c] = fma(ar[j][k], oct_bcast_d(ph[c], k), nw[c]);
+                    const bool ok = cs0 + j < cs1;
+#pragma unroll
+                    for (int c = 0; c < NX; ++c) ph[c] = ok ? nw[c] : ph[c];
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < NX; ++c) lds[cact ? V_PHI + ch * NX * NX + ce * NX + c : C::F_SINK] = ph[c];
+            wsync();
+        }
         return lds[V_FLAG] == 0.0;
     };
 
@@ -1079,50 +1140,119 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
         wsync();
         stamp(4);
-        // ---- backward chain p_t = Acl_t' p_{t+1} + g_t (lane i: element i); p_{t+1} broadcast
-        // from lanes 0..NX-1 by a DPP row broadcast (NX <= 16), the Acl column / g of the next stage read ahead
-        if (lane < NX) {
-            // lane i needs column i of Acl_t (stage block, B_CH + k*NX + i; Acl~ for VC)
-            const int va = (C::B_CH + lane) * 8;
-            auto ldA = [&](int ts, double* an, double& gn) __attribute__((always_inline)) {
-                const int tc = ts > 0 ? ts : 0;
+        if constexpr (C::CHK) {
+            const ChunkC cc = chunk_coords();
+            const int ch = cc.ch, ce = cc.ce, cs0 = cc.cs0, cs1 = cc.cs1;
+            const bool cact = cc.act;
+            // chunked: p_{s0} = Phi_c' p_{s1} + q_c per chunk (q_c the chunk's chain from p_{s1} = 0), so
+            //   A  every chunk runs its own CL steps from 0 (the last chunk from p_{K-1} = g_{K-1}: exact),
+            //   B  lanes < NX carry p across the chunk boundaries from the last chunk down (NCH - 1 steps,
+            //      Phi_c' from LDS),
+            //   C  every chunk re-runs its steps from its exact p_{s1}, storing p_t inside the chunk;
+            // (CL + NCH - 1 + CL dependent steps instead of K - 1).  Lane (ch, ce) holds column ce of Acl_t for
+            // its chunk's transitions t = cs1 - 1 - j in registers, loaded in one batch.
+            double ac[QP_CLM][NX], gc[QP_CLM];
 #pragma unroll
-                for (int k = 0; k < NX; ++k) an[k] = wb.ld(va + k * NX * 8, FBB + tc * C::FBS * 8);
-                gn = lds[V_G + tc * NX + lane];
-            };
-            auto chain = [&](double p, const double* ac, double g) __attribute__((always_inline)) -> double {
+            for (int j = 0; j < QP_CLM; ++j) {
+                const int tj = cs1 - 1 - j;
+                const bool ok = cact && j < CL && tj >= cs0;
+                const int vo = ok ? (C::B_CH + ce) * 8 + tj * C::FBS * 8 : QP_OOB;
+#pragma unroll
+                for (int k = 0; k < NX; ++k) ac[j][k] = wb.ld(vo + k * NX * 8, FBB);
+                gc[j] = lds[V_G + (ok ? tj : 0) * NX + (ce < NX ? ce : 0)];
+            }
+            auto chainT = [&](double q, const double* a, double g) __attribute__((always_inline)) -> double {
                 double v0 = g, v1 = 0.0;
 #pragma unroll
                 for (int k = 0; k < NX; ++k) {
-                    const double pkv = row_bcast_d(p, k);
-                    if (k & 1) v1 = fma(ac[k], pkv, v1); else v0 = fma(ac[k], pkv, v0);
+                    const double qk = oct_bcast_d(q, k);
+                    if (k & 1) v1 = fma(a[k], qk, v1); else v0 = fma(a[k], qk, v0);
                 }
                 return v0 + v1;
             };
-            double p = lds[V_G + (K - 1) * NX + lane];
-            lds[V_CH + (K - 1) * NX + lane] = p;
-            // QP_CPF register buffers: operands loaded QP_CPF stages ahead (a global load under
-            // full-chip load takes ~2,000 cycles; 8 stages measured no faster than 4 and spilled more)
-            double ab[CPF][NX], gb[CPF];
+            const double gK = lds[V_G + (K - 1) * NX + (ce < NX ? ce : 0)];
+            if (lane < NX) lds[V_CH + (K - 1) * NX + lane] = gK;
+            double q = (cs1 == KS) ? gK : 0.0;
 #pragma unroll
-            for (int b = 0; b < CPF; ++b) ldA(K - 2 - b, ab[b], gb[b]);
-            int ts = K - 2;
-            auto step = [&](double* a, double& g) __attribute__((always_inline)) {
-                p = chain(p, a, g);
-                lds[V_CH + ts * NX + lane] = p;
-                ldA(ts - CPF, a, g);
-                --ts;
-            };
-            // groups of QP_CPF steps with no exit inside the loop body (a mid-body exit makes the
-            // compiler's vmcnt tracking fall back to vmcnt(0) and drain the prefetches), then the
-            // remaining steps continuing the buffer rotation
-            while (ts >= CPF - 1) {
-#pragma unroll
-                for (int b = 0; b < CPF; ++b) step(ab[b], gb[b]);
+            for (int j = 0; j < QP_CLM; ++j) {
+                if (j < CL) {
+                    const double qn = chainT(q, ac[j], gc[j]);
+                    q = (cs1 - 1 - j >= cs0) ? qn : q;
+                }
             }
+            lds[cact ? V_CH + cs0 * NX + ce : C::F_SINK] = q;
+            wsync();
+            if (lane < NX) {
+                double p = lds[V_CH + min((NCH - 1) * CL, KS) * NX + lane];
+                for (int c = NCH - 2; c >= 0; --c) {
+                    double v0 = lds[V_CH + c * CL * NX + lane], v1 = 0.0;
 #pragma unroll
-            for (int b = 0; b < CPF - 1; ++b)
-                if (ts >= 0) step(ab[b], gb[b]);
+                    for (int k = 0; k < NX; ++k) {
+                        const double pk = row_bcast_d(p, k);
+                        const double f = lds[V_PHI + c * NX * NX + k * NX + lane];
+                        if (k & 1) v1 = fma(f, pk, v1); else v0 = fma(f, pk, v0);
+                    }
+                    p = v0 + v1;
+                    lds[V_CH + c * CL * NX + lane] = p;
+                }
+            }
+            wsync();
+            double p = lds[V_CH + (cact ? cs1 : 0) * NX + (ce < NX ? ce : 0)];
+#pragma unroll
+            for (int j = 0; j < QP_CLM; ++j) {
+                if (j < CL) {
+                    const int tj = cs1 - 1 - j;
+                    const double pn = chainT(p, ac[j], gc[j]);
+                    p = tj >= cs0 ? pn : p;
+                    lds[(cact && tj > cs0) ? V_CH + tj * NX + ce : C::F_SINK] = p;
+                }
+            }
+        } else {
+            // ---- backward chain p_t = Acl_t' p_{t+1} + g_t (lane i: element i); p_{t+1} broadcast
+            // from lanes 0..NX-1 by a DPP row broadcast (NX <= 16), the Acl column / g of the next stage read ahead
+            if (lane < NX) {
+                // lane i needs column i of Acl_t (stage block, B_CH + k*NX + i; Acl~ for VC)
+                const int va = (C::B_CH + lane) * 8;
+                auto ldA = [&](int ts, double* an, double& gn) __attribute__((always_inline)) {
+                    const int tc = ts > 0 ? ts : 0;
+    #pragma unroll
+                    for (int k = 0; k < NX; ++k) an[k] = wb.ld(va + k * NX * 8, FBB + tc * C::FBS * 8);
+                    gn = lds[V_G + tc * NX + lane];
+                };
+                auto chain = [&](double p, const double* ac, double g) __attribute__((always_inline)) -> double {
+                    double v0 = g, v1 = 0.0;
+    #pragma unroll
+                    for (int k = 0; k < NX; ++k) {
+                        const double pkv = row_bcast_d(p, k);
+                        if (k & 1) v1 = fma(ac[k], pkv, v1); else v0 = fma(ac[k], pkv, v0);
+                    }
+                    return v0 + v1;
+                };
+                double p = lds[V_G + (K - 1) * NX + lane];
+                lds[V_CH + (K - 1) * NX + lane] = p;
+                // QP_CPF register buffers: operands loaded QP_CPF stages ahead (a global load under
+                // full-chip load takes ~2,000 cycles; 8 stages measured no faster than 4 and spilled more)
+                double ab[CPF][NX], gb[CPF];
+    #pragma unroll
+                for (int b = 0; b < CPF; ++b) ldA(K - 2 - b, ab[b], gb[b]);
+                int ts = K - 2;
+                auto step = [&](double* a, double& g) __attribute__((always_inline)) {
+                    p = chain(p, a, g);
+                    lds[V_CH + ts * NX + lane] = p;
+                    ldA(ts - CPF, a, g);
+                    --ts;
+                };
+                // groups of QP_CPF steps with no exit inside the loop body (a mid-body exit makes the
+                // compiler's vmcnt tracking fall back to vmcnt(0) and drain the prefetches), then the
+                // remaining steps continuing the buffer rotation
+                while (ts >= CPF - 1) {
+    #pragma unroll
+                    for (int b = 0; b < CPF; ++b) step(ab[b], gb[b]);
+                }
+    #pragma unroll
+                for (int b = 0; b < CPF - 1; ++b)
+                    if (ts >= 0) step(ab[b], gb[b]);
+            }
         }
         wsync();
         stamp(5);
@@ -1289,44 +1419,113 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
         wsync();
         stamp(7);
-        // ---- forward chain xi_{t+1} = Acl_t xi_t + f_t
-        if (lane < NX) {
-            // lane i needs row i of Acl_t (stage block, B_CH + i*NX + k; Acl~ for VC)
-            const int va = (C::B_CH + lane * NX) * 8;
-            auto ldA = [&](int ts, double* an, double& fn) __attribute__((always_inline)) {
-                const int tc = ts < K - 1 ? ts : K - 2;
+        if constexpr (C::CHK) {
+            const ChunkC cc = chunk_coords();
+            const int ch = cc.ch, ce = cc.ce, cs0 = cc.cs0, cs1 = cc.cs1;
+            const bool cact = cc.act;
+            // chunked as the backward chain: x_{s1} = Phi_c x_{s0} + y_c per chunk;
+            //   A  every chunk runs its CL steps from 0 (chunk 0 from xi_0: exact),
+            //   B  lanes < NX carry x across the boundaries (NCH - 2 steps, Phi_c from LDS),
+            //   C  every chunk re-runs from its exact x_{s0}, storing x_t inside the chunk (and x_{K-1}).
+            // Lane (ch, ce) holds row ce of Acl_t, t = cs0 + j, in registers.
+            double ar[QP_CLM][NX], fr[QP_CLM];
 #pragma unroll
-                for (int k = 0; k < NX; ++k) an[k] = wb.ld(va + k * 8, FBB + tc * C::FBS * 8);
-                fn = lds[V_G + tc * NX + lane];
-            };
-            auto chain = [&](double x, const double* ac, double f) __attribute__((always_inline)) -> double {
+            for (int j = 0; j < QP_CLM; ++j) {
+                const int tj = cs0 + j;
+                const bool ok = cact && j < CL && tj < cs1;
+                const int vo = ok ? (C::B_CH + ce * NX) * 8 + tj * C::FBS * 8 : QP_OOB;
+#pragma unroll
+                for (int k = 0; k < NX; ++k) ar[j][k] = wb.ld(vo + k * 8, FBB);
+                fr[j] = lds[V_G + (ok ? tj : 0) * NX + (ce < NX ? ce : 0)];
+            }
+            auto chainF = [&](double x, const double* a, double f) __attribute__((always_inline)) -> double {
                 double w0 = f, w1 = 0.0;
 #pragma unroll
                 for (int k = 0; k < NX; ++k) {
-                    const double xk = row_bcast_d(x, k);
-                    if (k & 1) w1 = fma(ac[k], xk, w1); else w0 = fma(ac[k], xk, w0);
+                    const double xk = oct_bcast_d(x, k);
+                    if (k & 1) w1 = fma(a[k], xk, w1); else w0 = fma(a[k], xk, w0);
                 }
                 return w0 + w1;
             };
-            double x = lds[V_XI0 + lane];
-            lds[V_CH + lane] = x;
-            double ab[CPF][NX], fb[CPF];
+            const double x0 = lds[V_XI0 + (ce < NX ? ce : 0)];
+            double x = (ch == 0) ? x0 : 0.0;
 #pragma unroll
-            for (int b = 0; b < CPF; ++b) ldA(b, ab[b], fb[b]);
-            int ts = 0;
-            auto step = [&](double* a, double& f) __attribute__((always_inline)) {
-                x = chain(x, a, f);
-                lds[V_CH + (ts + 1) * NX + lane] = x;
-                ldA(ts + CPF, a, f);
-                ++ts;
-            };
-            while (ts <= K - 1 - CPF) {  // CPF steps per trip, no exit inside (see the backward chain)
-#pragma unroll
-                for (int b = 0; b < CPF; ++b) step(ab[b], fb[b]);
+            for (int j = 0; j < QP_CLM; ++j) {
+                if (j < CL) {
+                    const double xn = chainF(x, ar[j], fr[j]);
+                    x = (cs0 + j < cs1) ? xn : x;
+                }
             }
+            lds[cact ? V_CH + cs1 * NX + ce : C::F_SINK] = x;
+            if (lane < NX) lds[V_CH + lane] = x0;
+            wsync();
+            if (lane < NX) {
+                double xs = lds[V_CH + min(CL, KS) * NX + lane];
+                for (int c = 1; c < NCH - 1; ++c) {
+                    const int s1 = (c + 1) * CL;
+                    double w0 = lds[V_CH + s1 * NX + lane], w1 = 0.0;
 #pragma unroll
-            for (int b = 0; b < CPF - 1; ++b)
-                if (ts < K - 1) step(ab[b], fb[b]);
+                    for (int k = 0; k < NX; ++k) {
+                        const double xk = row_bcast_d(xs, k);
+                        const double f = lds[V_PHI + c * NX * NX + lane * NX + k];
+                        if (k & 1) w1 = fma(f, xk, w1); else w0 = fma(f, xk, w0);
+                    }
+                    xs = w0 + w1;
+                    lds[V_CH + s1 * NX + lane] = xs;
+                }
+            }
+            wsync();
+            x = lds[V_CH + (cact ? cs0 : 0) * NX + (ce < NX ? ce : 0)];
+#pragma unroll
+            for (int j = 0; j < QP_CLM; ++j) {
+                if (j < CL) {
+                    const int tj = cs0 + j;
+                    const double xn = chainF(x, ar[j], fr[j]);
+                    const bool ok = tj < cs1;
+                    x = ok ? xn : x;
+                    lds[(cact && ok && (tj + 1 < cs1 || tj + 1 == KS)) ? V_CH + (tj + 1) * NX + ce : C::F_SINK] = x;
+                }
+            }
+        } else {
+            // ---- forward chain xi_{t+1} = Acl_t xi_t + f_t
+            if (lane < NX) {
+                // lane i needs row i of Acl_t (stage block, B_CH + i*NX + k; Acl~ for VC)
+                const int va = (C::B_CH + lane * NX) * 8;
+                auto ldA = [&](int ts, double* an, double& fn) __attribute__((always_inline)) {
+                    const int tc = ts < K - 1 ? ts : K - 2;
+    #pragma unroll
+                    for (int k = 0; k < NX; ++k) an[k] = wb.ld(va + k * 8, FBB + tc * C::FBS * 8);
+                    fn = lds[V_G + tc * NX + lane];
+                };
+                auto chain = [&](double x, const double* ac, double f) __attribute__((always_inline)) -> double {
+                    double w0 = f, w1 = 0.0;
+    #pragma unroll
+                    for (int k = 0; k < NX; ++k) {
+                        const double xk = row_bcast_d(x, k);
+                        if (k & 1) w1 = fma(ac[k], xk, w1); else w0 = fma(ac[k], xk, w0);
+                    }
+                    return w0 + w1;
+                };
+                double x = lds[V_XI0 + lane];
+                lds[V_CH + lane] = x;
+                double ab[CPF][NX], fb[CPF];
+    #pragma unroll
+                for (int b = 0; b < CPF; ++b) ldA(b, ab[b], fb[b]);
+                int ts = 0;
+                auto step = [&](double* a, double& f) __attribute__((always_inline)) {
+                    x = chain(x, a, f);
+                    lds[V_CH + (ts + 1) * NX + lane] = x;
+                    ldA(ts + CPF, a, f);
+                    ++ts;
+                };
+                while (ts <= K - 1 - CPF) {  // CPF steps per trip, no exit inside (see the backward chain)
+    #pragma unroll
+                    for (int b = 0; b < CPF; ++b) step(ab[b], fb[b]);
+                }
+    #pragma unroll
+                for (int b = 0; b < CPF - 1; ++b)
+                    if (ts < K - 1) step(ab[b], fb[b]);
+            }
         }
         wsync();
         stamp(8);
@@ -2443,9 +2642,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
         stamp(3);
         newton(true, rcq2);
-        // step fraction: 0.99, or 0.999 once the affine predictor takes a (nearly) full step (the end
-        // game, where a 0.99 cap alone limits the gap reduction to 100x per iteration)
-        const double al = fmin(1.0, (aa >= 0.99 ? 0.999 : 0.99) * max_step(true, quad, probe));
+        // step fraction: 0.99, or QP_TAU_END once the affine predictor takes a (nearly) full step (the end
+        // game, where the fraction alone caps the gap reduction per iteration at 1 / (1 - fraction))
+        const double al = fmin(1.0, (aa >= 0.99 ? QP_TAU_END : 0.99) * max_step(true, quad, probe));
         stamp(3);
         {
             const double chk = wave_sum(al + probe);  // NaN / Inf anywhere in the direction poisons the sum

@@ -36,7 +36,7 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 template <int L>
 __device__ __forceinline__ double row_bcast_c(double v) {
     static_assert(L >= 0 && L < 16, "row lane");
-    return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + L, 0xF, 0xF, false);
+    return __builtin_amdgcn_mov_dpp(v, 0x150 + L, 0xF, 0xF, false);   // every lane written: no `old` to set up
 }
 __device__ __forceinline__ double row_bcast_d(double v, int l) {
     switch (l) {
@@ -56,6 +56,28 @@ __device__ __forceinline__ double row_bcast_d(double v, int l) {
         case 13: return row_bcast_c<13>(v);
         case 14: return row_bcast_c<14>(v);
         default: return row_bcast_c<15>(v);
+    }
+}
+
+// Lane L (< 8) of this lane's 8-lane group (lanes 8g .. 8g+7), broadcast by two bank-masked 64-bit DPP
+// row_newbcast moves: banks 0-1 of each 16-lane row (its lanes 0-7) take row lane L, banks 2-3 (lanes 8-15)
+// take row lane 8 + L.  Eight independent groups exchange in two VALU ops.
+template <int L>
+__device__ __forceinline__ double oct_bcast_c(double v) {
+    static_assert(L >= 0 && L < 8, "group lane");
+    const double lo = __builtin_amdgcn_mov_dpp(v, 0x150 + L, 0xF, 0x3, false);
+    return __builtin_amdgcn_update_dpp(lo, v, 0x158 + L, 0xF, 0xC, false);
+}
+__device__ __forceinline__ double oct_bcast_d(double v, int l) {
+    switch (l) {
+        case 0: return oct_bcast_c<0>(v);
+        case 1: return oct_bcast_c<1>(v);
+        case 2: return oct_bcast_c<2>(v);
+        case 3: return oct_bcast_c<3>(v);
+        case 4: return oct_bcast_c<4>(v);
+        case 5: return oct_bcast_c<5>(v);
+        case 6: return oct_bcast_c<6>(v);
+        default: return oct_bcast_c<7>(v);
     }
 }
 

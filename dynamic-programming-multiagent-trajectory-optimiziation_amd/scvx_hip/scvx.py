@@ -19,6 +19,28 @@ from . import (DEFAULT_NSUB, MODEL_DIMS, QPSolver, QPSpec, collision_check, coll
                foh_batched, jacobi_update)
 
 
+def balanced_order(iters, world):
+    """An agent order for `world` contiguous shards (rank r owns order[r*n:(r+1)*n]) in which every shard gets
+    the same mix of per-agent IPM iteration counts (e.g. the last step's `iters`): agents sorted by
+    iterations (descending; ties by index) are dealt to the shards in serpentine order (0..W-1, W-1..0, ...),
+    and each shard keeps its agents in ascending index order.  Under the Jacobi update every agent solves
+    against the previous iterate of all others (Distributed_opt/dist_scvx_3d.py:93-118), so which rank solves
+    which agent does not change any subproblem: the order only moves work between ranks.  A shard's QP launch
+    lasts as long as its slowest SIMD's waves, so spreading the long solves evens out the ranks once a GPU holds
+    more agents than SIMDs."""
+    import numpy as np
+    iters = np.asarray(iters)
+    N = iters.size
+    if N % world:
+        raise ValueError(f"balanced_order: {N} agents do not shard over {world} ranks")
+    idx = np.lexsort((np.arange(N), -iters))
+    rank_of = np.empty(N, np.int64)
+    for k, a in enumerate(idx):
+        rd, ps = divmod(k, world)
+        rank_of[a] = ps if rd % 2 == 0 else world - 1 - ps
+    return np.concatenate([np.nonzero(rank_of == r)[0] for r in range(world)])
+
+
 class HipBackend:
     """The product compute path: the libscvx_hip.so kernels (no CPU fallback)."""
 

@@ -230,12 +230,14 @@ struct Agent {
     Vec xref;                    // Xbar (K*n): the proximal term's centre
     Vec y;                       // dynamics multipliers (K-1)*n
     Vec y_init, y_fin;
+    double trv = 0.0;            // trust radius of this solve
 };
 
 static void setup_agent(Agent& ag, const scvx_qp_template* T, const double* disc, double sigma, const double* Xr,
                         const double* Ur, const double* x_init, const double* x_final, double trv,
                         const double* crow, const int32_t* ccount) {
     ag.T = T;
+    ag.trv = trv;
     int n = T->n_x, m = T->n_u, K = T->K, pd = T->pos_dim;
     ag.n = n; ag.m = m; ag.K = K; ag.pd = pd;
     int stride = n * (n + 2 * m + 2);
@@ -810,6 +812,10 @@ static void warm_save(const Agent& ag, double* w) {
 static void warm_point(Agent& ag, const double* w, double eta) {
     const scvx_qp_template* T = ag.T;
     const int st = warm_node_stride(T), n = ag.n, m = ag.m, K = ag.K;
+    // experiment knobs (diagnostics): floors of the trust-region facets' slack / dual relative to the radius
+    const char* ek = std::getenv("SCVX_WARM_TRK");
+    const char* el = std::getenv("SCVX_WARM_TRL");
+    const double ks = ek ? std::atof(ek) : 0.0, kl = el ? std::atof(el) : 0.0;
     for (int t = 0; t < K; ++t) {
         Node& N = ag.nd[t];
         const double* o = w + (size_t)t * st;
@@ -817,8 +823,9 @@ static void warm_point(Agent& ag, const double* w, double eta) {
         for (int r = 0; r < N.nr; ++r) {
             double v = N.h[r];
             for (int j = 0; j < N.nv; ++j) v -= N.G(r, j) * N.z[j];
-            N.s[r] = std::max(v, eta);
-            N.lam[r] = std::max(o[N.nv + r], eta);
+            const bool trf = r < (1 << m) && t < K - 1;
+            N.s[r] = std::max(v, (trf && ks > 0) ? std::min(eta, ks * ag.trv) : eta);
+            N.lam[r] = std::max(o[N.nv + r], (trf && kl > 0) ? std::min(eta, kl * ag.trv) : eta);
         }
         if (N.soc) {
             N.ssoc[0] = T->u_max;
@@ -1204,10 +1211,11 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out, const double*
                 }
             }
             if (!newton(rco, rcq, dz, ds, dl, dsq, dlq, dy, dyi, dyf)) { status = fail_status; break; }
-            // step fraction (kernel: the same rule): 0.99 of the way to the boundary, 0.999 once the
-            // affine predictor takes a (nearly) full step -- the end game, where a 0.99 cap alone
-            // limits the gap reduction to 100x per iteration
-            const double eta = (aa >= 0.99) ? 0.999 : 0.99;
+            // step fraction (kernel: the same rule, QP_TAU_END): 0.99 of the way to the boundary, 1 - 1e-5 once
+            // the affine predictor takes a (nearly) full step -- the end game, where the fraction alone caps
+            // the gap reduction per iteration at 1 / (1 - fraction).  SCVX_TAU_END: experiment knob
+            static const double tau_end = std::getenv("SCVX_TAU_END") ? std::atof(std::getenv("SCVX_TAU_END")) : 0.99999;
+            const double eta = (aa >= 0.99) ? tau_end : 0.99;
             double al = std::min(1.0, eta * max_step(ds, dl, dsq, dlq));
             if (near && al < 1e-2) { status = SCVX_STATUS_MAX_ITER; break; }  // stall at reduced accuracy (kernel)
             if (std::getenv("SCVX_DEBUG")) {

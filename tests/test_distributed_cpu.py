@@ -136,16 +136,19 @@ def test_sharded_jacobi_matches_single_process():
 N_CULL, J_MAX = 8, 2
 
 
-def _run_culled(rank, world, port, q):
+def _run_culled(rank, world, port, q, order=None):
     """The culled coupling path of the C4 / C5 configurations: the QP keeps the J_MAX nearest rows per node,
     every reference row is checked at the solution, violating agents are re-solved with all N - 1 rows
-    (j_max_hi), the global trust-region rule all-reduces the cost."""
+    (j_max_hi), the global trust-region rule all-reduces the cost.  order: agent order of the shards
+    (scvx_hip.scvx.balanced_order; rank r owns order[r*n:(r+1)*n]); None = contiguous."""
     import scvx_hip
     from scvx_hip.scvx import CouplingSpec, JacobiSCvx
     if world > 1:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     sc = _problem(N_CULL)
+    if order is not None:
+        sc = {k: (v[order] if isinstance(v, np.ndarray) and v.shape[:1] == (N_CULL,) else v) for k, v in sc.items()}
     n_loc = N_CULL // world
     sl = slice(rank * n_loc, (rank + 1) * n_loc)
     T = lambda a: torch.tensor(np.ascontiguousarray(a))
@@ -187,3 +190,40 @@ def test_sharded_culled_coupling_matches_single_process():
     for k in range(ITERS):
         for key in ("violated", "resolved", "overflow"):
             assert res[0][2][k][key] + res[1][2][k][key] == ck_single[k][key], (k, key)
+
+
+def test_balanced_shard_order_matches_single_process():
+    """Shards of a non-identity agent order (scvx_hip.scvx.balanced_order: every rank gets the same mix of
+    per-agent IPM iteration counts): gloo world 2 gives bit-identical iterates, radii and check counts to one
+    process owning all agents in that order.  Against the contiguous order the iterates agree to the
+    subproblems' accuracy, not bitwise: a node's collision rows are listed in neighbour-index order, so the order
+    changes the IPM's summation order, and the shared collision slack makes the coupled subproblem LP-like in S
+    (its minimiser is not unique).  The Jacobi update itself is order-free."""
+    from scvx_hip.scvx import balanced_order
+    iters = np.array([9, 5, 5, 12, 5, 6, 14, 5])          # e.g. the last step's IPM iterations
+    order = balanced_order(iters, 2)
+    assert sorted(order.tolist()) == list(range(N_CULL)) and not np.array_equal(order, np.arange(N_CULL))
+    assert {14, 12} & set(iters[order[:4]].tolist()) in ({14}, {12})      # the two longest solves split
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    _run_culled(0, 1, 0, q, order)
+    _, X_single, tr_single, ck_single, st = q.get()
+    assert st == 0
+    port = _free_port()
+    procs = [ctx.Process(target=_run_culled, args=(r, 2, port, q, order)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (x, tr, ck, s_)) for r, x, tr, ck, s_ in (q.get(timeout=300) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    np.testing.assert_array_equal(np.concatenate([res[0][0], res[1][0]]), X_single)
+    np.testing.assert_array_equal(np.concatenate([res[0][1], res[1][1]]), tr_single)
+    for k in range(ITERS):
+        for key in ("violated", "resolved", "overflow"):
+            assert res[0][2][k][key] + res[1][2][k][key] == ck_single[k][key], (k, key)
+    _run_culled(0, 1, 0, q)                                   # contiguous order, one process
+    _, X_contig, _, ck_contig, _ = q.get()
+    inv = np.argsort(order)
+    np.testing.assert_allclose(X_single[inv], X_contig, rtol=0, atol=1e-3)
+    assert [c["overflow"] for c in ck_single] == [c["overflow"] for c in ck_contig] == [0] * ITERS
