@@ -41,6 +41,20 @@ def device_model(model):
     return DeviceModel.from_callables(f, A, B, model.n_x, model.n_u)
 
 
+def subproblem_model(model):
+    """The device model the convex-subproblem kernels (QP / SCP) run: a built-in name, or for any other model
+    its runtime-compiled DeviceModel -- those kernels depend only on (n_x, n_u) and are instantiated for them
+    at the first solve (model_id SCVX_MODEL_RUNTIME, csrc/subproblem_rtc.hip)."""
+    return device_model(model)
+
+
+def same_device_model(a, b):
+    """Two resolved device models describe one kernel class (built-in name, or equal generated source)."""
+    if isinstance(a, str) or isinstance(b, str):
+        return a == b
+    return a is b or (a.dims == b.dims and a.source == b.source)
+
+
 def builtin_model(model, what):
     """The built-in device model name of `model`, for the kernels that are compiled per model class
     (the SCP subproblem, the inter-sample search): any other model is rejected loudly, before anything is

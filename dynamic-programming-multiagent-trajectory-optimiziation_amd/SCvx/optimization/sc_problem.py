@@ -17,7 +17,7 @@ import numpy as np
 
 import scvx_hip
 
-from ..discretization.first_order_hold import builtin_model
+from ..discretization.first_order_hold import subproblem_model
 from ..global_parameters import K as GLOBAL_K
 from .variables import Parameter, ParameterError, ProblemResult, SolverError, Variable
 
@@ -49,7 +49,9 @@ class SCProblem:
         self.n_u = model.n_u
         self.K = GLOBAL_K
         self.device = device
-        self._dev_model = builtin_model(model, "SCProblem")
+        # a built-in model name, or a user model's runtime-compiled DeviceModel: its constraint data come from
+        # model.scp_constraints() (the data of the reference's get_constraints, sc_problem.py:50)
+        self._dev_model = subproblem_model(model)
         n, m, K = self.n_x, self.n_u, self.K
         self.var = {"X": Variable((n, K), name="X"), "U": Variable((m, K), name="U"),
                     "nu": Variable((n, K - 1), name="nu"), "sigma": Variable((), name="sigma", nonneg=True)}

@@ -20,7 +20,7 @@ import numpy as np
 
 import scvx_hip
 
-from ..discretization.first_order_hold import FirstOrderHold, builtin_model
+from ..discretization.first_order_hold import FirstOrderHold, same_device_model, subproblem_model
 from ..global_parameters import CONV_TOL, MAX_ITER, TRUST_RADIUS0, WEIGHT_NU, WEIGHT_SIGMA, WEIGHT_SLACK, K
 from ..utils.logging import Logger
 from .sc_problem import SCProblem, _solver
@@ -41,9 +41,9 @@ class BatchedSCVXSolver:
         self.weight_nu = WEIGHT_NU
         self.weight_slack = WEIGHT_SLACK
         self.weight_sigma = WEIGHT_SIGMA
-        self._name = builtin_model(self.models[0], "BatchedSCVXSolver")
+        self._name = subproblem_model(self.models[0])
         for m in self.models[1:]:
-            if builtin_model(m, "BatchedSCVXSolver") != self._name:
+            if not same_device_model(subproblem_model(m), self._name):
                 raise ValueError("BatchedSCVXSolver: all agents must share one model class")
         self.problems = [SCProblem(m, device=device) for m in self.models]
         self.loggers = [Logger() for _ in self.models]
@@ -85,7 +85,8 @@ class BatchedSCVXSolver:
             lg.clear()
         self.ipm_iters = []
         for it in range(self.max_iter):
-            disc = scvx_hip.foh_batched(self._name, X, U, sigma, out=disc)
+            disc = (scvx_hip.foh_batched(self._name, X, U, sigma, out=disc) if isinstance(self._name, str)
+                    else self._name.foh(X, U, sigma, out=disc))
             out = solver.solve(disc, X, U, sigma, tr, x_init, x_final)
             Xn, Un, nun, sgn = out["X"], out["U"], out["nu"], out["sigma"].clamp_min(0.0)
             nu_norm = nun.abs().sum(-1).amax(-1)                       # induced 1-norm (scvx_solver.py:82)

@@ -7,6 +7,7 @@
 #include "qp_caps.hpp"
 #include "qp_ipm.hpp"
 #include "scvx_hip.h"
+#include "subproblem_rtc.hpp"
 
 namespace scvx {
 int qp_launch_di(int idx, const QPArgs& a, hipStream_t st);
@@ -47,8 +48,17 @@ const ModelTable* model_of(const scvx_qp_template& T) {
     return nullptr;
 }
 
-// validates the template; on success sets the model entry and the capacity class
-int qp_check(const scvx_qp_template* T, int N, const ModelTable*& mt, int& cls) {
+// the kernel class of a template: a compiled row-capacity class of a built-in model (mt, cls), or -- for
+// model_id = SCVX_MODEL_RUNTIME -- the exact class (n_x, n_u, n_box, n_obs, j_max, VC) compiled at run time
+struct QPClass {
+    const ModelTable* mt = nullptr;
+    int cls = -1;
+    bool rt = false;
+    int nx = 0, nu = 0, nb = 0, no = 0, nc = 0, vc = 0;
+};
+
+// validates the template; on success sets the class
+int qp_check(const scvx_qp_template* T, int N, QPClass& c) {
     if (!T || N < 0) return set_error(SCVX_EINVAL, "qp: null template");
     if (T->K < 2 || T->K > WAVE) return set_error(SCVX_EUNSUPPORTED, "qp: K must be in [2, 64]");
     if (T->pos_dim < 1 || T->pos_dim > 3 || T->pos_dim > T->n_x) return set_error(SCVX_EINVAL, "qp: pos_dim");
@@ -57,22 +67,34 @@ int qp_check(const scvx_qp_template* T, int N, const ModelTable*& mt, int& cls) 
     for (int b = 0; b < T->n_box; ++b)
         if (T->box_idx[b] < 0 || T->box_idx[b] >= T->n_x) return set_error(SCVX_EINVAL, "qp: box index");
     if (T->max_iter < 1) return set_error(SCVX_EINVAL, "qp: max_iter");
-    mt = model_of(*T);
-    if (!mt) return set_error(SCVX_EUNSUPPORTED, "qp: model id / dimensions");
-    cls = qp_pick_caps(mt->caps, mt->ncaps, *T);
     if (T->w_nu < 0.0 || T->w_prox < 0.0) return set_error(SCVX_EINVAL, "qp: w_nu / w_prox must be >= 0");
-    if (cls < 0)
+    c = QPClass{};
+    c.nx = T->n_x; c.nu = T->n_u;
+    if (T->model_id == SCVX_MODEL_RUNTIME) {
+        // the kernel's limits: the 3 x 3 position block (n_x >= 3), the solve chains' 16-lane broadcast and the
+        // virtual control's Gauss-Jordan over 4 n_x lanes (n_x <= 16), 2^n_u trust-region facets (n_u <= 4)
+        if (T->n_x < 3 || T->n_x > 16 || T->n_u < 1 || T->n_u > 4)
+            return set_error(SCVX_EUNSUPPORTED, "qp: runtime model needs 3 <= n_x <= 16 and 1 <= n_u <= 4");
+        if (T->j_max > 32) return set_error(SCVX_EUNSUPPORTED, "qp: j_max <= 32");
+        c.rt = true;
+        c.nb = T->n_box; c.no = T->n_obs; c.nc = T->j_max; c.vc = T->w_nu > 0.0 ? 1 : 0;
+        return SCVX_OK;
+    }
+    c.mt = model_of(*T);
+    if (!c.mt) return set_error(SCVX_EUNSUPPORTED, "qp: model id / dimensions");
+    c.cls = qp_pick_caps(c.mt->caps, c.mt->ncaps, *T);
+    if (c.cls < 0)
         return set_error(SCVX_EUNSUPPORTED, T->w_nu > 0.0
             ? "qp: no virtual-control class for this model / row counts (w_nu > 0: quad n_box <= 4, n_obs <= 16, j_max <= 32; di n_box <= 2, n_obs <= 8, no coupling)"
             : "qp: more box / obstacle / collision rows than the largest capacity class (j_max <= 32, n_obs <= 16)");
+    const int* cp = c.mt->caps + QP_CAPS_W * c.cls;
+    c.nb = cp[0]; c.no = cp[1]; c.nc = cp[2]; c.vc = cp[3];
     return SCVX_OK;
 }
 
-size_t ws_bytes(const ModelTable& mt, int cls, int N, int K) {
-    const int* c = mt.caps + QP_CAPS_W * cls;
-    const int nb = c[0], no = c[1], nc = c[2], nv = c[3] ? mt.nx : 0;
-    const int ns = no + nc, ng = no + (nc > 0 ? 1 : 0);
-    return sizeof(double) * (size_t)N * (size_t)qp_ws_doubles(mt.nx, mt.nu, nb, ns, ng, K, nv);
+size_t ws_bytes(const QPClass& c, int N, int K) {
+    const int nv = c.vc ? c.nx : 0, ns = c.no + c.nc, ng = c.no + (c.nc > 0 ? 1 : 0);
+    return sizeof(double) * (size_t)N * (size_t)qp_ws_doubles(c.nx, c.nu, c.nb, ns, ng, K, nv);
 }
 }  // namespace
 
@@ -88,10 +110,9 @@ extern "C" int scvx_qp_set_trace(double* buf, int agent, int cap) {
 }
 
 extern "C" size_t scvx_qp_workspace_bytes(const scvx_qp_template* tpl, int N) {
-    const ModelTable* mt = nullptr;
-    int cls = -1;
-    if (N <= 0 || qp_check(tpl, N, mt, cls) != SCVX_OK) return 0;
-    return ws_bytes(*mt, cls, N, tpl->K);
+    QPClass c;
+    if (N <= 0 || qp_check(tpl, N, c) != SCVX_OK) return 0;
+    return ws_bytes(c, N, tpl->K);
 }
 
 extern "C" int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const double* disc, const double* sigma,
@@ -101,9 +122,8 @@ extern "C" int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const d
                                      double* nu, double* obj, int32_t* status, int32_t* iters,
                                      const int32_t* warm, void* workspace,
                                      size_t workspace_bytes, void* stream) {
-    const ModelTable* mt = nullptr;
-    int cls = -1;
-    int rc = qp_check(tpl, N, mt, cls);
+    QPClass c;
+    int rc = qp_check(tpl, N, c);
     if (rc != SCVX_OK) return rc;
     if (N == 0) return SCVX_OK;
     if (!disc || !sigma || !Xref || !Uref || !x_init || !tr || !X || !U || !slack_coll || !obj || !status || !iters)
@@ -114,7 +134,7 @@ extern "C" int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const d
     if (tpl->j_max > 0 && (!coll_rows || !coll_count)) return set_error(SCVX_EINVAL, "qp: collision rows required");
     if (tpl->w_nu > 0.0 && !nu) return set_error(SCVX_EINVAL, "qp: nu output required (w_nu > 0)");
     if (warm && tpl->K < 2 * tpl->n_x) return set_error(SCVX_EUNSUPPORTED, "qp: warm start needs K >= 2 n_x");
-    const size_t need = ws_bytes(*mt, cls, N, tpl->K);
+    const size_t need = ws_bytes(c, N, tpl->K);
     if (!workspace || workspace_bytes < need) return set_error(SCVX_EWORKSPACE, "qp: workspace too small");
     QPArgs a{};
     a.T = *tpl;
@@ -125,5 +145,6 @@ extern "C" int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const d
     a.ws = (double*)workspace;
     a.ws_agent = (long long)(need / sizeof(double) / (size_t)N);
     a.trace = g_trace; a.trace_agent = g_trace_agent; a.trace_cap = g_trace_cap;
-    return mt->launch(cls, a, (hipStream_t)stream);
+    if (c.rt) return rtc_qp_launch(a, c.nb, c.no, c.nc, c.vc, (hipStream_t)stream);
+    return c.mt->launch(c.cls, a, (hipStream_t)stream);
 }

@@ -37,9 +37,13 @@
 // Factor outputs other than Acl go to stage-minor workspace columns (ws[col * 64 + t]) that the
 // lane-parallel passes read coalesced.
 #pragma once
+#ifndef __HIPCC_RTC__   // (this header is also compiled at run time for user models: csrc/subproblem_rtc.hip)
 #include <hip/hip_runtime.h>
 
 #include "common.hpp"
+#endif
+#include <type_traits>
+
 #include "scvx_hip.h"
 #include "wave_ops.hpp"
 
@@ -97,6 +101,17 @@ constexpr int qp_fbs(int nx, int nu, int nv = 0) { return 3 * nu * nx + nu * nu 
 // what its nodes touch (C3: 1024 agents x 199 KB stay inside the 256 MB Infinity Cache)
 constexpr long long qp_ws_doubles(int nx, int nu, int nb, int ns, int ng, int K, int nv = 0) {
     return (long long)K * (qp_ncol(nx, nu, nb, ns, ng, nv) + qp_gpk(nx, nu, nv) + qp_fbs(nx, nu, nv));
+}
+// LDS doubles of a class (QPCfg::lds_doubles, written out for the host of a runtime-compiled class, which
+// has no QPCfg instantiation; QPCfg asserts that both agree)
+constexpr int qp_lds_doubles(int nx, int nu, int nb, int no, int nc, int vc, int K) {
+    const int nv = vc ? nx : 0;
+    const int pkt = qp_pkt(nx, nu, nv);
+    const int f_sink = pkt + 5 * nx * nx + 5 * nx * nu + nu * nu;
+    const int f_end = qp_even(f_sink + (nx > 8 ? nx : 8) + 4 * nv * nx);
+    const int nr = (1 << nu) + 2 * nb + no + nc + no + (nc > 0 ? 1 : 0);
+    const int l_var = qp_even(f_end + 2 * nx * nx + 8 * nx + 1 + 4) + 16 + 2 * nr * 64;
+    return l_var + K * nx + (K + 1) * nx + (nx <= 8 ? 8 * nx * nx : 0);
 }
 // byte offset of every access of a lane without a node (t >= K): beyond num_records of any workspace
 constexpr int QP_OOB = 0x40000000;
@@ -225,6 +240,7 @@ struct QPCfg {
     // then (chunked solve chains, NX <= 8) the chunk transition matrices Phi_c [QP_NCH][NX][NX]
     static constexpr bool CHK = NX <= 8;
     static constexpr int lds_doubles(int K) { return L_VAR + K * NX + (K + 1) * NX + (CHK ? QP_NCH * NX * NX : 0); }
+    static_assert(lds_doubles(50) == qp_lds_doubles(NX, NU, NB, NO, NC, VC, 50), "host LDS formula");
     static_assert(4 * NV <= WAVE, "virtual control: one Gauss-Jordan column per lane");
 };
 
@@ -2761,6 +2777,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     }
 }
 
+#ifndef __HIPCC_RTC__
 // launch helpers (qp_capi.hip picks the instantiation)
 template <class C>
 int qp_launch(const QPArgs& a, hipStream_t st) {
@@ -2769,5 +2786,6 @@ int qp_launch(const QPArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(qp_ipm_kernel<C>, dim3(a.N), dim3(WAVE), lds, st, a);
     return check_launch("qp_ipm_kernel");
 }
+#endif
 
 }  // namespace scvx

@@ -4,7 +4,9 @@
 // order, so lanes of the wave exchange data through LDS without a hardware barrier: a phase
 // boundary only needs the compiler not to move LDS accesses across it (wsync).
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
+#endif
 
 namespace scvx {
 

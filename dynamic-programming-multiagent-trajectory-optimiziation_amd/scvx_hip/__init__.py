@@ -25,7 +25,7 @@ from ._lib import MODEL_DIMS, MODEL_IDS, STATUS, QPTemplate, SCPTemplate, ScvxEr
 DEFAULT_NSUB = {"di": 1, "si": 1, "unicycle": 16, "quad": 16}
 QUAD_PARAMS = (1.0, 9.81, 0.02, 0.02, 0.04)
 
-__all__ = ["foh_batched", "integrate_nonlinear", "collision_rows", "collision_check", "qp_solve_batched", "QPSpec", "SCPSpec", "SCPSolver", "slab_update",
+__all__ = ["model_dims", "model_id", "default_nsub", "foh_batched", "integrate_nonlinear", "collision_rows", "collision_check", "qp_solve_batched", "QPSpec", "SCPSpec", "SCPSolver", "slab_update",
            "intersample_batched",
            "disc_stride", "unpack_disc", "ScvxError", "MODEL_DIMS", "DEFAULT_NSUB"]
 
@@ -55,15 +55,36 @@ def _dev(t, dtype=None, name="tensor"):
     return ctypes.c_void_p(t.data_ptr())
 
 
+def model_dims(model):
+    """(n_x, n_u) of a built-in model name or of a runtime-compiled model (scvx_hip.rtc.DeviceModel, `.dims`)."""
+    if isinstance(model, str):
+        return MODEL_DIMS[model]
+    dims = getattr(model, "dims", None)
+    if dims is None:
+        raise TypeError(f"model must be a built-in name {sorted(MODEL_DIMS)} or a scvx_hip.rtc.DeviceModel")
+    return tuple(dims)
+
+
+def model_id(model):
+    """The template's model_id: the built-in id, or SCVX_MODEL_RUNTIME for a runtime-compiled model (the QP and
+    SCP kernels are then instantiated for its dimensions at the first solve)."""
+    return MODEL_IDS[model] if isinstance(model, str) else _lib.SCVX_MODEL_RUNTIME
+
+
+def default_nsub(model):
+    """RK4 substeps of the FOH: the built-in table, 16 for a user model (as the nonlinear built-ins)."""
+    return DEFAULT_NSUB[model] if isinstance(model, str) else 16
+
+
 def disc_stride(model):
-    n, m = MODEL_DIMS[model]
+    n, m = model_dims(model)
     return n * (n + 2 * m + 2)
 
 
 def unpack_disc(disc, model):
     """[..., K-1, n(n+2m+2)] -> (A_bar, B_bar, C_bar, S_bar, z_bar) in the reference's F-order
     column layout (..., n*n, K-1) etc. (first_order_hold.py:20-24, 75-85)."""
-    n, m = MODEL_DIMS[model]
+    n, m = model_dims(model)
     o = [0, n * n, n * n + n * m, n * n + 2 * n * m, n * n + 2 * n * m + n, n * n + 2 * n * m + 2 * n]
     return tuple(disc[..., o[i]:o[i + 1]].transpose(-1, -2) for i in range(5))
 
@@ -206,11 +227,11 @@ class QPSpec:
     w_prox: float = 0.0
 
     def to_c(self):
-        n, m = MODEL_DIMS[self.model]
+        n, m = model_dims(self.model)
         if self.w_final < 0 or (self.w_final > 0 and self.has_final):
             raise ValueError("QPSpec: w_final > 0 (soft terminal) needs has_final=False")
         t = QPTemplate()
-        t.model_id, t.n_x, t.n_u, t.K, t.pos_dim = MODEL_IDS[self.model], n, m, self.K, self.pos_dim
+        t.model_id, t.n_x, t.n_u, t.K, t.pos_dim = model_id(self.model), n, m, self.K, self.pos_dim
         t.has_final, t.fix_last_input, t.ineq_last = int(self.has_final), int(self.fix_last_input), int(self.ineq_last)
         t.w_last = self.w_last
         if len(self.box) > _lib.SCVX_MAX_BOX or len(self.obs) > _lib.SCVX_MAX_OBS:
@@ -243,7 +264,7 @@ class QPSolver:
         self.ctpl = spec.to_c()
         nbytes = lib().scvx_qp_workspace_bytes(ctypes.byref(self.ctpl), N)
         self.workspace = torch.empty(max(nbytes // 8, 1), dtype=torch.float64, device=device)
-        n, m = MODEL_DIMS[spec.model]
+        n, m = model_dims(spec.model)
         K = spec.K
         self.X = torch.empty((N, K, n), dtype=torch.float64, device=device)
         self.U = torch.empty((N, K, m), dtype=torch.float64, device=device)
@@ -262,7 +283,7 @@ class QPSolver:
         """Host-side shape checks: the kernel indexes every buffer with the template's compile-time
         dimensions, so a mis-shaped tensor would be read out of bounds on the device."""
         spec, N = self.spec, (self.N if N is None else N)
-        n, m = MODEL_DIMS[spec.model]
+        n, m = model_dims(spec.model)
         K = spec.K
         want = {"disc": (disc, (N, K - 1, disc_stride(spec.model))), "sigma": (sigma, (N,)),
                 "Xref": (Xref, (N, K, n)), "Uref": (Uref, (N, K, m)), "x_init": (x_init, (N, n)),
@@ -362,9 +383,9 @@ class SCPSpec:
     r_slab: float = 0.0
 
     def to_c(self):
-        n, m = MODEL_DIMS[self.model]
+        n, m = model_dims(self.model)
         t = SCPTemplate()
-        t.model_id, t.n_x, t.n_u, t.K, t.pos_dim = MODEL_IDS[self.model], n, m, int(self.K), int(self.pos_dim)
+        t.model_id, t.n_x, t.n_u, t.K, t.pos_dim = model_id(self.model), n, m, int(self.K), int(self.pos_dim)
         t.has_final, t.pin_u_first, t.pin_u_last = int(self.has_final), int(self.pin_u_first), int(self.pin_u_last)
         if len(self.u_bounds) > _lib.SCVX_MAX_BOX or len(self.x_bounds) > _lib.SCVX_MAX_BOX:
             raise ValueError("too many bound constraints")
@@ -412,7 +433,7 @@ class SCPSolver:
         self.ctpl = spec.to_c()
         nbytes = lib().scvx_scp_workspace_bytes(ctypes.byref(self.ctpl), N)
         self.workspace = torch.empty(max(nbytes // 8, 1), dtype=torch.float64, device=device)
-        n, m = MODEL_DIMS[spec.model]
+        n, m = model_dims(spec.model)
         K, f64 = spec.K, torch.float64
         self.X = torch.empty((N, K, n), dtype=f64, device=device)
         self.U = torch.empty((N, K, m), dtype=f64, device=device)

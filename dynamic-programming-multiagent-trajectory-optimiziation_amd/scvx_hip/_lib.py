@@ -16,6 +16,7 @@ SCVX_MAX_BOX, SCVX_MAX_OBS, SCVX_MAX_NBR = 4, 16, 32
 SCVX_IS_MAX_PROJ, SCVX_IS_MAX_STATE = 3, 12
 MODEL_IDS = {"di": 0, "unicycle": 1, "si": 2, "quad": 3}
 MODEL_DIMS = {"di": (6, 3), "unicycle": (3, 2), "si": (3, 3), "quad": (12, 4)}
+SCVX_MODEL_RUNTIME = 255   # any other model: the subproblem kernels are compiled for its (n_x, n_u) at run time
 STATUS = {0: "optimal", 1: "optimal_inaccurate", 2: "solver_error"}
 
 # every symbol declared in include/scvx_hip.h
@@ -26,7 +27,7 @@ EXPORTS = ("scvx_version", "scvx_last_error", "scvx_foh_batched", "scvx_integrat
            "scvx_intersample_batched", "scvx_admm_consensus_batched", "scvx_scp_game_solve_batched",
            "scvx_slab_update_batched", "scvx_jacobi_update_batched", "scvx_rtc_model_create",
            "scvx_rtc_model_source", "scvx_rtc_model_log", "scvx_rtc_model_destroy", "scvx_rtc_foh_batched",
-           "scvx_rtc_integrate_nonlinear_batched")
+           "scvx_rtc_integrate_nonlinear_batched", "scvx_rtc_subproblem_compile")
 SCVX_MAX_MODEL_PARAMS, SCVX_RTC_MAX_NX, SCVX_RTC_MAX_NU = 16, 16, 8
 
 
@@ -109,6 +110,7 @@ def lib():
         L.scvx_collision_rows_batched.argtypes = [i32, i32, i32, i32, vp, i32, i32, dbl, dbl, i32, vp, vp, vp]
         L.scvx_collision_rows_indexed.argtypes = [i32, i32, i32, i32, vp, vp, i32, dbl, dbl, i32, vp, vp, vp]
         L.scvx_collision_check_batched.argtypes = [i32, i32, i32, i32, vp, i32, i32, dbl, vp, vp, dbl, vp, vp, vp]
+        L.scvx_rtc_subproblem_compile.argtypes = [i32, vp, i32, vp]
         L.scvx_scp_workspace_bytes.argtypes = [ctypes.POINTER(SCPTemplate), i32]
         L.scvx_scp_workspace_bytes.restype = sz
         L.scvx_scp_solve_batched.argtypes = [ctypes.POINTER(SCPTemplate), i32] + [vp] * 19 + [vp, sz, vp]

@@ -15,8 +15,8 @@ import dataclasses
 from dataclasses import dataclass
 from typing import Optional
 
-from . import (DEFAULT_NSUB, MODEL_DIMS, QPSolver, QPSpec, collision_check, collision_rows, collision_rows_indexed,
-               foh_batched, jacobi_update)
+from . import (QPSolver, QPSpec, collision_check, collision_rows, collision_rows_indexed, default_nsub, foh_batched,
+               jacobi_update, model_dims)
 
 
 def balanced_order(iters, world):
@@ -45,7 +45,9 @@ class HipBackend:
     """The product compute path: the libscvx_hip.so kernels (no CPU fallback)."""
 
     def foh(self, model, X, U, sigma, nsub, out):
-        return foh_batched(model, X, U, sigma, nsub=nsub, out=out)
+        if isinstance(model, str):
+            return foh_batched(model, X, U, sigma, nsub=nsub, out=out)
+        return model.foh(X, U, sigma, nsub=nsub, out=out)   # a runtime-compiled model (scvx_hip.rtc.DeviceModel)
 
     def collision_rows(self, X_all, i0, n_local, R, j_max, pos_dim, cull, rows, count):
         return collision_rows(X_all, i0, n_local, R, j_max, pos_dim, cull, rows, count)
@@ -120,11 +122,11 @@ class JacobiSCvx:
         self.on_fail, self.tr_max = on_fail, float(tr0 if tr_max is None else tr_max)
         self.fused_update = fused_update
         self.tie_rtol = float(tie_rtol)
-        self.warm_start = warm_start and spec.K >= 2 * MODEL_DIMS[spec.model][0]
+        self.warm_start = warm_start and spec.K >= 2 * model_dims(spec.model)[0]
         self.warm = None   # (N,) int32 device: the previous solve of the agent qualifies as a warm start
         self.warm_max_status = int(warm_max_status)
         self.group = group
-        self.nsub = nsub or DEFAULT_NSUB[spec.model]
+        self.nsub = nsub or default_nsub(spec.model)
         self.solver = self.backend.qp_solver(spec, self.N, self.device)
         self.tr = torch.full((self.N,), float(tr0), dtype=torch.float64, device=self.device)
         self.prev_cost = torch.full((self.N,), float("inf"), dtype=torch.float64, device=self.device)
@@ -139,7 +141,7 @@ class JacobiSCvx:
         self.i0 = self.rank * self.N
         self.N_total = self.N * self.world
         if coupling is not None:
-            n, _ = MODEL_DIMS[spec.model]
+            n, _ = model_dims(spec.model)
             self.X_all = torch.empty((self.N_total, spec.K, n), dtype=torch.float64, device=self.device)
             self.rows = torch.zeros((self.N, spec.K, spec.j_max, spec.pos_dim + 1), dtype=torch.float64,
                                     device=self.device)

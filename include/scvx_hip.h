@@ -18,7 +18,9 @@
 #ifndef SCVX_HIP_H
 #define SCVX_HIP_H
 
+#ifndef __HIPCC_RTC__  /* hipRTC (runtime-compiled kernels of user models) provides size_t itself */
 #include <stddef.h>
+#endif
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -38,6 +40,9 @@ extern "C" {
 #define SCVX_MODEL_UNICYCLE 1          /* n=3,  m=2  SCvx/models/unicycle_model.py:54-63   */
 #define SCVX_MODEL_SINGLE_INTEGRATOR 2 /* n=3,  m=3  SCvx/models/single_integrator_model.py:54-57 */
 #define SCVX_MODEL_QUADROTOR 3         /* n=12, m=4  build-defined           */
+/* any other model: n_x / n_u taken from the template; the subproblem kernels (QP, SCP) are compiled for
+   those dimensions at the first solve (hipRTC) -- the user-model path of scvx_rtc_model_create */
+#define SCVX_MODEL_RUNTIME 255
 
 /* per-agent solver status (maps to cvxpy.OPTIMAL / OPTIMAL_INACCURATE / ...) */
 #define SCVX_STATUS_OPTIMAL 0
@@ -106,6 +111,14 @@ int scvx_rtc_foh_batched(const scvx_rtc_model* model, const double* params, int 
 int scvx_rtc_integrate_nonlinear_batched(const scvx_rtc_model* model, const double* params, int n_params,
                                          int K, int N, const double* X, const double* U, const double* sigma,
                                          int nsub, int piecewise, double* Xout, void* stream);
+
+/* Compile (no GPU needed) the subproblem kernel a SCVX_MODEL_RUNTIME template is served by, into the
+ * process-wide code-object cache the first solve would fill (a warm-up / a build check of user classes):
+ *   kind 0  the trust-region QP (scvx_qp_solve_batched), cls = {n_x, n_u, n_box, n_obs, j_max class, VC}
+ *   kind 1  the SCProblem (scvx_scp_solve_batched),       cls = {n_x, n_u, n_extra, waves per agent}
+ * (the class ints of csrc/qp_capi.hip / csrc/scp_ipm.hip).  *code_bytes (optional) = code-object size.
+ * SCVX_EINVAL with the compiler log in scvx_last_error() on a compile error. */
+int scvx_rtc_subproblem_compile(int kind, const int* cls, int ncls, size_t* code_bytes);
 
 /* ------------------------------------------------------------------------------------------
  * Batched trust-region subproblem (one per agent), the convex solve the reference hands to

@@ -7,8 +7,9 @@
     generate no code; a bad expression fails loudly with the compiler log;
   * symbolic re-tracing of numpy callables: reference-style sympy-lambdified models, the drop-in
     model classes (hand-written numpy), finite-difference Jacobians (differentiated from f);
-  * the drop-in FirstOrderHold routes a custom model to the runtime path, and the per-class kernels
-    (SCProblem, BatchedSCVXSolver) reject it loudly.
+  * the drop-in FirstOrderHold routes a custom model to the runtime path; SCProblem / BatchedSCVXSolver take
+    it too (their kernels are instantiated for its dimensions at run time: tests/test_rtc_subproblem_gpu.py),
+    the inter-sample search (built-in models only) rejects it loudly.
 """
 import glob
 import os
@@ -161,6 +162,26 @@ def test_first_order_hold_routes_custom_models():
     car.scvx_device_model = dm
     assert device_model(car) is dm
     with pytest.raises(NotImplementedError, match="runtime-compiled FOH path only"):
-        builtin_model(car, "SCProblem")
-    with pytest.raises(NotImplementedError):
-        SCProblem(car)
+        builtin_model(car, "segment_minima")            # the inter-sample search: built-in models only
+    sp = SCProblem(car)                                 # the subproblem kernels take any (n_x, n_u) (hipRTC)
+    assert sp._dev_model is dm
+    from SCvx.discretization.first_order_hold import same_device_model
+    assert same_device_model(dm, device_model(cm.KinematicCar())) and not same_device_model(dm, "unicycle")
+
+
+@pytest.mark.parametrize("kind,cls", [(0, (4, 2, 2, 1, 0, 0)), (1, (4, 2, 0, 2))], ids=["qp_car", "scp_car"])
+def test_runtime_subproblem_kernels_compile_without_gpu(kind, cls):
+    """The subproblem kernels a user model's template is served by (model_id SCVX_MODEL_RUNTIME) compile
+    through hipRTC from the headers embedded in the library (the classes tests/test_rtc_subproblem_gpu.py
+    launches: the kinematic car's QP with 2 box rows + 1 obstacle, its SCProblem on 2 waves)."""
+    import ctypes
+    from scvx_hip import _lib
+    L = _lib.lib()
+    f = L.scvx_rtc_subproblem_compile
+    f.restype = ctypes.c_int
+    arr = (ctypes.c_int * len(cls))(*cls)
+    nbytes = ctypes.c_size_t(0)
+    rc = f(kind, arr, len(cls), ctypes.byref(nbytes))
+    assert rc == 0, L.scvx_last_error().decode()
+    assert nbytes.value > 10000
+    assert f(0, arr, 3, None) != 0                     # wrong class length fails loudly
