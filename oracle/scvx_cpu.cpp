@@ -462,7 +462,32 @@ static void riccati_factor(const Agent& ag, const std::vector<Mat>& H, Riccati& 
             }
         }
         Mat L = Rh;
-        if (!chol(L)) {
+        // LDL' of Rh with the kernel's rule (phase 3): pivots that rounding pushed below 1e-13 max|diag| are
+        // clamped there (Rh is a Schur complement that loses definiteness at extreme barrier scalings: an active
+        // trust-region facet adds D g g' with D ~ 1e12, whose sum with the O(1e-4) objective curvature cannot be
+        // represented); NaN is fatal
+        bool chol_ok;
+        {
+            double dmax = 0.0;
+            for (int j = 0; j < m; ++j) dmax = std::max(dmax, std::fabs(L(j, j)));
+            const double dmin = 1e-13 * dmax + 1e-300;
+            chol_ok = dmax == dmax;
+            for (int j = 0; j < m; ++j) {
+                double d = L(j, j);
+                for (int k = 0; k < j; ++k) d -= L(j, k) * L(j, k);
+                chol_ok = chol_ok && d == d;
+                if (!(d > dmin)) d = dmin;
+                d = std::sqrt(d);
+                L(j, j) = d;
+                for (int i = j + 1; i < m; ++i) {
+                    double v = L(i, j);
+                    for (int k = 0; k < j; ++k) v -= L(i, k) * L(j, k);
+                    L(i, j) = v / d;
+                }
+                for (int i = 0; i < j; ++i) L(i, j) = 0.0;
+            }
+        }
+        if (!chol_ok) {
             if (std::getenv("SCVX_DEBUG")) {
                 std::fprintf(stderr, "   chol(Rh) failed at stage %d:", t);
                 for (int i = 0; i < m; ++i) std::fprintf(stderr, " %.3e", Rh(i, i));

