@@ -132,10 +132,15 @@ def make_coupled(config, world, rank, device):
     if N_total % world:
         raise SystemExit(f"{config}: {N_total} agents do not shard over {world} ranks")
     n_loc = N_total // world
-    sl = slice(rank * n_loc, (rank + 1) * n_loc)
-    t = {k: torch.tensor(np.ascontiguousarray(sc[k][sl]), device=device)
-         for k in ("X", "U", "x_init", "x_final", "sigma")}
+    t = shard_tensors(sc, np.arange(rank * n_loc, (rank + 1) * n_loc), device)
     return sc, t, dict(model=model, R=R, obs=obs, box=box, j_max=j_max, N_total=N_total, n_loc=n_loc, vc=vc)
+
+
+def shard_tensors(sc, idx, device):
+    """The agents `idx` of a coupled construction (a contiguous block, or a balanced order's block) on device."""
+    import torch
+    return {k: torch.tensor(np.ascontiguousarray(sc[k][idx]), device=device)
+            for k in ("X", "U", "x_init", "x_final", "sigma")}
 
 
 def host_info():
@@ -499,6 +504,8 @@ def main():
     ap.add_argument("--agents", type=int, default=N_AGENTS, help="c3: agents per GPU")
     ap.add_argument("--cpu-sample", type=int, default=1024)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--balance", action="store_true",
+                    help="c4/c5 at --gpus > 1: deal agents to ranks by their first-step IPM iterations (DESIGN §6)")
     ap.add_argument("--tol", type=float, default=1e-8,
                     help="IPM relative stopping tolerance; default = Clarabel's defaults (tol_feas = tol_gap_rel = "
                          "1e-8), the solver of the reference's dist_scvx_3d.py:110")
@@ -523,7 +530,7 @@ def main():
     import torch
     import torch.distributed as dist
     import scvx_hip
-    from scvx_hip.scvx import CouplingSpec, JacobiSCvx
+    from scvx_hip.scvx import CouplingSpec, JacobiSCvx, balanced_order
 
     if world > 1:
         torch.cuda.set_device(local)
@@ -553,6 +560,18 @@ def main():
                                tol=args.tol, max_iter=60, **cfg["vc"])
         drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, coupling=CouplingSpec(R=cfg["R"]),
                          tr_rule="global", warm_max_status=args.warm_status)
+        if args.balance and world > 1:
+            # one untimed step on contiguous shards measures every agent's IPM iterations; the shards are then
+            # re-dealt so each rank gets the same mix (scvx_hip.scvx.balanced_order), and the run
+            # restarts from the initial iterate on the new shards (the warmup steps follow as usual)
+            _, _, out0 = drv.step(w["X"].clone(), w["U"].clone())
+            it_loc = out0["iters"].to(torch.int32).contiguous()
+            allit = [torch.empty_like(it_loc) for _ in range(world)]
+            dist.all_gather(allit, it_loc)
+            order = balanced_order(torch.cat(allit).cpu().numpy(), world)
+            w = shard_tensors(sc, order[rank * N:(rank + 1) * N], device)
+            drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, coupling=CouplingSpec(R=cfg["R"]),
+                             tr_rule="global", warm_max_status=args.warm_status)
     it_state = [w["X"].clone(), w["U"].clone()]   # the current iterate (X, U), rebound every step
 
     def step(marks=None):
@@ -659,7 +678,9 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": data,
-            "config": {"workload": workload, "agents_per_gpu": N, "K": K, "parallelism": f"agents sharded x{world}"},
+            "config": {"workload": workload, "agents_per_gpu": N, "K": K,
+                       "parallelism": f"agents sharded x{world}" + (" (balanced order)" if (args.balance and world > 1
+                                                                         and args.config != "c3") else "")},
             "roofline": {"bound": "fp64_valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                          "traffic_unit": "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE; warm-started launches as in the "

@@ -91,7 +91,7 @@ constexpr int qp_ncol(int nx, int nu, int nb, int ns, int ng, int nv = 0) {
     // warm-start state (row duals, initial / terminal multipliers)
     return qp_dstr(nx, nu) + nx * nu + 4 * ns + 4 * ng + (nx + nu) + ng + ((1 << nu) + 2 * nb + ns + ng) + nu +
            ((nx + nu) + nx + 2 * (nu + 1) + ng) + (3 * (nu + 1) + 1 + (nu + 1)) + 11 * nv +
-           ((1 << nu) + 2 * nb + ns + ng) + 1;
+           ((1 << nu) + 2 * nb + ns + ng) + 1 + (nx > 8 ? 2 * ((1 << nu) + 2 * nb + ns + ng) : 0);
 }
 // factor outputs per stage (stage-major block): K, kappa, LD, W2, P, Pi, u, Acl, [virtual control: G^-1 P,
 // G^-1 Pi, G^-1, Acl~], one junk slot (the global store of lanes without an output of their own)
@@ -110,7 +110,7 @@ constexpr int qp_lds_doubles(int nx, int nu, int nb, int no, int nc, int vc, int
     const int f_sink = pkt + 5 * nx * nx + 5 * nx * nu + nu * nu;
     const int f_end = qp_even(f_sink + (nx > 8 ? nx : 8) + 4 * nv * nx);
     const int nr = (1 << nu) + 2 * nb + no + nc + no + (nc > 0 ? 1 : 0);
-    const int l_var = qp_even(f_end + 2 * nx * nx + 8 * nx + 1 + 4) + 16 + 2 * nr * 64;
+    const int l_var = qp_even(f_end + 2 * nx * nx + 8 * nx + 1 + 4) + 16 + (nx > 8 ? 0 : 2 * nr * 64);
     return l_var + K * nx + (K + 1) * nx + (nx <= 8 ? 8 * nx * nx : 0);
 }
 // byte offset of every access of a lane without a node (t >= K): beyond num_records of any workspace
@@ -220,7 +220,11 @@ struct QPCfg {
     // warm start: the row duals lambda_r at the last iterate (NR), and y_init (lanes 0..NX-1) / y_fin (lanes
     // NX..2NX-1) in one column (needs K >= 2 NX: the host checks)
     static constexpr int C_WL = C_VRD + 2 * NV, C_WY = C_WL + NR;
-    static constexpr int NCOL = C_WY + 1;
+    // row slacks / duals: LDS [r][lane] for n <= 8; for the n = 12 classes workspace columns (their 49 rows
+    // took 50 KB of LDS per agent, two waves per CU; in columns the class runs four)
+    static constexpr bool ROWG = NX > 8;
+    static constexpr int C_RS = C_WY + 1, C_RL = C_RS + (ROWG ? NR : 0);
+    static constexpr int NCOL = C_RL + (ROWG ? NR : 0);
     static_assert(NCOL == qp_ncol(NX, NU, NB, NS, NG, NV), "column count");
     // LDS (doubles, compile-time offsets except the K-sized blocks at the end):
     // factor: the current stage's packet, P', Pi' (col-major), T1, T2 (col-major), W1, W2 (col-major), Qh,
@@ -235,7 +239,8 @@ struct QPCfg {
     static constexpr int L_M = F_END, L_PI0 = L_M + NX * NX, L_XE = L_PI0 + NX * NX, L_XI0 = L_XE + NX,
                          L_R2F = L_XI0 + NX, L_YI = L_R2F + NX, L_YF = L_YI + NX, L_DYI = L_YF + NX,
                          L_DYF = L_DYI + NX, L_PIV = L_DYF + NX, L_ONE = L_PIV + NX, L_FLAG = L_ONE + 1,
-                         L_ST = qp_even(L_FLAG + 4), L_S = L_ST + 16, L_L = L_S + NR * 64, L_VAR = L_L + NR * 64;
+                         L_ST = qp_even(L_FLAG + 4), L_S = L_ST + 16, L_L = L_S + (NX > 8 ? 0 : NR * 64),
+                         L_VAR = L_L + (NX > 8 ? 0 : NR * 64);
     // row slacks s / duals lambda [r][lane]; then K-sized: chain offsets g/f [K][NX], chain vectors [K+1][NX];
     // then (chunked solve chains, NX <= 8) the chunk transition matrices Phi_c [QP_NCH][NX][NX]
     static constexpr bool CHK = NX <= 8;
@@ -629,81 +634,104 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         // phase descriptors (rebuilt per call: nothing of them stays live outside the sweep)
         constexpr int E1 = 2 * NX * NX + 2 * NX * NU + 2 * NX, E2 = NX * NX + NU * NX + NU * NU, E4 = 4 * NX * NX;
         constexpr int R1 = (E1 + WAVE - 1) / WAVE, R2 = (E2 + WAVE - 1) / WAVE, R4 = (E4 + WAVE - 1) / WAVE;
-        int d1[R1][4], d2[R2][4], d4[R4][4];
-        {
+        // descriptors of repetition `rep` of lane `ln` (out: L, R, O, B packed as qp_decode reads them)
+        auto fill1 = [&](int ln, int rep, int (&d)[4]) __attribute__((always_inline)) {
             const int sink = C::F_SINK;
+            int o = ln + rep * WAVE, L = 0, R = 0, O = -1, B = 0;
+            if (o < NX * NX) {  // T1 = P' A  -> T1 column-major
+                const int i = o / NX, j = o % NX;
+                L = qp_dpk(C::F_PP + i * NX, 0); R = qp_dpk(C::P_A + j * NX, 1); O = C::F_T1 + j * NX + i;
+            } else if ((o -= NX * NX) < NX * NU) {  // T2 = P' Bt -> column-major
+                const int i = o / NU, j = o % NU;
+                L = qp_dpk(C::F_PP + i * NX, 0); R = qp_dpk(C::P_BT + j * NX, 1); O = C::F_T2 + j * NX + i;
+            } else if ((o -= NX * NU) < NX * NX) {  // W1 = A' Pi'   (I at the last stage)
+                const int i = o / NX, j = o % NX;
+                L = qp_dpk(C::P_A + i * NX, 1); R = qp_dpk(C::F_PIP + j * NX, 0); O = C::F_W1 + o;
+                B = (i == j) ? (V_ONE | (2 << 16)) : 0;
+            } else if ((o -= NX * NX) < NU * NX) {  // W2 = Bt' Pi' -> column-major (C_{K-2}' at the last stage)
+                const int i = o / NX, j = o % NX;
+                L = qp_dpk(C::P_BT + i * NX, 1); R = qp_dpk(C::F_PIP + j * NX, 0);
+                O = (C::F_W2 + j * NU + i) | ((C::B_W2 + o + 1) << 17);
+                B = (C::P_C + i * NX + j) | (1 << 15) | (2 << 16);
+            } else if ((o -= NU * NX) < NX) {  // u = P' e  (global only)
+                L = qp_dpk(C::F_PP + o * NX, 0); R = qp_dpk(C::P_E, 1); O = sink | ((C::B_U + o + 1) << 17);
+            } else if ((o -= NX) < NX) {  // xe += Pi'' e
+                L = qp_dpk(C::F_PIP + o * NX, 0); R = qp_dpk(C::P_E, 1); O = (V_XE + o) | (1 << 15);
+            }
+            d[0] = L; d[1] = R; d[2] = O; d[3] = B;
+        };
+        auto fill2 = [&](int ln, int rep, int (&d)[4]) __attribute__((always_inline)) {
+            int o = ln + rep * WAVE, L = 0, R = 0, O = -1, B = 0;
+            if (o < NX * NX) {  // Qh = Q + A' T1 (symmetric: (min, max) element for both halves)
+                const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
+                L = qp_dpk(C::P_A + p * NX, 1); R = qp_dpk(C::F_T1 + q * NX, 0); O = C::F_QH + o;
+                B = (C::P_Q + p * NX + q) | (1 << 15) | (1 << 16);
+            } else if ((o -= NX * NX) < NU * NX) {  // Sh = S' + Bt' T1 -> column-major
+                const int i = o / NX, j = o % NX;
+                L = qp_dpk(C::P_BT + i * NX, 1); R = qp_dpk(C::F_T1 + j * NX, 0); O = C::F_SH + j * NU + i;
+                B = (C::P_S + j * NU + i) | (1 << 15) | (1 << 16);
+            } else if ((o -= NU * NX) < NU * NU) {  // Rh = R + Bt' T2
+                const int i = o / NU, j = o % NU, p = i < j ? i : j, q = i < j ? j : i;
+                L = qp_dpk(C::P_BT + p * NX, 1); R = qp_dpk(C::F_T2 + q * NX, 0); O = C::F_RH + o;
+                B = (C::P_R + p * NU + q) | (1 << 15) | (1 << 16);
+            }
+            d[0] = L; d[1] = R; d[2] = O; d[3] = B;
+        };
+        auto fill4 = [&](int ln, int rep, int (&d)[4]) __attribute__((always_inline)) {
+            const int sink = C::F_SINK;
+            int o = ln + rep * WAVE, L = 0, R = 0, O = -1, B = 0;
+            if (o < NX * NX) {  // P = Qh + Sh' K (symmetric)
+                const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
+                L = qp_dpk(C::F_SH + p * NU, 0); R = qp_dpk(C::F_KK + q * NU, 0);
+                O = (C::F_PP + o) | ((C::B_P + o + 1) << 17); B = (C::F_QH + p * NX + q) | (1 << 16);
+            } else if ((o -= NX * NX) < NX * NX) {  // Pi = W1 + Sh' kappa -> Pi' column-major
+                const int i = o / NX, j = o % NX;
+                L = qp_dpk(C::F_SH + i * NU, 0); R = qp_dpk(C::F_KK + (NX + j) * NU, 0);
+                O = (C::F_PIP + j * NX + i) | ((C::B_PI + o + 1) << 17); B = (C::F_W1 + o) | (1 << 16);
+            } else if ((o -= NX * NX) < NX * NX) {  // M += W2' kappa (symmetric)
+                const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
+                L = qp_dpk(C::F_W2 + p * NU, 0); R = qp_dpk(C::F_KK + (NX + q) * NU, 0); O = (V_M + o) | (1 << 15);
+            } else if ((o -= NX * NX) < NX * NX) {  // Acl = A + Bt K  -> global (+ LDS column-major for VC)
+                const int i = o / NX, j = o % NX;
+                L = qp_dpk(C::P_BTR + i * NU, 1); R = qp_dpk(C::F_KK + j * NU, 0);
+                O = (C::NV > 0 ? C::F_ACLC + j * NX + i : sink) | ((C::B_ACL + o + 1) << 17);
+                B = (C::P_A + j * NX + i) | (1 << 15) | (1 << 16);
+            }
+            d[0] = L; d[1] = R; d[2] = O; d[3] = B;
+        };
+        // n = 12 classes (CMP): the 20 repetitions' descriptors are rebuilt inside every stage from an opaque
+        // lane index instead of being held across the sweep (120 registers that spilled to scratch in the
+        // factor's inner loop); the n <= 8 classes decode them once per sweep
+        constexpr bool CMP = NX > 8;
+        int d1[CMP ? 1 : R1][4], d2[CMP ? 1 : R2][4], d4[CMP ? 1 : R4][4];
+        if constexpr (!CMP) {
             const int ln = qp_opaque(lane);  // volatile: keeps the descriptors inside the IPM loop
 #pragma unroll
-            for (int rep = 0; rep < R1; ++rep) {
-                int o = ln + rep * WAVE, L = 0, R = 0, O = -1, B = 0;
-                if (o < NX * NX) {  // T1 = P' A  -> T1 column-major
-                    const int i = o / NX, j = o % NX;
-                    L = qp_dpk(C::F_PP + i * NX, 0); R = qp_dpk(C::P_A + j * NX, 1); O = C::F_T1 + j * NX + i;
-                } else if ((o -= NX * NX) < NX * NU) {  // T2 = P' Bt -> column-major
-                    const int i = o / NU, j = o % NU;
-                    L = qp_dpk(C::F_PP + i * NX, 0); R = qp_dpk(C::P_BT + j * NX, 1); O = C::F_T2 + j * NX + i;
-                } else if ((o -= NX * NU) < NX * NX) {  // W1 = A' Pi'   (I at the last stage)
-                    const int i = o / NX, j = o % NX;
-                    L = qp_dpk(C::P_A + i * NX, 1); R = qp_dpk(C::F_PIP + j * NX, 0); O = C::F_W1 + o;
-                    B = (i == j) ? (V_ONE | (2 << 16)) : 0;
-                } else if ((o -= NX * NX) < NU * NX) {  // W2 = Bt' Pi' -> column-major (C_{K-2}' at the last stage)
-                    const int i = o / NX, j = o % NX;
-                    L = qp_dpk(C::P_BT + i * NX, 1); R = qp_dpk(C::F_PIP + j * NX, 0);
-                    O = (C::F_W2 + j * NU + i) | ((C::B_W2 + o + 1) << 17);
-                    B = (C::P_C + i * NX + j) | (1 << 15) | (2 << 16);
-                } else if ((o -= NU * NX) < NX) {  // u = P' e  (global only)
-                    L = qp_dpk(C::F_PP + o * NX, 0); R = qp_dpk(C::P_E, 1); O = sink | ((C::B_U + o + 1) << 17);
-                } else if ((o -= NX) < NX) {  // xe += Pi'' e
-                    L = qp_dpk(C::F_PIP + o * NX, 0); R = qp_dpk(C::P_E, 1); O = (V_XE + o) | (1 << 15);
-                }
-                d1[rep][0] = L; d1[rep][1] = R; d1[rep][2] = O; d1[rep][3] = B;
-            }
+            for (int rep = 0; rep < R1; ++rep) fill1(ln, rep, d1[rep]);
 #pragma unroll
-            for (int rep = 0; rep < R2; ++rep) {
-                int o = ln + rep * WAVE, L = 0, R = 0, O = -1, B = 0;
-                if (o < NX * NX) {  // Qh = Q + A' T1 (symmetric: (min, max) element for both halves)
-                    const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
-                    L = qp_dpk(C::P_A + p * NX, 1); R = qp_dpk(C::F_T1 + q * NX, 0); O = C::F_QH + o;
-                    B = (C::P_Q + p * NX + q) | (1 << 15) | (1 << 16);
-                } else if ((o -= NX * NX) < NU * NX) {  // Sh = S' + Bt' T1 -> column-major
-                    const int i = o / NX, j = o % NX;
-                    L = qp_dpk(C::P_BT + i * NX, 1); R = qp_dpk(C::F_T1 + j * NX, 0); O = C::F_SH + j * NU + i;
-                    B = (C::P_S + j * NU + i) | (1 << 15) | (1 << 16);
-                } else if ((o -= NU * NX) < NU * NU) {  // Rh = R + Bt' T2
-                    const int i = o / NU, j = o % NU, p = i < j ? i : j, q = i < j ? j : i;
-                    L = qp_dpk(C::P_BT + p * NX, 1); R = qp_dpk(C::F_T2 + q * NX, 0); O = C::F_RH + o;
-                    B = (C::P_R + p * NU + q) | (1 << 15) | (1 << 16);
-                }
-                d2[rep][0] = L; d2[rep][1] = R; d2[rep][2] = O; d2[rep][3] = B;
-            }
+            for (int rep = 0; rep < R2; ++rep) fill2(ln, rep, d2[rep]);
 #pragma unroll
-            for (int rep = 0; rep < R4; ++rep) {
-                int o = ln + rep * WAVE, L = 0, R = 0, O = -1, B = 0;
-                if (o < NX * NX) {  // P = Qh + Sh' K (symmetric)
-                    const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
-                    L = qp_dpk(C::F_SH + p * NU, 0); R = qp_dpk(C::F_KK + q * NU, 0);
-                    O = (C::F_PP + o) | ((C::B_P + o + 1) << 17); B = (C::F_QH + p * NX + q) | (1 << 16);
-                } else if ((o -= NX * NX) < NX * NX) {  // Pi = W1 + Sh' kappa -> Pi' column-major
-                    const int i = o / NX, j = o % NX;
-                    L = qp_dpk(C::F_SH + i * NU, 0); R = qp_dpk(C::F_KK + (NX + j) * NU, 0);
-                    O = (C::F_PIP + j * NX + i) | ((C::B_PI + o + 1) << 17); B = (C::F_W1 + o) | (1 << 16);
-                } else if ((o -= NX * NX) < NX * NX) {  // M += W2' kappa (symmetric)
-                    const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
-                    L = qp_dpk(C::F_W2 + p * NU, 0); R = qp_dpk(C::F_KK + (NX + q) * NU, 0); O = (V_M + o) | (1 << 15);
-                } else if ((o -= NX * NX) < NX * NX) {  // Acl = A + Bt K  -> global (+ LDS column-major for VC)
-                    const int i = o / NX, j = o % NX;
-                    L = qp_dpk(C::P_BTR + i * NU, 1); R = qp_dpk(C::F_KK + j * NU, 0);
-                    O = (C::NV > 0 ? C::F_ACLC + j * NX + i : sink) | ((C::B_ACL + o + 1) << 17);
-                    B = (C::P_A + j * NX + i) | (1 << 15) | (1 << 16);
-                }
-                d4[rep][0] = L; d4[rep][1] = R; d4[rep][2] = O; d4[rep][3] = B;
-            }
+            for (int rep = 0; rep < R4; ++rep) fill4(ln, rep, d4[rep]);
         }
-        // decoded once per sweep; accumulating outputs (xe, M) are summed in registers
-        constexpr bool CMP = NX > 8;   // compact repetitions (QPRepC) for the n = 12 classes
-        using Rep = typename std::conditional<CMP, QPRepC, QPRep>::type;
-        Rep q1[R1], q2[R2], q4[R4];
+        // decoded once per sweep (n <= 8); accumulating outputs (xe, M) are summed in registers
+        QPRep q1[CMP ? 1 : R1], q2[CMP ? 1 : R2], q4[CMP ? 1 : R4];
         double a1[R1], a2[R2], a4[R4];
+        // n = 12: the compact repetitions of one phase, decoded where the phase runs
+        auto dec1 = [&](QPRepC (&q)[R1]) __attribute__((always_inline)) {
+            const int ln = qp_opaque(lane);
+#pragma unroll
+            for (int r = 0; r < R1; ++r) { int d[4]; fill1(ln, r, d); q[r] = qp_decode_c(d, V_ONE, C::F_SINK, C::B_JNK); }
+        };
+        auto dec2 = [&](QPRepC (&q)[R2]) __attribute__((always_inline)) {
+            const int ln = qp_opaque(lane);
+#pragma unroll
+            for (int r = 0; r < R2; ++r) { int d[4]; fill2(ln, r, d); q[r] = qp_decode_c(d, V_ONE, C::F_SINK, C::B_JNK); }
+        };
+        auto dec4 = [&](QPRepC (&q)[R4]) __attribute__((always_inline)) {
+            const int ln = qp_opaque(lane);
+#pragma unroll
+            for (int r = 0; r < R4; ++r) { int d[4]; fill4(ln, r, d); q[r] = qp_decode_c(d, V_ONE, C::F_SINK, C::B_JNK); }
+        };
         // virtual control: the M contributions -Pi'' G^-1 Pi' of every stage (registers, like a4)
         constexpr int R0 = (NX * NX + WAVE - 1) / WAVE;
         double amv[R0];
@@ -711,20 +739,17 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         for (int r = 0; r < R0; ++r) amv[r] = 0.0;
 #pragma unroll
         for (int r = 0; r < R1; ++r) {
-            if constexpr (CMP) q1[r] = qp_decode_c(d1[r], V_ONE, C::F_SINK, C::B_JNK);
-            else q1[r] = qp_decode(d1[r], V_ONE, C::F_SINK, C::B_JNK);
+            if constexpr (!CMP) q1[r] = qp_decode(d1[r], V_ONE, C::F_SINK, C::B_JNK);
             a1[r] = 0.0;
         }
 #pragma unroll
         for (int r = 0; r < R2; ++r) {
-            if constexpr (CMP) q2[r] = qp_decode_c(d2[r], V_ONE, C::F_SINK, C::B_JNK);
-            else q2[r] = qp_decode(d2[r], V_ONE, C::F_SINK, C::B_JNK);
+            if constexpr (!CMP) q2[r] = qp_decode(d2[r], V_ONE, C::F_SINK, C::B_JNK);
             a2[r] = 0.0;
         }
 #pragma unroll
         for (int r = 0; r < R4; ++r) {
-            if constexpr (CMP) q4[r] = qp_decode_c(d4[r], V_ONE, C::F_SINK, C::B_JNK);
-            else q4[r] = qp_decode(d4[r], V_ONE, C::F_SINK, C::B_JNK);
+            if constexpr (!CMP) q4[r] = qp_decode(d4[r], V_ONE, C::F_SINK, C::B_JNK);
             a4[r] = 0.0;
         }
         for (int e = lane; e < NX * NX; e += WAVE) { lds[C::F_PP + e] = 0.0; lds[C::F_PIP + e] = 0.0; lds[V_M + e] = 0.0; }
@@ -734,8 +759,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         // packets stream through one LDS slot (a stage's packet is overwritten by the next one after its
         // last read), loads issued 3 stages ahead (register buffers pf[0..2], so the stage loop is
         // unrolled by 3 to keep their indices static)
-        // prefetch distance: 3 stages; 2 for the n = 12 classes (9 doubles per buffer, register pressure)
-        constexpr int FPD = NX > 8 ? 2 : 3;
+        // prefetch distance: 3 stages; 1 for the n = 12 classes (9 doubles per buffer: the deeper buffers were
+        // spilled to scratch in the stage loop, and a stage there outlasts a packet load anyway)
+        constexpr int FPD = NX > 8 ? 1 : 3;
         double pf[FPD][PFN];
         // lane's global packet element per prefetch slot (structural zeros read past the end: 0)
         int pfo[PFN];
@@ -762,11 +788,14 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             pf_load(K - 3, pf[2]);
             pf_store(K - 1, pf[0]);
             pf_load(K - 4, pf[0]);
-        } else {
+        } else if constexpr (FPD == 2) {
             pf_load(K - 1, pf[0]);
             pf_load(K - 2, pf[1]);
             pf_store(K - 1, pf[0]);
             pf_load(K - 3, pf[0]);
+        } else {
+            pf_load(K - 1, pf[0]);
+            pf_store(K - 1, pf[0]);
         }
         wsync();
         bool bad = false;
@@ -833,11 +862,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 wsync();
             }
             // ---- phase 1: T1 = P'A, T2 = P'Bt, W1 = A'Pi', W2 = Bt'Pi', u = P'e, xe += Pi''e
-            if constexpr (CMP) qp_phase_c<NX, R1, E1 - NX, E1>(lds, q1, blast, wb, fbo, a1);
+            if constexpr (CMP) { QPRepC qc[R1]; dec1(qc); qp_phase_c<NX, R1, E1 - NX, E1>(lds, qc, blast, wb, fbo, a1); }
             else qp_phase<NX, R1>(lds, q1, blast, wb, fbo, a1);
             wsync();
             // ---- phase 2: Qh = Q + A'T1, Sh = S' + Bt'T1, Rh = R + Bt'T2
-            if constexpr (CMP) qp_phase_c<NX, R2, 0, 0>(lds, q2, blast, wb, fbo, a2);
+            if constexpr (CMP) { QPRepC qc[R2]; dec2(qc); qp_phase_c<NX, R2, 0, 0>(lds, qc, blast, wb, fbo, a2); }
             else qp_phase<NX, R2>(lds, q2, blast, wb, fbo, a2);
             wsync();
             // ---- phase 3: Rh = L D L' in registers (every lane); [K | kappa] = -Rh^-1 [Sh | W2]
@@ -918,7 +947,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             }
             wsync();
             // ---- phase 4: P = Qh + Sh'K, Pi = W1 + Sh'kappa, M += W2'kappa, Acl = A + Bt K
-            if constexpr (CMP) qp_phase_c<NU, R4, 2 * NX * NX, 3 * NX * NX>(lds, q4, blast, wb, fbo, a4);
+            if constexpr (CMP) { QPRepC qc[R4]; dec4(qc); qp_phase_c<NU, R4, 2 * NX * NX, 3 * NX * NX>(lds, qc, blast, wb, fbo, a4); }
             else qp_phase<NU, R4>(lds, q4, blast, wb, fbo, a4);
             if (ts > 0) pf_store(ts - 1, cb);
             wsync();
@@ -933,7 +962,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 wsync();
             }
         };
-        // stage K-1's packet is in LDS, K-2 in pf[1], K-3 in pf[2], K-4 in pf[0]
+        // (FPD = 3) stage K-1's packet is in LDS, K-2 in pf[1], K-3 in pf[2], K-4 in pf[0]
         int ts = K - 1;
         if constexpr (FPD == 3) {
             stage(ts, pf[0], pf[1]);  // (its load of K-4 went out before the loop)
@@ -946,7 +975,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 stage(ts, pf[0], pf[1]);
                 --ts;
             }
-        } else {  // LDS: K-1, pf[1]: K-2, pf[0]: K-3 (in flight)
+        } else if constexpr (FPD == 2) {  // LDS: K-1, pf[1]: K-2, pf[0]: K-3 (in flight)
             stage(ts, pf[0], pf[1]);
             --ts;
             while (ts >= 0) {
@@ -955,16 +984,21 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 stage(ts, pf[0], pf[1]);
                 --ts;
             }
+        } else {  // LDS: K-1; each stage loads ts-1 into pf[0] and stores it to the ring at its end
+            for (; ts >= 0; --ts) stage(ts, pf[0], pf[0]);
         }
         if (bad) lds[V_FLAG] = 1.0;  // any lane (all agree)
         // the register-accumulated outputs (xe, M) to their LDS homes
         if constexpr (CMP) {
+            QPRepC c1[R1], c4[R4];
+            dec1(c1);
+            dec4(c4);
 #pragma unroll
             for (int r = 0; r < R1; ++r)
-                if (WAVE * r < E1 && WAVE * r + WAVE > E1 - NX && (q1[r].F & 4)) lds[q1[r].O] = a1[r];
+                if (WAVE * r < E1 && WAVE * r + WAVE > E1 - NX && (c1[r].F & 4)) lds[c1[r].O] = a1[r];
 #pragma unroll
             for (int r = 0; r < R4; ++r)
-                if (WAVE * r < 3 * NX * NX && WAVE * r + WAVE > 2 * NX * NX && (q4[r].F & 4)) lds[q4[r].O] = a4[r];
+                if (WAVE * r < 3 * NX * NX && WAVE * r + WAVE > 2 * NX * NX && (c4[r].F & 4)) lds[c4[r].O] = a4[r];
         } else {
 #pragma unroll
             for (int r = 0; r < R1; ++r)
@@ -1615,13 +1649,37 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     // ------------------------------------------------------------------ node state (workspace)
     // Phase-local register copies: every node phase loads what it uses as one batch and stores
     // what it changes, so no node-sized state is live across the sweeps.
-    double z[NZ], y[NX], sq[NQ], lq[NQ], av[NGA], ub[NU], sg[NSA][3], sb[NSA];
+    // soft rows (g0, g1, g2, b) of this node: registers for up to 8 rows; above that (the 16- and 48-row classes,
+    // whose node state would not fit the register file next to them) every use re-reads its workspace column
+    // (an opaque offset per load: no load is merged with another and kept live across the phase)
+    constexpr bool SGS = NS > 8;
+    constexpr int NSR = SGS ? 1 : NSA;
+    double z[NZ], y[NX], sq[NQ], lq[NQ], av[NGA], ub[NU], sg[NSR][3], sb[NSR];
+    auto sgv = [&](int q, int i) __attribute__((always_inline)) -> double {
+        if constexpr (SGS) return wb.ld(qp_opaque(vt), (C::C_SOFT + q * 4 + i) * colb);
+        else return i < 3 ? sg[q][i] : sb[q];
+    };
     // virtual control state of this node (VC classes, lanes t < K-1): nu, e, and per component the slacks /
     // duals of the rows nu - e <= 0 (index 2i) and -nu - e <= 0 (2i + 1)
     double vn[NVA], ve[NVA], vs[2 * NVA], vl[2 * NVA];
     // row slacks s_r and duals lambda_r of this node: LDS [r][lane]
-    auto s_ = [&](int r) __attribute__((always_inline)) -> double& { return lds[V_S + r * WAVE + lane]; };
-    auto l_ = [&](int r) __attribute__((always_inline)) -> double& { return lds[V_L + r * WAVE + lane]; };
+    // (n = 12 classes: workspace columns C_RS / C_RL, C::ROWG)
+    auto s_ = [&](int r) __attribute__((always_inline)) -> double {
+        if constexpr (C::ROWG) return cld(C::C_RS + r);
+        else return lds[V_S + r * WAVE + lane];
+    };
+    auto l_ = [&](int r) __attribute__((always_inline)) -> double {
+        if constexpr (C::ROWG) return cld(C::C_RL + r);
+        else return lds[V_L + r * WAVE + lane];
+    };
+    auto s_set = [&](int r, double v) __attribute__((always_inline)) {
+        if constexpr (C::ROWG) cst(C::C_RS + r, v);
+        else lds[V_S + r * WAVE + lane] = v;
+    };
+    auto l_set = [&](int r, double v) __attribute__((always_inline)) {
+        if constexpr (C::ROWG) cst(C::C_RL + r, v);
+        else lds[V_L + r * WAVE + lane] = v;
+    };
     int bidx[NBA];
     auto issue_state = [&]() __attribute__((always_inline)) {
 #pragma unroll
@@ -1635,7 +1693,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
         for (int j = 0; j < NU; ++j) ub[j] = cld(C::C_UB + j);
 #pragma unroll
-        for (int q = 0; q < NS; ++q) {
+        for (int q = 0; q < (SGS ? 0 : NS); ++q) {
 #pragma unroll
             for (int i = 0; i < 3; ++i) sg[q][i] = cld(C::C_SOFT + q * 4 + i);
             sb[q] = cld(C::C_SOFT + q * 4 + 3);
@@ -1652,7 +1710,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         hold(z, NZ); hold(y, NX); hold(sq, NQ); hold(lq, NQ); hold(av, NGA); hold(ub, NU);
         if (NV > 0) { hold(vn, NV); hold(ve, NV); hold(vs, 2 * NV); hold(vl, 2 * NV); }
 #pragma unroll
-        for (int q = 0; q < NS; ++q) { hold(sg[q], 3); hold(&sb[q], 1); }
+        for (int q = 0; q < (SGS ? 0 : NS); ++q) { hold(sg[q], 3); hold(&sb[q], 1); }
 #pragma unroll
         for (int b = 0; b < NB; ++b) bidx[b] = qp_opaque(T.box_idx[b]);
     };
@@ -1708,8 +1766,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             gz = lo ? -xi : xi; h = lo ? -T.box_lo[b] : T.box_hi[b];
         } else if (r < C::R_GRP) {
             const int q = r - C::R_OBS, g = q < NO ? q : NO;
-            gz = -(sg[q][0] * zz[0] + sg[q][1] * zz[1] + sg[q][2] * zz[2]) - aa[g];
-            h = -sb[q];
+            gz = -(sgv(q, 0) * zz[0] + sgv(q, 1) * zz[1] + sgv(q, 2) * zz[2]) - aa[g];
+            h = -sgv(q, 3);
         } else {
             gz = -aa[r - C::R_GRP]; h = 0.0;
         }
@@ -1726,7 +1784,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         } else if (r < C::R_GRP) {
             const int q = r - C::R_OBS, g = q < NO ? q : NO;
 #pragma unroll
-            for (int i = 0; i < 3; ++i) gzv[i] -= c * sg[q][i];
+            for (int i = 0; i < 3; ++i) gzv[i] -= c * sgv(q, i);
             gav[g] -= c;
         } else {
             gav[r - C::R_GRP] -= c;
@@ -1774,7 +1832,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 const int q = r - C::R_OBS, g = q < NO ? q : NO;
                 Haa[g] += Dr;
 #pragma unroll
-                for (int i = 0; i < 3; ++i) Hpa[g][i] += Dr * sg[q][i];
+                for (int i = 0; i < 3; ++i) Hpa[g][i] += Dr * sgv(q, i);
             } else {
                 Haa[r - C::R_GRP] += Dr;
                 D0[r - C::R_GRP] = Dr;
@@ -1807,7 +1865,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             const int q = r - C::R_OBS, g = q < NO ? q : NO;
             double c[3];
 #pragma unroll
-            for (int i = 0; i < 3; ++i) c[i] = sg[q][i] - hp[g][i];
+            for (int i = 0; i < 3; ++i) c[i] = sgv(q, i) - hp[g][i];
 #pragma unroll
             for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -1915,18 +1973,19 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     };
     // dynamics residual rp_t = x_{t+1} - A x_t - B u_t - C u_{t+1} - S sigma - z  (lane t < K-1)
     // (dt: this node's transposed disc row, batch-loaded by the caller)
-    auto dyn_residual = [&](const double* zz, const double* dt, double* rp) __attribute__((always_inline)) {
+    // (dt(e): element e of the row -- a register copy, or for n = 12 a load per use)
+    auto dyn_residual = [&](const double* zz, auto dt, double* rp) __attribute__((always_inline)) {
         double zn[NZ];
 #pragma unroll
         for (int i = 0; i < NZ; ++i) zn[i] = __shfl_down(zz[i], 1, WAVE);
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
-            double v = zn[i] - fma(dt[NX * NX + 2 * NX * NU + i], sig, dt[NX * NX + 2 * NX * NU + NX + i]);
+            double v = zn[i] - fma(dt(NX * NX + 2 * NX * NU + i), sig, dt(NX * NX + 2 * NX * NU + NX + i));
 #pragma unroll
-            for (int k = 0; k < NX; ++k) v -= dt[k * NX + i] * zz[k];
+            for (int k = 0; k < NX; ++k) v -= dt(k * NX + i) * zz[k];
 #pragma unroll
             for (int j = 0; j < NU; ++j)
-                v -= dt[NX * NX + j * NX + i] * zz[NX + j] + dt[NX * NX + NX * NU + j * NX + i] * zn[NX + j];
+                v -= dt(NX * NX + j * NX + i) * zz[NX + j] + dt(NX * NX + NX * NU + j * NX + i) * zn[NX + j];
             rp[i] = (t < K - 1) ? v : 0.0;
         }
     };
@@ -1993,8 +2052,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             double gz, h;
             row_eval(r, z, av, gz, h);
             const bool on = row_on(r);
-            s_(r) = on ? fmax(h - gz, QP_WARM_ETA) : 1.0;
-            l_(r) = on ? fmax(wl[r], QP_WARM_ETA) : 0.0;
+            s_set(r, on ? fmax(h - gz, QP_WARM_ETA) : 1.0);
+            l_set(r, on ? fmax(wl[r], QP_WARM_ETA) : 0.0);
         }
         if (soc) {
             double nu2 = 0.0, nl2 = 0.0;
@@ -2019,17 +2078,21 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     // minimiser of 1/2 z'Pz + q'z + 1/2 ||Gz - h||^2 s.t. Az = b from z_ref (aux = 0), unit scaling
     // (CVXOPT coneqp initialisation; oracle/qp_dense.py does the same on the dense form)
         fresh();
-        double dt[C::DSTR];
+        constexpr bool DSTRM = NX > 8;   // n = 12: the 264-double disc row is read per use, not held
+        double dt[DSTRM ? 1 : C::DSTR];
         issue_state();
-        ldn(dt, C::C_DT, C::DSTR);
+        if constexpr (!DSTRM) ldn(dt, C::C_DT, C::DSTR);
         hold_state();
-        hold(dt, C::DSTR);
+        if constexpr (!DSTRM) hold(dt, C::DSTR);
 #pragma unroll
-        for (int r = 0; r < NR; ++r) { s_(r) = 1.0; l_(r) = 0.0; }
+        for (int r = 0; r < NR; ++r) { s_set(r, 1.0); l_set(r, 0.0); }
         double Wu[NU * NU], rp[NX];
 #pragma unroll
         for (int e = 0; e < NU * NU; ++e) Wu[e] = (e / NU == e % NU) ? 1.0 : 0.0;
-        dyn_residual(z, dt, rp);
+        dyn_residual(z, [&](int e) __attribute__((always_inline)) -> double {
+            if constexpr (DSTRM) return wb.ld(qp_opaque(vt), (C::C_DT + e) * colb);
+            else return dt[e];
+        }, rp);
         assemble(true, Wu, rp);
         double r1[NZ], r1a[NGA];
 #pragma unroll
@@ -2071,8 +2134,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             double gz, h;
             row_eval(r, z, av, gz, h);
             const bool on = row_on(r);
-            s_(r) = on ? h - gz : 1.0;
-            l_(r) = on ? gz - h : 0.0;
+            s_set(r, on ? h - gz : 1.0);
+            l_set(r, on ? gz - h : 0.0);
             if (on) { smin = fmin(smin, h - gz); lmin = fmin(lmin, gz - h); }
         }
 #pragma unroll
@@ -2098,7 +2161,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         const double shs = fmax(0.0, 1.0 - smin), shl = fmax(0.0, 1.0 - lmin);
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
-            if (row_on(r)) { s_(r) += shs; l_(r) += shl; }
+            if (row_on(r)) { s_set(r, s_(r) + shs); l_set(r, l_(r) + shl); }
         }
         if (soc) { sq[0] += shs; lq[0] += shl; }
 #pragma unroll
@@ -2125,13 +2188,16 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         // doubles) is never live next to the iterate: that peak made the C3 class spill.  The second
         // chunk's loads are issued once the first chunk is dead (one extra round trip per iteration).
         fresh();
-        double Cpr[NX * NU], dA[NX * NX], dSz[2 * NX];
+        // n = 12 classes: A (NX^2 = 144 doubles) is not held in registers; it is read one column at a time
+        // (below, once the multiplier terms of rd are in), in the same summation order
+        constexpr bool ASTR = NX > 8;
+        double Cpr[NX * NU], dA[ASTR ? 1 : NX * NX], dSz[2 * NX];
         issue_state();
-        ldn(dA, C::C_DT, NX * NX);
+        if constexpr (!ASTR) ldn(dA, C::C_DT, NX * NX);
         ldn(dSz, C::C_DT + NX * NX + 2 * NX * NU, 2 * NX);
         load_cp(Cpr);
         hold_state();
-        hold(dA, NX * NX);
+        if constexpr (!ASTR) hold(dA, NX * NX);
         hold(dSz, 2 * NX);
         double zn[NZ];
 #pragma unroll
@@ -2141,8 +2207,10 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
             double v = zn[i] - fma(dSz[i], sig, dSz[NX + i]);
+            if constexpr (!ASTR) {
 #pragma unroll
-            for (int k = 0; k < NX; ++k) v -= dA[k * NX + i] * z[k];
+                for (int k = 0; k < NX; ++k) v -= dA[k * NX + i] * z[k];
+            }
             rp[i] = v;
         }
         // dual residual rd = Pz + q + A'y + G'lam (z and group parts)
@@ -2213,11 +2281,25 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                         for (int i = 0; i < NX; ++i) rd[NX + j] -= Cpr[j * NX + i] * ym[i];
                 }
-                if (t < K - 1) {
+                if (t < K - 1 && !ASTR) {
 #pragma unroll
                     for (int k = 0; k < NX; ++k)
 #pragma unroll
                         for (int i = 0; i < NX; ++i) rd[k] -= dA[k * NX + i] * y[i];
+                }
+            }
+            if constexpr (ASTR) {   // column k of A: rp -= A(:, k) x_k, rd_k -= A(:, k)' y (orders as above)
+                const bool ay = act && t < K - 1;
+#pragma unroll
+                for (int k = 0; k < NX; ++k) {
+                    double col[NX];
+                    const int vo = qp_opaque(vt);
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) col[i] = wb.ld(vo, (C::C_DT + k * NX + i) * colb);
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) rp[i] -= col[i] * z[k];
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) rd[k] -= ay ? col[i] * y[i] : 0.0;
                 }
             }
         }
@@ -2688,8 +2770,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             if (row_on(r)) {
                 double dsr, dlr;
                 row_dir(r, true, dsr, dlr);
-                s_(r) += al * dsr;
-                l_(r) += al * dlr;
+                s_set(r, s_(r) + al * dsr);
+                l_set(r, l_(r) + al * dlr);
             }
         }
         if constexpr (NV > 0) {
