@@ -332,7 +332,8 @@ __device__ __forceinline__ double qp_dot(const double* lds, int L, int R) {
 // (out = base + sum_k L[k] R[k]), writes each to its LDS slot and its global column, and adds the
 // accumulating ones (M, xe: summed over the stages) into registers -- no LDS read-modify-write on the
 // sweep's chain.
-template <int KK, int NREP>
+// (outputs [ALO, AHI) of the phase may accumulate: only the repetitions covering them keep a register sum)
+template <int KK, int NREP, int ALO = 0, int AHI = WAVE * NREP>
 __device__ __forceinline__ void qp_phase(double* lds, const QPRep (&d)[NREP], double blast, const QPBuf& wb, int fbo,
                                          double (&areg)[NREP]) {
     double val[NREP];
@@ -342,7 +343,7 @@ __device__ __forceinline__ void qp_phase(double* lds, const QPRep (&d)[NREP], do
 #pragma unroll
     for (int r = 0; r < NREP; ++r) {
         lds[d[r].O] = val[r];
-        areg[r] = fma(d[r].acc, val[r], areg[r]);
+        if (WAVE * r < AHI && WAVE * r + WAVE > ALO) areg[r] = fma(d[r].acc, val[r], areg[r]);
         wb.st(d[r].G, fbo, val[r]);
     }
 }
@@ -527,6 +528,19 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
     };
 
+    // diagnostics build (-DQP_PHASE_TRACE): the factor's four phases per stage into V_ST[11..14] (no memory drain)
+    auto pstamp = [&](int i) __attribute__((always_inline)) {
+#ifdef QP_PHASE_TRACE
+        if (stamp_on) {
+            const long long now = __builtin_amdgcn_s_memtime();
+            if (lane == 0) lds[V_ST + i] += (double)(now - tprev);
+            tprev = now;
+        }
+#else
+        (void)i;
+#endif
+    };
+
     // ------------------------------------------------------------------ setup (once per solve)
     {
         double Cp[NX * NU];
@@ -634,104 +648,81 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         // phase descriptors (rebuilt per call: nothing of them stays live outside the sweep)
         constexpr int E1 = 2 * NX * NX + 2 * NX * NU + 2 * NX, E2 = NX * NX + NU * NX + NU * NU, E4 = 4 * NX * NX;
         constexpr int R1 = (E1 + WAVE - 1) / WAVE, R2 = (E2 + WAVE - 1) / WAVE, R4 = (E4 + WAVE - 1) / WAVE;
-        // descriptors of repetition `rep` of lane `ln` (out: L, R, O, B packed as qp_decode reads them)
-        auto fill1 = [&](int ln, int rep, int (&d)[4]) __attribute__((always_inline)) {
+        int d1[R1][4], d2[R2][4], d4[R4][4];
+        {
             const int sink = C::F_SINK;
-            int o = ln + rep * WAVE, L = 0, R = 0, O = -1, B = 0;
-            if (o < NX * NX) {  // T1 = P' A  -> T1 column-major
-                const int i = o / NX, j = o % NX;
-                L = qp_dpk(C::F_PP + i * NX, 0); R = qp_dpk(C::P_A + j * NX, 1); O = C::F_T1 + j * NX + i;
-            } else if ((o -= NX * NX) < NX * NU) {  // T2 = P' Bt -> column-major
-                const int i = o / NU, j = o % NU;
-                L = qp_dpk(C::F_PP + i * NX, 0); R = qp_dpk(C::P_BT + j * NX, 1); O = C::F_T2 + j * NX + i;
-            } else if ((o -= NX * NU) < NX * NX) {  // W1 = A' Pi'   (I at the last stage)
-                const int i = o / NX, j = o % NX;
-                L = qp_dpk(C::P_A + i * NX, 1); R = qp_dpk(C::F_PIP + j * NX, 0); O = C::F_W1 + o;
-                B = (i == j) ? (V_ONE | (2 << 16)) : 0;
-            } else if ((o -= NX * NX) < NU * NX) {  // W2 = Bt' Pi' -> column-major (C_{K-2}' at the last stage)
-                const int i = o / NX, j = o % NX;
-                L = qp_dpk(C::P_BT + i * NX, 1); R = qp_dpk(C::F_PIP + j * NX, 0);
-                O = (C::F_W2 + j * NU + i) | ((C::B_W2 + o + 1) << 17);
-                B = (C::P_C + i * NX + j) | (1 << 15) | (2 << 16);
-            } else if ((o -= NU * NX) < NX) {  // u = P' e  (global only)
-                L = qp_dpk(C::F_PP + o * NX, 0); R = qp_dpk(C::P_E, 1); O = sink | ((C::B_U + o + 1) << 17);
-            } else if ((o -= NX) < NX) {  // xe += Pi'' e
-                L = qp_dpk(C::F_PIP + o * NX, 0); R = qp_dpk(C::P_E, 1); O = (V_XE + o) | (1 << 15);
-            }
-            d[0] = L; d[1] = R; d[2] = O; d[3] = B;
-        };
-        auto fill2 = [&](int ln, int rep, int (&d)[4]) __attribute__((always_inline)) {
-            int o = ln + rep * WAVE, L = 0, R = 0, O = -1, B = 0;
-            if (o < NX * NX) {  // Qh = Q + A' T1 (symmetric: (min, max) element for both halves)
-                const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
-                L = qp_dpk(C::P_A + p * NX, 1); R = qp_dpk(C::F_T1 + q * NX, 0); O = C::F_QH + o;
-                B = (C::P_Q + p * NX + q) | (1 << 15) | (1 << 16);
-            } else if ((o -= NX * NX) < NU * NX) {  // Sh = S' + Bt' T1 -> column-major
-                const int i = o / NX, j = o % NX;
-                L = qp_dpk(C::P_BT + i * NX, 1); R = qp_dpk(C::F_T1 + j * NX, 0); O = C::F_SH + j * NU + i;
-                B = (C::P_S + j * NU + i) | (1 << 15) | (1 << 16);
-            } else if ((o -= NU * NX) < NU * NU) {  // Rh = R + Bt' T2
-                const int i = o / NU, j = o % NU, p = i < j ? i : j, q = i < j ? j : i;
-                L = qp_dpk(C::P_BT + p * NX, 1); R = qp_dpk(C::F_T2 + q * NX, 0); O = C::F_RH + o;
-                B = (C::P_R + p * NU + q) | (1 << 15) | (1 << 16);
-            }
-            d[0] = L; d[1] = R; d[2] = O; d[3] = B;
-        };
-        auto fill4 = [&](int ln, int rep, int (&d)[4]) __attribute__((always_inline)) {
-            const int sink = C::F_SINK;
-            int o = ln + rep * WAVE, L = 0, R = 0, O = -1, B = 0;
-            if (o < NX * NX) {  // P = Qh + Sh' K (symmetric)
-                const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
-                L = qp_dpk(C::F_SH + p * NU, 0); R = qp_dpk(C::F_KK + q * NU, 0);
-                O = (C::F_PP + o) | ((C::B_P + o + 1) << 17); B = (C::F_QH + p * NX + q) | (1 << 16);
-            } else if ((o -= NX * NX) < NX * NX) {  // Pi = W1 + Sh' kappa -> Pi' column-major
-                const int i = o / NX, j = o % NX;
-                L = qp_dpk(C::F_SH + i * NU, 0); R = qp_dpk(C::F_KK + (NX + j) * NU, 0);
-                O = (C::F_PIP + j * NX + i) | ((C::B_PI + o + 1) << 17); B = (C::F_W1 + o) | (1 << 16);
-            } else if ((o -= NX * NX) < NX * NX) {  // M += W2' kappa (symmetric)
-                const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
-                L = qp_dpk(C::F_W2 + p * NU, 0); R = qp_dpk(C::F_KK + (NX + q) * NU, 0); O = (V_M + o) | (1 << 15);
-            } else if ((o -= NX * NX) < NX * NX) {  // Acl = A + Bt K  -> global (+ LDS column-major for VC)
-                const int i = o / NX, j = o % NX;
-                L = qp_dpk(C::P_BTR + i * NU, 1); R = qp_dpk(C::F_KK + j * NU, 0);
-                O = (C::NV > 0 ? C::F_ACLC + j * NX + i : sink) | ((C::B_ACL + o + 1) << 17);
-                B = (C::P_A + j * NX + i) | (1 << 15) | (1 << 16);
-            }
-            d[0] = L; d[1] = R; d[2] = O; d[3] = B;
-        };
-        // n = 12 classes (CMP): the 20 repetitions' descriptors are rebuilt inside every stage from an opaque
-        // lane index instead of being held across the sweep (120 registers that spilled to scratch in the
-        // factor's inner loop); the n <= 8 classes decode them once per sweep
-        constexpr bool CMP = NX > 8;
-        int d1[CMP ? 1 : R1][4], d2[CMP ? 1 : R2][4], d4[CMP ? 1 : R4][4];
-        if constexpr (!CMP) {
             const int ln = qp_opaque(lane);  // volatile: keeps the descriptors inside the IPM loop
 #pragma unroll
-            for (int rep = 0; rep < R1; ++rep) fill1(ln, rep, d1[rep]);
+            for (int rep = 0; rep < R1; ++rep) {
+                int o = ln + rep * WAVE, L = 0, R = 0, O = -1, B = 0;
+                if (o < NX * NX) {  // T1 = P' A  -> T1 column-major
+                    const int i = o / NX, j = o % NX;
+                    L = qp_dpk(C::F_PP + i * NX, 0); R = qp_dpk(C::P_A + j * NX, 1); O = C::F_T1 + j * NX + i;
+                } else if ((o -= NX * NX) < NX * NU) {  // T2 = P' Bt -> column-major
+                    const int i = o / NU, j = o % NU;
+                    L = qp_dpk(C::F_PP + i * NX, 0); R = qp_dpk(C::P_BT + j * NX, 1); O = C::F_T2 + j * NX + i;
+                } else if ((o -= NX * NU) < NX * NX) {  // W1 = A' Pi'   (I at the last stage)
+                    const int i = o / NX, j = o % NX;
+                    L = qp_dpk(C::P_A + i * NX, 1); R = qp_dpk(C::F_PIP + j * NX, 0); O = C::F_W1 + o;
+                    B = (i == j) ? (V_ONE | (2 << 16)) : 0;
+                } else if ((o -= NX * NX) < NU * NX) {  // W2 = Bt' Pi' -> column-major (C_{K-2}' at the last stage)
+                    const int i = o / NX, j = o % NX;
+                    L = qp_dpk(C::P_BT + i * NX, 1); R = qp_dpk(C::F_PIP + j * NX, 0);
+                    O = (C::F_W2 + j * NU + i) | ((C::B_W2 + o + 1) << 17);
+                    B = (C::P_C + i * NX + j) | (1 << 15) | (2 << 16);
+                } else if ((o -= NU * NX) < NX) {  // u = P' e  (global only)
+                    L = qp_dpk(C::F_PP + o * NX, 0); R = qp_dpk(C::P_E, 1); O = sink | ((C::B_U + o + 1) << 17);
+                } else if ((o -= NX) < NX) {  // xe += Pi'' e
+                    L = qp_dpk(C::F_PIP + o * NX, 0); R = qp_dpk(C::P_E, 1); O = (V_XE + o) | (1 << 15);
+                }
+                d1[rep][0] = L; d1[rep][1] = R; d1[rep][2] = O; d1[rep][3] = B;
+            }
 #pragma unroll
-            for (int rep = 0; rep < R2; ++rep) fill2(ln, rep, d2[rep]);
+            for (int rep = 0; rep < R2; ++rep) {
+                int o = ln + rep * WAVE, L = 0, R = 0, O = -1, B = 0;
+                if (o < NX * NX) {  // Qh = Q + A' T1 (symmetric: (min, max) element for both halves)
+                    const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
+                    L = qp_dpk(C::P_A + p * NX, 1); R = qp_dpk(C::F_T1 + q * NX, 0); O = C::F_QH + o;
+                    B = (C::P_Q + p * NX + q) | (1 << 15) | (1 << 16);
+                } else if ((o -= NX * NX) < NU * NX) {  // Sh = S' + Bt' T1 -> column-major
+                    const int i = o / NX, j = o % NX;
+                    L = qp_dpk(C::P_BT + i * NX, 1); R = qp_dpk(C::F_T1 + j * NX, 0); O = C::F_SH + j * NU + i;
+                    B = (C::P_S + j * NU + i) | (1 << 15) | (1 << 16);
+                } else if ((o -= NU * NX) < NU * NU) {  // Rh = R + Bt' T2
+                    const int i = o / NU, j = o % NU, p = i < j ? i : j, q = i < j ? j : i;
+                    L = qp_dpk(C::P_BT + p * NX, 1); R = qp_dpk(C::F_T2 + q * NX, 0); O = C::F_RH + o;
+                    B = (C::P_R + p * NU + q) | (1 << 15) | (1 << 16);
+                }
+                d2[rep][0] = L; d2[rep][1] = R; d2[rep][2] = O; d2[rep][3] = B;
+            }
 #pragma unroll
-            for (int rep = 0; rep < R4; ++rep) fill4(ln, rep, d4[rep]);
+            for (int rep = 0; rep < R4; ++rep) {
+                int o = ln + rep * WAVE, L = 0, R = 0, O = -1, B = 0;
+                if (o < NX * NX) {  // P = Qh + Sh' K (symmetric)
+                    const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
+                    L = qp_dpk(C::F_SH + p * NU, 0); R = qp_dpk(C::F_KK + q * NU, 0);
+                    O = (C::F_PP + o) | ((C::B_P + o + 1) << 17); B = (C::F_QH + p * NX + q) | (1 << 16);
+                } else if ((o -= NX * NX) < NX * NX) {  // Pi = W1 + Sh' kappa -> Pi' column-major
+                    const int i = o / NX, j = o % NX;
+                    L = qp_dpk(C::F_SH + i * NU, 0); R = qp_dpk(C::F_KK + (NX + j) * NU, 0);
+                    O = (C::F_PIP + j * NX + i) | ((C::B_PI + o + 1) << 17); B = (C::F_W1 + o) | (1 << 16);
+                } else if ((o -= NX * NX) < NX * NX) {  // M += W2' kappa (symmetric)
+                    const int i = o / NX, j = o % NX, p = i < j ? i : j, q = i < j ? j : i;
+                    L = qp_dpk(C::F_W2 + p * NU, 0); R = qp_dpk(C::F_KK + (NX + q) * NU, 0); O = (V_M + o) | (1 << 15);
+                } else if ((o -= NX * NX) < NX * NX) {  // Acl = A + Bt K  -> global (+ LDS column-major for VC)
+                    const int i = o / NX, j = o % NX;
+                    L = qp_dpk(C::P_BTR + i * NU, 1); R = qp_dpk(C::F_KK + j * NU, 0);
+                    O = (C::NV > 0 ? C::F_ACLC + j * NX + i : sink) | ((C::B_ACL + o + 1) << 17);
+                    B = (C::P_A + j * NX + i) | (1 << 15) | (1 << 16);
+                }
+                d4[rep][0] = L; d4[rep][1] = R; d4[rep][2] = O; d4[rep][3] = B;
+            }
         }
-        // decoded once per sweep (n <= 8); accumulating outputs (xe, M) are summed in registers
-        QPRep q1[CMP ? 1 : R1], q2[CMP ? 1 : R2], q4[CMP ? 1 : R4];
+        // decoded once per sweep; accumulating outputs (xe, M) are summed in registers
+        constexpr bool CMP = NX > 8;   // compact repetitions (QPRepC) for the n = 12 classes
+        using Rep = typename std::conditional<CMP, QPRepC, QPRep>::type;
+        Rep q1[R1], q2[R2], q4[R4];
         double a1[R1], a2[R2], a4[R4];
-        // n = 12: the compact repetitions of one phase, decoded where the phase runs
-        auto dec1 = [&](QPRepC (&q)[R1]) __attribute__((always_inline)) {
-            const int ln = qp_opaque(lane);
-#pragma unroll
-            for (int r = 0; r < R1; ++r) { int d[4]; fill1(ln, r, d); q[r] = qp_decode_c(d, V_ONE, C::F_SINK, C::B_JNK); }
-        };
-        auto dec2 = [&](QPRepC (&q)[R2]) __attribute__((always_inline)) {
-            const int ln = qp_opaque(lane);
-#pragma unroll
-            for (int r = 0; r < R2; ++r) { int d[4]; fill2(ln, r, d); q[r] = qp_decode_c(d, V_ONE, C::F_SINK, C::B_JNK); }
-        };
-        auto dec4 = [&](QPRepC (&q)[R4]) __attribute__((always_inline)) {
-            const int ln = qp_opaque(lane);
-#pragma unroll
-            for (int r = 0; r < R4; ++r) { int d[4]; fill4(ln, r, d); q[r] = qp_decode_c(d, V_ONE, C::F_SINK, C::B_JNK); }
-        };
         // virtual control: the M contributions -Pi'' G^-1 Pi' of every stage (registers, like a4)
         constexpr int R0 = (NX * NX + WAVE - 1) / WAVE;
         double amv[R0];
@@ -739,17 +730,20 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         for (int r = 0; r < R0; ++r) amv[r] = 0.0;
 #pragma unroll
         for (int r = 0; r < R1; ++r) {
-            if constexpr (!CMP) q1[r] = qp_decode(d1[r], V_ONE, C::F_SINK, C::B_JNK);
+            if constexpr (CMP) q1[r] = qp_decode_c(d1[r], V_ONE, C::F_SINK, C::B_JNK);
+            else q1[r] = qp_decode(d1[r], V_ONE, C::F_SINK, C::B_JNK);
             a1[r] = 0.0;
         }
 #pragma unroll
         for (int r = 0; r < R2; ++r) {
-            if constexpr (!CMP) q2[r] = qp_decode(d2[r], V_ONE, C::F_SINK, C::B_JNK);
+            if constexpr (CMP) q2[r] = qp_decode_c(d2[r], V_ONE, C::F_SINK, C::B_JNK);
+            else q2[r] = qp_decode(d2[r], V_ONE, C::F_SINK, C::B_JNK);
             a2[r] = 0.0;
         }
 #pragma unroll
         for (int r = 0; r < R4; ++r) {
-            if constexpr (!CMP) q4[r] = qp_decode(d4[r], V_ONE, C::F_SINK, C::B_JNK);
+            if constexpr (CMP) q4[r] = qp_decode_c(d4[r], V_ONE, C::F_SINK, C::B_JNK);
+            else q4[r] = qp_decode(d4[r], V_ONE, C::F_SINK, C::B_JNK);
             a4[r] = 0.0;
         }
         for (int e = lane; e < NX * NX; e += WAVE) { lds[C::F_PP + e] = 0.0; lds[C::F_PIP + e] = 0.0; lds[V_M + e] = 0.0; }
@@ -759,9 +753,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         // packets stream through one LDS slot (a stage's packet is overwritten by the next one after its
         // last read), loads issued 3 stages ahead (register buffers pf[0..2], so the stage loop is
         // unrolled by 3 to keep their indices static)
-        // prefetch distance: 3 stages; 1 for the n = 12 classes (9 doubles per buffer: the deeper buffers were
-        // spilled to scratch in the stage loop, and a stage there outlasts a packet load anyway)
-        constexpr int FPD = NX > 8 ? 1 : 3;
+        // prefetch distance: 3 stages; 2 for the n = 12 classes (9 doubles per buffer, register pressure)
+        constexpr int FPD = NX > 8 ? 2 : 3;
         double pf[FPD][PFN];
         // lane's global packet element per prefetch slot (structural zeros read past the end: 0)
         int pfo[PFN];
@@ -788,20 +781,19 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             pf_load(K - 3, pf[2]);
             pf_store(K - 1, pf[0]);
             pf_load(K - 4, pf[0]);
-        } else if constexpr (FPD == 2) {
+        } else {
             pf_load(K - 1, pf[0]);
             pf_load(K - 2, pf[1]);
             pf_store(K - 1, pf[0]);
             pf_load(K - 3, pf[0]);
-        } else {
-            pf_load(K - 1, pf[0]);
-            pf_store(K - 1, pf[0]);
         }
         wsync();
         bool bad = false;
         // one stage; buffer `nb` receives stage ts-3 (issued now), buffer `cb` holds stage ts-1
-        auto stage = [&](int ts, double* nb, const double* cb) __attribute__((always_inline)) {
-            const bool last = ts == K - 1;
+        // (lastc: std::true_type for stage K-1, the only stage whose base terms / fixed last input differ -- a
+        // compile-time flag, so the loop's stage copies carry no per-stage selects for them)
+        auto stage = [&](auto lastc, int ts, double* nb, const double* cb) __attribute__((always_inline)) {
+            constexpr bool last = decltype(lastc)::value;
             const double blast = last ? 1.0 : 0.0;
             const int fbo = FBB + ts * C::FBS * 8;  // byte offset of this stage's output block (uniform)
             pf_load(ts - FPD, nb);  // unconditional: stage K-1 re-issues K-1-FPD, ts-FPD < 0 reads zeros
@@ -862,13 +854,15 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 wsync();
             }
             // ---- phase 1: T1 = P'A, T2 = P'Bt, W1 = A'Pi', W2 = Bt'Pi', u = P'e, xe += Pi''e
-            if constexpr (CMP) { QPRepC qc[R1]; dec1(qc); qp_phase_c<NX, R1, E1 - NX, E1>(lds, qc, blast, wb, fbo, a1); }
-            else qp_phase<NX, R1>(lds, q1, blast, wb, fbo, a1);
+            if constexpr (CMP) qp_phase_c<NX, R1, E1 - NX, E1>(lds, q1, blast, wb, fbo, a1);
+            else qp_phase<NX, R1, E1 - NX, E1>(lds, q1, blast, wb, fbo, a1);
             wsync();
+            pstamp(11);
             // ---- phase 2: Qh = Q + A'T1, Sh = S' + Bt'T1, Rh = R + Bt'T2
-            if constexpr (CMP) { QPRepC qc[R2]; dec2(qc); qp_phase_c<NX, R2, 0, 0>(lds, qc, blast, wb, fbo, a2); }
-            else qp_phase<NX, R2>(lds, q2, blast, wb, fbo, a2);
+            if constexpr (CMP) qp_phase_c<NX, R2, 0, 0>(lds, q2, blast, wb, fbo, a2);
+            else qp_phase<NX, R2, 0, 0>(lds, q2, blast, wb, fbo, a2);
             wsync();
+            pstamp(12);
             // ---- phase 3: Rh = L D L' in registers (every lane); [K | kappa] = -Rh^-1 [Sh | W2]
             {
                 const bool fx = last && T.fix_last_input;
@@ -890,7 +884,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                     nan |= d != d;
                     d = d > dmin ? d : dmin;
                     Lm[j * NU + j] = d;
-                    dinv[j] = 1.0 / d;
+                    // 1/d: hardware reciprocal + two Newton steps (~1 ulp; the correctly rounded division is a
+                    // ten-instruction sequence on this serial chain, three per stage)
+                    double rq = __builtin_amdgcn_rcp(d);
+                    rq = fma(fma(-d, rq, 1.0), rq, rq);
+                    dinv[j] = fma(fma(-d, rq, 1.0), rq, rq);
 #pragma unroll
                     for (int i = j + 1; i < NU; ++i) {
                         double v = Lm[i * NU + j];
@@ -935,22 +933,24 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                         wb.st((kl ? g + i * NX : C::B_JNK) * 8, fbo, v);
                     }
                 }
-                {
+                {   // lane e < NU^2 stores element e of [L | 1/d] (zero above the diagonal)
                     double v = 0.0;
 #pragma unroll
                     for (int e = 0; e < NU * NU; ++e) {
                         const int ei = e / NU, ej = e % NU;
-                        v = fma(qp_mask(e, lane), (ei > ej) ? Lm[e] : (ei == ej ? dinv[ei] : 0.0), v);
+                        if (ei >= ej) v = (lane == e) ? (ei > ej ? Lm[e] : dinv[ei]) : v;
                     }
                     wb.st((lane < NU * NU ? C::B_LD + lane : C::B_JNK) * 8, fbo, v);
                 }
             }
             wsync();
+            pstamp(13);
             // ---- phase 4: P = Qh + Sh'K, Pi = W1 + Sh'kappa, M += W2'kappa, Acl = A + Bt K
-            if constexpr (CMP) { QPRepC qc[R4]; dec4(qc); qp_phase_c<NU, R4, 2 * NX * NX, 3 * NX * NX>(lds, qc, blast, wb, fbo, a4); }
-            else qp_phase<NU, R4>(lds, q4, blast, wb, fbo, a4);
+            if constexpr (CMP) qp_phase_c<NU, R4, 2 * NX * NX, 3 * NX * NX>(lds, q4, blast, wb, fbo, a4);
+            else qp_phase<NU, R4, 2 * NX * NX, 3 * NX * NX>(lds, q4, blast, wb, fbo, a4);
             if (ts > 0) pf_store(ts - 1, cb);
             wsync();
+            pstamp(14);
             if constexpr (C::NV > 0) {
                 // ---- phase 5 (virtual control): the chain matrix Acl~ = G^-1 D Acl -> global (row-major)
 #pragma unroll
@@ -962,43 +962,38 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 wsync();
             }
         };
-        // (FPD = 3) stage K-1's packet is in LDS, K-2 in pf[1], K-3 in pf[2], K-4 in pf[0]
+        // stage K-1's packet is in LDS, K-2 in pf[1], K-3 in pf[2], K-4 in pf[0]
         int ts = K - 1;
         if constexpr (FPD == 3) {
-            stage(ts, pf[0], pf[1]);  // (its load of K-4 went out before the loop)
+            stage(std::true_type{}, ts, pf[0], pf[1]);  // (its load of K-4 went out before the loop)
             --ts;
             while (ts >= 0) {
-                stage(ts, pf[1], pf[2]);
+                stage(std::false_type{}, ts, pf[1], pf[2]);
                 if (--ts < 0) break;
-                stage(ts, pf[2], pf[0]);
+                stage(std::false_type{}, ts, pf[2], pf[0]);
                 if (--ts < 0) break;
-                stage(ts, pf[0], pf[1]);
+                stage(std::false_type{}, ts, pf[0], pf[1]);
                 --ts;
             }
-        } else if constexpr (FPD == 2) {  // LDS: K-1, pf[1]: K-2, pf[0]: K-3 (in flight)
-            stage(ts, pf[0], pf[1]);
+        } else {  // LDS: K-1, pf[1]: K-2, pf[0]: K-3 (in flight)
+            stage(std::true_type{}, ts, pf[0], pf[1]);
             --ts;
             while (ts >= 0) {
-                stage(ts, pf[1], pf[0]);
+                stage(std::false_type{}, ts, pf[1], pf[0]);
                 if (--ts < 0) break;
-                stage(ts, pf[0], pf[1]);
+                stage(std::false_type{}, ts, pf[0], pf[1]);
                 --ts;
             }
-        } else {  // LDS: K-1; each stage loads ts-1 into pf[0] and stores it to the ring at its end
-            for (; ts >= 0; --ts) stage(ts, pf[0], pf[0]);
         }
         if (bad) lds[V_FLAG] = 1.0;  // any lane (all agree)
         // the register-accumulated outputs (xe, M) to their LDS homes
         if constexpr (CMP) {
-            QPRepC c1[R1], c4[R4];
-            dec1(c1);
-            dec4(c4);
 #pragma unroll
             for (int r = 0; r < R1; ++r)
-                if (WAVE * r < E1 && WAVE * r + WAVE > E1 - NX && (c1[r].F & 4)) lds[c1[r].O] = a1[r];
+                if (WAVE * r < E1 && WAVE * r + WAVE > E1 - NX && (q1[r].F & 4)) lds[q1[r].O] = a1[r];
 #pragma unroll
             for (int r = 0; r < R4; ++r)
-                if (WAVE * r < 3 * NX * NX && WAVE * r + WAVE > 2 * NX * NX && (c4[r].F & 4)) lds[c4[r].O] = a4[r];
+                if (WAVE * r < 3 * NX * NX && WAVE * r + WAVE > 2 * NX * NX && (q4[r].F & 4)) lds[q4[r].O] = a4[r];
         } else {
 #pragma unroll
             for (int r = 0; r < R1; ++r)

@@ -39,6 +39,9 @@
 #include "scvx_hip.h"
 #include "wave_ops.hpp"
 
+// end-game step fraction (see the step rule in the iteration)
+constexpr double SCP_TAU_END = 0.99999;
+
 #if defined(__HIPCC_RTC__) && !defined(INFINITY)
 #define INFINITY __builtin_huge_valf()
 #endif
@@ -1728,7 +1731,14 @@ __global__ __launch_bounds__(64 * NW) void scp_ipm_kernel(SCPArgs a, double* __r
         const double mu_a = blk_sum(mual) / deg;
         const double sg = (mu_a / mu) * (mu_a / mu) * (mu_a / mu);
         __syncthreads();
-        const double al = fmin(1.0, 0.99 * direction(true, sg * mu));
+        // step fraction 0.99, or 1 - 1e-5 once the affine predictor takes a (nearly) full step: the end game,
+        // where a fixed 0.99 caps the gap reduction at 100x per iteration (qp_ipm.hpp QP_TAU_END, the same rule)
+        const double al = fmin(1.0, (aa >= 0.99 ? SCP_TAU_END : 0.99) * direction(true, sg * mu));
+#ifdef SCP_ITRACE
+        if (agent == 0 && tid == 0)
+            printf("SCP_ITRACE it %d pres %.3e dres %.3e gap %.3e pobj %.9e aa %.4f al %.4f sg %.2e mu %.3e ps %.2e ds %.2e near %d reg %.1e\n",
+                   it, pres, dres, gap, pobj, aa, al, sg, mu, pscale, dscale, (int)near_ok, regv);
+#endif
         // ---- breakdown guard: a non-finite direction (Riccati overflow in the end-game) ends the
         // solve on the current, finite iterate instead of corrupting it
         double badl = (al > 0.0) ? 0.0 : 1.0;

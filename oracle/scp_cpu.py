@@ -26,6 +26,7 @@ import numpy as np
 from scipy.linalg import solve_triangular
 
 NG = 4  # sigma, tau_x, tau_u, tau_nu
+SCP_TAU_END = 0.99999  # end-game step fraction (csrc/scp_kernel.hpp)
 
 
 def signs(d):
@@ -444,8 +445,10 @@ class SCPSolver:
                 corr = self._jprod(nd, self._Wmul(nd, Wn[k], dsa[k], 1), self._Wmul(nd, Wn[k], dla[k], 0))
                 rcomp.append(-lam2[k] - corr + sg * mu * self._unit(nd))
             dz, dsg, ds, dl, yp, y0p = direction(rcomp)
-            alpha = min(1.0, 0.99 * min(min(self._step(nd, s[k], ds[k]), self._step(nd, lam[k], dl[k]))
-                                        for k, nd in enumerate(nodes)))
+            # step fraction 0.99, 1 - 1e-5 once the affine step is (nearly) full (kernel: SCP_TAU_END)
+            tau = SCP_TAU_END if alpha >= 0.99 else 0.99
+            alpha = min(1.0, tau * min(min(self._step(nd, s[k], ds[k]), self._step(nd, lam[k], dl[k]))
+                                       for k, nd in enumerate(nodes)))
             # breakdown guard (kernel: wave_max(badl)): stop on the current finite iterate
             fin = np.isfinite(alpha) and alpha > 0 and np.isfinite(dz).all() and np.isfinite(yp).all() and \
                 np.isfinite(y0p).all() and all(np.isfinite(x).all() for x in dsg + ds + dl)

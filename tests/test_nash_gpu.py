@@ -60,14 +60,17 @@ def _check_against_oracle(p, X, U, nu, sigma, obj_kernel, w_u2):
     from oracle import nash_ref, scp_dense as sd
     ref = nash_ref.best_response(p)
     assert ref["status"] in ("optimal", "optimal_inaccurate"), ref["status"]
-    # the checker's own certificate: a best-iterate exit must still be a near-exact KKT point
-    assert ref["rel_gap"] <= 1e-8 and ref["cert"]["primal"] <= 1e-9 and ref["cert"]["stationarity"] <= 1e-9, \
+    # the checker's own certificate: a best-iterate exit must still be a near-exact KKT point (primal /
+    # stationarity residuals <= 1e-9, duality gap <= 1e-6 relative); the objective agreement asserted below is
+    # 1e-6 plus the checker's own gap (the oracle stops short on a few degenerate best responses: <= 5.3e-7
+    # measured)
+    assert ref["rel_gap"] <= 1e-6 and ref["cert"]["primal"] <= 1e-9 and ref["cert"]["stationarity"] <= 1e-9, \
         (ref["rel_gap"], ref["cert"])
     obj = sd.scp_objective(p, X, U, nu, sigma)
-    assert abs(obj - ref["obj"]) <= 1e-6 * abs(ref["obj"]), (obj, ref["obj"])
+    assert abs(obj - ref["obj"]) <= (1e-6 + ref["rel_gap"]) * abs(ref["obj"]), (obj, ref["obj"], ref["rel_gap"])
     assert abs(obj_kernel - obj) <= 1e-7 * abs(obj), (obj_kernel, obj)        # kernel-reported objective
     assert sd.scp_violation(p, X, U, nu, sigma) < 1e-7
-    gap = abs(obj - ref["obj"]) + 1e-7 * abs(ref["obj"])
+    gap = abs(obj - ref["obj"]) + (1e-7 + ref["rel_gap"]) * abs(ref["obj"])
     assert np.linalg.norm(U - ref["U"]) <= np.sqrt(gap / w_u2) + 1e-6
     return ref
 
@@ -283,3 +286,63 @@ def test_si_nash_solver_trace_matches_reference_iteration(cuda):
         cur[i] = steps[-1]["X"].copy()
     for i in range(3):
         np.testing.assert_array_equal(X[i], cur[i].T)
+
+
+def test_batched_game_solves_match_oracle(cuda):
+    """The batched game kernel on the bench's construction (bench.py --config nash: the three agents' best
+    responses after two Gauss-Seidel iterations, neighbour positions jittered by +-0.05), 96 agents in one
+    launch.  No solve fails; solves that end at the reduced tolerances (status 1: the third agent's problem
+    converges linearly in its end game -- the gap falls ~7x per full Newton step -- and meets the float64
+    floor one iteration short of 1e-9) are checked like the optimal ones against the oracle
+    (oracle/nash_ref.py): value 1e-6 relative, violation 1e-7, U within the strong-convexity bound."""
+    import torch
+    import scvx_hip
+    from oracle import nash_ref
+    from SCvx.config import default_game as G
+    from SCvx.global_parameters import K as KG
+    from SCvx.models.game_model import GameUnicycleModel
+    from SCvx.models.multi_agent_model import MultiAgentModel
+    from SCvx.optimization.nash_solver import NashSolver
+    from SCvx.utils.initial_guess import initial_guess
+    X0, U0 = (list(v) for v in zip(*(initial_guess(p["r_init"], p["r_final"], G.OBSTACLES, G.CLEARANCE, KG)
+                                     for p in G.AGENT_PARAMS)))
+    mam = MultiAgentModel(G.AGENT_PARAMS)
+    for i, p in enumerate(G.AGENT_PARAMS):
+        mam.models[i] = GameUnicycleModel(**{k: p[k] for k in ("r_init", "r_final", "obstacles", "control_weight",
+                                                               "collision_weight", "collision_radius",
+                                                               "control_rate_weight", "curvature_weight")})
+    ns = NashSolver(mam, max_iter=2, tol=-1.0)
+    ns.solve(X0, U0, 1.0)
+    br = ns.br_solvers
+    N = 96
+    pick = [a % 3 for a in range(N)]
+    T = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float64, device=cuda)  # noqa: E731
+    ins = [b.scp.host_inputs() for b in br]
+    args_b = {k: T(np.stack([ins[i][k] for i in pick]) if np.ndim(ins[0][k]) else [ins[i][k] for i in pick])
+              for k in ins[0]}
+    X_prev = np.stack([np.asarray(br[i].X_prev_param.require(), float).T for i in pick])
+    P = np.stack([np.stack([np.asarray(br[i].Y_params[j].require(), float).T for j in sorted(br[i].Y_params)])
+                  for i in pick])
+    P = P + np.random.default_rng(5).uniform(-0.05, 0.05, P.shape)
+    spec = br[0].spec()
+    z = scvx_hip.slab_update(T(X_prev), T(P), spec.pos_dim)
+    out = scvx_hip.SCPSolver(spec, N, device=cuda).solve_game(X_prev=T(X_prev), slab_z=z, slab_P=T(P), **args_b)
+    g = {k: v.cpu().numpy() for k, v in out.items()}
+    st = g["status"]
+    assert (st != 2).all(), np.bincount(st, minlength=3)
+    zn = z.cpu().numpy()
+    checked = {0: 0, 1: 0}
+    for a in range(N):
+        if checked[int(st[a])] >= 4:
+            continue
+        i = pick[a]
+        h = ins[i]
+        cons = mam.models[i].scp_constraints()
+        slabs = [(zn[a][j], P[a][j]) for j in range(P.shape[1])]
+        prob = nash_ref.game_problem("unicycle", h["Xref"], h["Uref"], h["sigma_ref"], cons, WTS, X_prev[a], slabs,
+                                     spec.r_slab, tr=h["tr"], disc=_disc_stacks(h["disc"], 3, 2))
+        _check_against_oracle(prob, g["X"][a], g["U"][a], g["nu"][a], h["sigma_ref"], float(g["obj"][a]),
+                              WTS["control_weight"])
+        checked[int(st[a])] += 1
+    print("status counts", np.bincount(st, minlength=3).tolist(), "checked", checked)
+    assert checked[0] >= 4
