@@ -64,6 +64,7 @@ static int scp_launch(const scvx_scp_template* T, int N, const double* disc, con
         if (T->xb_idx[b] < 0 || T->xb_idx[b] >= T->n_x) return set_error(SCVX_EINVAL, "scp: state bound index");
     if (T->has_final && !T->pin_u_last) return set_error(SCVX_EUNSUPPORTED, "scp: has_final requires pin_u_last");
     if (T->max_iter < 1) return set_error(SCVX_EINVAL, "scp: max_iter");
+    if (T->waves_per_agent < 0 || T->waves_per_agent > 2) return set_error(SCVX_EINVAL, "scp: waves_per_agent (0, 1, 2)");
     if (!disc || !Xref || !Uref || !sigma_ref || !tr || !x_init || !x_final || !X || !U || !nu || !sigma || !obj ||
         !status || !iters || (T->n_obs && !s_obs) || (T->n_nbr && (!nbr_pos || !nbr_Y || !nbr_Lam || !s_nbr)))
         return set_error(SCVX_EINVAL, "scp: null buffer");
@@ -99,7 +100,9 @@ static int scp_launch(const scvx_scp_template* T, int N, const double* disc, con
             simds = 4 * cus;
         if (simds <= 0) simds = 1024;
     }
-    const bool two = g_scp_waves == 2 || (g_scp_waves == 0 && T->K > WAVE && 2LL * N <= simds);
+    // the template's own mapping; 0 falls back to the process default (scvx_scp_set_waves_per_agent)
+    const int wsel = T->waves_per_agent ? T->waves_per_agent : g_scp_waves;
+    const bool two = wsel == 2 || (wsel == 0 && T->K > WAVE && 2LL * N <= simds);
     if (T->model_id == SCVX_MODEL_UNICYCLE && T->n_x == 3 && T->n_u == 2) {
         if (T->has_soc) return set_error(SCVX_EUNSUPPORTED, "scp: SOC rows need n_u + 1 <= 4");
         if (ne == 0)

@@ -381,6 +381,10 @@ class SCPSpec:
     w_in: float = 0.0
     n_slab: int = 0
     r_slab: float = 0.0
+    # launch mapping of this template's solves: 0 = the library's default (automatic: two waves per agent when
+    # K > 64 and the launch leaves SIMDs idle), 1 or 2 forced -- per template, so concurrent callers never
+    # share it (the process-wide scvx_scp_set_waves_per_agent is only the default for 0)
+    waves_per_agent: int = 0
 
     def to_c(self):
         n, m = model_dims(self.model)
@@ -420,6 +424,9 @@ class SCPSpec:
             t.theta_idx, t.n_slab, t.r_slab = int(self.theta_idx), int(self.n_slab), float(self.r_slab)
         else:
             t.theta_idx = -1
+        if self.waves_per_agent not in (0, 1, 2):
+            raise ValueError("waves_per_agent must be 0, 1 or 2")
+        t.waves_per_agent = int(self.waves_per_agent)
         return t
 
 

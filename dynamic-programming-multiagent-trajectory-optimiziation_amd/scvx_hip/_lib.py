@@ -11,7 +11,7 @@ LIB_PATH = os.environ.get("SCVX_HIP_LIB") or os.path.join(HERE, "libscvx_hip.so"
 
 # the C-ABI revision these bindings are written for (SCVX_HIP_VERSION of include/scvx_hip.h): a library of
 # another revision would take these argument lists with shifted pointers, so lib() refuses it
-SCVX_HIP_VERSION = 3
+SCVX_HIP_VERSION = 4
 SCVX_MAX_BOX, SCVX_MAX_OBS, SCVX_MAX_NBR = 4, 16, 32
 SCVX_IS_MAX_PROJ, SCVX_IS_MAX_STATE = 3, 12
 MODEL_IDS = {"di": 0, "unicycle": 1, "si": 2, "quad": 3}
@@ -69,6 +69,7 @@ class SCPTemplate(ctypes.Structure):
         ("game", ctypes.c_int32), ("sigma_fixed", ctypes.c_int32), ("w_u2", ctypes.c_double),
         ("w_du", ctypes.c_double), ("w_dth", ctypes.c_double), ("theta_idx", ctypes.c_int32),
         ("w_in", ctypes.c_double), ("n_slab", ctypes.c_int32), ("r_slab", ctypes.c_double),
+        ("waves_per_agent", ctypes.c_int32),
     ]
 
 

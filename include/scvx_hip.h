@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SCVX_HIP_VERSION 3
+#define SCVX_HIP_VERSION 4
 
 #define SCVX_OK 0
 #define SCVX_EINVAL (-1)
@@ -303,6 +303,9 @@ typedef struct scvx_scp_template {
     double w_in;            /* inertia_weight       * ||X - X_prev||_F^2              (:99-100) */
     int32_t n_slab;         /* slab rows z_{j,k}'(p_k - P_{j,k}) >= r_slab per node (:121-124), <= SCVX_MAX_NBR */
     double r_slab;          /* collision_radius */
+    /* launch mapping of this template's solves (version 4): 0 = the process default of
+     * scvx_scp_set_waves_per_agent (itself automatic unless set), 1 or 2 waves per agent forced */
+    int32_t waves_per_agent;
 } scvx_scp_template;
 
 /*
@@ -325,8 +328,10 @@ size_t scvx_scp_workspace_bytes(const scvx_scp_template* tpl, int N);
 
 /* Waves per agent of the SCP kernels (scvx_scp_solve_batched / scvx_scp_game_solve_batched): 0 (default) =
  * automatic -- two when K > 64 and the launch leaves SIMDs idle (2 N <= 4 x CUs), so the node phases of a
- * K <= 128 agent run in one pass; 1 or 2 forces the mapping (parity tests of both paths).  Process-wide.
- * Returns SCVX_OK, or SCVX_EINVAL for another value.  (No reference counterpart: a launch parameter.) */
+ * K <= 128 agent run in one pass; 1 or 2 forces the mapping.  This setter is a process-wide DEFAULT, read
+ * only by templates whose own `waves_per_agent` is 0; concurrent callers that need a mapping set it in
+ * their template (version 4) and never touch the default.  Returns SCVX_OK, or SCVX_EINVAL for another
+ * value.  (No reference counterpart: a launch parameter.) */
 int scvx_scp_set_waves_per_agent(int waves);
 
 /* ------------------------------------------------------------------------------------------

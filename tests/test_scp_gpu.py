@@ -10,14 +10,15 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def spec_and_tensors(probs, torch, dev, max_iter=100, tol=1e-9):
+def spec_and_tensors(probs, torch, dev, max_iter=100, tol=1e-9, waves_per_agent=0):
     import scvx_hip
     p0 = probs[0]
     nn = len(p0.get("nbrs") or [])
     spec = scvx_hip.SCPSpec(model=p0["model"], K=p0["Xref"].shape[0], pos_dim=p0["pos_dim"],
                             u_bounds=p0["u_bounds"], u_soc=p0["u_soc"], x_bounds=p0["x_bounds"], obs=p0["obs"],
                             w_nu=p0["w_nu"], w_slack=p0["w_slack"], w_sigma=p0["w_sigma"], n_nbr=nn,
-                            rho=p0.get("rho", 0.0), d_min=p0.get("d_min", 1.0), max_iter=max_iter, tol=tol)
+                            rho=p0.get("rho", 0.0), d_min=p0.get("d_min", 1.0), max_iter=max_iter, tol=tol,
+                            waves_per_agent=waves_per_agent)
     T = lambda a: torch.tensor(np.ascontiguousarray(a), dtype=torch.float64, device=dev)  # noqa: E731
     args = dict(disc=T(np.stack([p["disc"] for p in probs])), Xref=T(np.stack([p["Xref"] for p in probs])),
                 Uref=T(np.stack([p["Uref"] for p in probs])), sigma_ref=T([p["sigma_ref"] for p in probs]),
@@ -80,7 +81,7 @@ def test_scproblem_matches_reference_formulation(cuda, model, K):
                                           ("unicycle", False, 200)])
 def test_one_and_two_waves_per_agent(cuda, model, admm, K):
     """K > 64 nodes: the same agents through the one-wave mapping (node phases in two or more passes; what a
-    launch that fills every SIMD uses) and the two-wave mapping (scvx_scp_set_waves_per_agent; what a
+    launch that fills every SIMD uses) and the two-wave mapping (SCPSpec.waves_per_agent; what a
     single-agent launch uses; K = 200 takes two passes of 128 threads).  Both at the dense oracle's optimal
     value (1e-7, feasibility 1e-7); their reductions sum in different orders, so they agree to the
     stopping tolerance, not bit for bit."""
@@ -88,13 +89,17 @@ def test_one_and_two_waves_per_agent(cuda, model, admm, K):
     import scvx_hip
     from oracle import scp_dense as sd
     probs = instances(model, K, 3 if K <= 100 else 2, admm=admm, seed=5)
-    out = {}
+    out = {w: solve_gpu(probs, torch, cuda, waves_per_agent=w) for w in (1, 2)}   # the template's own mapping
+    # the process-wide setter is only the default of templates that leave waves_per_agent = 0
     try:
-        for w in (1, 2):
-            scvx_hip.check(scvx_hip.lib().scvx_scp_set_waves_per_agent(w), "scvx_scp_set_waves_per_agent")
-            out[w] = solve_gpu(probs, torch, cuda)
+        scvx_hip.check(scvx_hip.lib().scvx_scp_set_waves_per_agent(2), "scvx_scp_set_waves_per_agent")
+        again = solve_gpu(probs, torch, cuda, waves_per_agent=1)
+        dflt = solve_gpu(probs, torch, cuda)
     finally:
         scvx_hip.lib().scvx_scp_set_waves_per_agent(0)
+    for k in ("X", "U", "obj", "iters"):
+        np.testing.assert_array_equal(again[k], out[1][k])
+        np.testing.assert_array_equal(dflt[k], out[2][k])
     assert scvx_hip.lib().scvx_scp_set_waves_per_agent(3) != 0   # only 0, 1, 2
     for a, p in enumerate(probs):
         ref = sd.solve_scproblem(p, tol=1e-10)
