@@ -13,8 +13,9 @@ Checked at step 18 (tr = 2^-4 x 0.25) of the loop, on the step's own inputs (dis
   * status-1 solves against the dense reference-form oracle (oracle/qp_dense.py, dist_scvx_3d.py:51-111 as
     written): optimal value within 1e-7 relative, violation < 1e-5 (Clarabel's reduced feasibility, as
     tests/test_coupled_gpu.py); status-0 solves: value 1e-7, violation 1e-7;
-  * the warm-started solve equals the cold solve of the same subproblem in value (both within the 1e-8 gap
-    test of the optimum: 2e-8 relative)."""
+  * the warm-started solve equals the cold solve of the same subproblem in value: 2e-8 relative where both
+    end optimal (both within the 1e-8 gap test), 5e-5 where either ends at the reduced tolerances (measured
+    3.5e-6 at most)."""
 import numpy as np
 import pytest
 
@@ -61,9 +62,15 @@ def test_c4_late_steps_match_dense_oracle(cuda):
     cold = scvx_hip.QPSolver(spec, N, device=cuda).solve(drv.disc, drv.sigma, X, U, drv.x_init, drv.x_final, trp,
                                                          rows, cnt)
     st = out["status"].cpu().numpy()
+    stc = cold["status"].cpu().numpy()
     ow, oc = out["obj"].cpu().numpy(), cold["obj"].cpu().numpy()
-    # both stop within 1e-8 (relative, absolute below |obj| = 1) of the optimal value: 2e-8 apart at most
-    np.testing.assert_allclose(ow, oc, rtol=2e-8, atol=2e-8)
+    # both optimal: each within 1e-8 (relative, absolute below |obj| = 1) of the optimal value, 2e-8 apart at
+    # most; a status-1 end on either side certifies only the reduced gap (5e-5 relative)
+    both = (st == 0) & (stc == 0)
+    np.testing.assert_allclose(ow[both], oc[both], rtol=2e-8, atol=2e-8)
+    np.testing.assert_allclose(ow[~both], oc[~both], rtol=5e-5, atol=1e-8)
+    print("warm vs cold: both optimal", int(both.sum()), "max rel diff where either is status 1",
+          float(np.max(np.abs(ow[~both] - oc[~both]) / np.maximum(1.0, np.abs(oc[~both])), initial=0.0)))
     dn, Xh, Uh = drv.disc.cpu().numpy(), X.cpu().numpy(), U.cpu().numpy()
     sig, xf = drv.sigma.cpu().numpy(), drv.x_final.cpu().numpy()
     rn, cn = rows.cpu().numpy(), cnt.cpu().numpy()
