@@ -35,7 +35,7 @@ def test_c4_late_steps_match_dense_oracle(cuda):
     spec = scvx_hip.QPSpec(model="di", K=bench.K, box=cfg["box"], obs=cfg["obs"], w_obs=1e6, j_max=cfg["j_max"],
                            w_coll=1e4, tol=1e-8, max_iter=60)
     drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], bench.TR0, coupling=CouplingSpec(R=cfg["R"]),
-                     tr_rule="global")
+                     tr_rule="global", warm_max_status=1)   # bench.py's default
     X, U = w["X"].clone(), w["U"].clone()
     N = X.shape[0]
     fr0 = []

@@ -25,7 +25,7 @@ def main(steps=25, dump_steps="12,18", n_dump=4, cap=64):
     dump_steps = {int(s) for s in str(dump_steps).split(",") if s}
     dev = torch.device("cuda:0")
     sc, w, cfg = bench.make_coupled("c4", 1, 0, dev)
-    ws = int(os.environ.get("WARM_STATUS", "0"))
+    ws = int(os.environ.get("WARM_STATUS", "1"))   # bench.py default
     spec = scvx_hip.QPSpec(model="di", K=bench.K, box=cfg["box"], obs=cfg["obs"], w_obs=1e6, j_max=cfg["j_max"],
                            w_coll=1e4, tol=1e-8, max_iter=60)
     drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], bench.TR0, coupling=CouplingSpec(R=cfg["R"]),

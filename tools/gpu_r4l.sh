@@ -10,4 +10,6 @@ timeout -k 10 200 python -u tools/trace_coupled.py c5 4 > gpurun_out/trace_c5_ba
 SCVX_HIP_LIB=$D timeout -k 10 200 python -u tools/trace_coupled.py c5 4 > gpurun_out/trace_c5_D_$TAG.log 2>&1
 timeout -k 10 240 python -u bench.py --config c5 --no-cpu > gpurun_out/ab_${TAG}_c5_base.log 2>&1
 SCVX_HIP_LIB=$D timeout -k 10 240 python -u bench.py --config c5 --no-cpu > gpurun_out/ab_${TAG}_c5_D.log 2>&1
+SCVX_HIP_LIB=dbg/ptr/libscvx_hip.so TRACE=1 REPS=2 timeout -k 10 120 python -u tools/gpurun_quick.py 1024 > gpurun_out/trace_ptr_$TAG.log 2>&1
+timeout -k 10 240 python -u bench.py --config c4 --no-cpu --warm-status 1 > gpurun_out/bench_c4_ws1_$TAG.log 2>&1
 echo done
