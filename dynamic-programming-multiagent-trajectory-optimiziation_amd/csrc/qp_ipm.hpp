@@ -78,11 +78,11 @@ struct QPArgs {
 // ---- sizes shared by host (workspace / LDS bytes) and device
 constexpr int qp_dstr(int nx, int nu) { return nx * (nx + 2 * nu + 2); }
 constexpr int qp_pkt(int nx, int nu, int nv = 0) { return 2 * nx * nx + 4 * nx * nu + nu * nu + nx + nv; }
-// global (compact) packet: Q as its diagonal + the 3 off-diagonals of the position block, S, R upper
-// packed, e, A, Bt (column-major), C_{t-1} -- expanded to the LDS packet layout by the factor's prefetch
-// (+ the virtual control's node curvature D, nv doubles)
+// global packet: n <= 8 compact (Q as its diagonal + the 3 off-diagonals of the position block, S, R upper
+// packed, e, A, Bt (column-major), C_{t-1}, the virtual control's D) -- expanded to the LDS packet layout by the
+// factor's prefetch through a per-lane gather table; n = 12 dense (the LDS layout itself, QPCfg::DPK)
 constexpr int qp_gpk(int nx, int nu, int nv = 0) {
-    return (nx + 3) + nx * nu + nu * (nu + 1) / 2 + nx + nx * nx + 2 * nx * nu + nv;
+    return nx > 8 ? qp_pkt(nx, nu, nv) : (nx + 3) + nx * nu + nu * (nu + 1) / 2 + nx + nx * nx + 2 * nx * nu + nv;
 }
 constexpr int qp_even(int x) { return (x + 1) & ~1; }
 // workspace columns (K doubles each: one per node) of a capacity class
@@ -99,8 +99,14 @@ constexpr int qp_fbs(int nx, int nu, int nv = 0) { return 3 * nu * nx + nu * nu 
 // per agent: columns [c][K], packets [K][GPK], factor blocks [K][FBS] -- only the K nodes: lanes >= K
 // address past the end of the buffer (loads read 0, stores are dropped), so the agent's footprint is
 // what its nodes touch (C3: 1024 agents x 199 KB stay inside the 256 MB Infinity Cache)
+// n = 12 classes: the factor's per-lane phase descriptors, [repetition][lane] x 16 bytes (QPRepC + pad), after the
+// factor blocks (agent-independent, rewritten at each sweep; see the factor sweep)
+constexpr int qp_nrep(int nx, int nu) {
+    return (2 * nx * nx + 2 * nx * nu + 2 * nx + 63) / 64 + (nx * nx + nu * nx + nu * nu + 63) / 64 + (4 * nx * nx + 63) / 64;
+}
+constexpr int qp_dtab(int nx, int nu) { return nx > 8 ? qp_nrep(nx, nu) * 64 * 2 : 0; }
 constexpr long long qp_ws_doubles(int nx, int nu, int nb, int ns, int ng, int K, int nv = 0) {
-    return (long long)K * (qp_ncol(nx, nu, nb, ns, ng, nv) + qp_gpk(nx, nu, nv) + qp_fbs(nx, nu, nv));
+    return (long long)K * (qp_ncol(nx, nu, nb, ns, ng, nv) + qp_gpk(nx, nu, nv) + qp_fbs(nx, nu, nv)) + qp_dtab(nx, nu);
 }
 // LDS doubles of a class (QPCfg::lds_doubles, written out for the host of a runtime-compiled class, which
 // has no QPCfg instantiation; QPCfg asserts that both agree)
@@ -148,15 +154,25 @@ struct QPCfg {
                          P_A = P_E + NX, P_BT = P_A + NX * NX, P_BTR = P_BT + NX * NU, P_C = P_BTR + NX * NU,
                          P_D = P_C + NX * NU, PKT = P_D + NV;
     static_assert(PKT == qp_pkt(NX, NU, NV), "packet size");
-    // global packet (compact; qp_gpk): Q diagonal | Q position-block off-diagonals (0,1) (0,2) (1,2) |
-    // S | R upper packed | e | A (column-major) | Bt (column-major) | C_{t-1} (column-major)
+    // global packet (compact, n <= 8; qp_gpk): Q diagonal | Q position-block off-diagonals (0,1) (0,2) (1,2) |
+    // S | R upper packed | e | A (column-major) | Bt (column-major) | C_{t-1} (column-major) | D
     static constexpr int G_QD = 0, G_QO = G_QD + NX, G_S = G_QO + 3, G_R = G_S + NX * NU,
                          G_E = G_R + NU * (NU + 1) / 2, G_A = G_E + NX, G_BT = G_A + NX * NX, G_C = G_BT + NX * NU,
-                         G_D = G_C + NX * NU, GPK = G_D + NV;
+                         G_D = G_C + NX * NU;
+    // n = 12 (DPK): the global packet has the LDS layout element for element.  The compact form needs a per-lane
+    // gather table of PFN offsets live across the factor sweep; at n = 12 the register allocator spilled it to
+    // scratch, and every reload waited for the packet prefetches in flight.  The dense prefetch is one
+    // contiguous load per 64 elements; Q's structural zeros are written once per solve (setup), with the
+    // constant A | Bt | Bt row-major | C_{t-1}; the node phase writes Q's nonzeros (both triangles), S, R (both
+    // halves), e, D.  (n <= 8 keeps the compact form: its 3-entry table costs nothing, the dense packet's extra
+    // traffic does: C3 780 -> 742 SCvx-it/s, A/B round 4.)
+    static constexpr bool DPK = NX > 8;
+    static constexpr int GPK = DPK ? PKT : G_D + NV;
     static_assert(GPK == qp_gpk(NX, NU, NV), "global packet size");
     static_assert(NX >= 3, "the position block is 3 x 3");
     // global packet element of LDS packet element e (-1: a structural zero)
     static constexpr int gsrc(int e) {
+        if (DPK) return e;
         if (e < P_S) {
             const int i = e / NX, j = e % NX;
             if (i == j) return G_QD + i;
@@ -178,6 +194,9 @@ struct QPCfg {
         if (e < P_D) return G_C + (e - P_C);
         return G_D + (e - P_D);
     }
+    // global packet index of the node-phase outputs e, D and of the constant blocks
+    static constexpr int gE = DPK ? P_E : G_E, gD = DPK ? P_D : G_D, gS = DPK ? P_S : G_S, gA = DPK ? P_A : G_A,
+                         gBT = DPK ? P_BT : G_BT, gC = DPK ? P_C : G_C;
     static_assert(NX <= 16, "the solve chains broadcast within one 16-lane row");
     // factor outputs: stage-major blocks [t][FBS] (coalesced stores from the element-parallel
     // factor; each lane-parallel pass reads its own stage's block)
@@ -260,6 +279,7 @@ __host__ __device__ constexpr int qp_dpk(int off, int) { return off; }
 // VGPR (voffset) and the column part as a (rematerialisable) SGPR constant (soffset), so no
 // per-column 64-bit address is ever materialised in vector registers.
 typedef unsigned int qp_u2 __attribute__((ext_vector_type(2)));
+typedef unsigned int qp_u4 __attribute__((ext_vector_type(4)));
 // Every memory op of the factor sweep is unconditional: lanes with nothing to store write to the
 // junk slot of the stage block, and prefetch loads of padding / structurally zero packet elements
 // read past the end of the workspace (0).  A load or store under a divergent branch makes the
@@ -276,6 +296,14 @@ struct QPBuf {
     __device__ __forceinline__ void st(int voff, int soff, double v) const {
         soff = __builtin_amdgcn_readfirstlane(soff);
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(qp_u2, v), rs, voff, soff, 0);
+    }
+    __device__ __forceinline__ qp_u4 ld4(int voff, int soff) const {
+        soff = __builtin_amdgcn_readfirstlane(soff);
+        return __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
+    }
+    __device__ __forceinline__ void st4(int voff, int soff, qp_u4 v) const {
+        soff = __builtin_amdgcn_readfirstlane(soff);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, 0);
     }
 };
 // keep a value opaque to the optimiser (volatile: re-derived where it is used, never hoisted)
@@ -352,41 +380,53 @@ __device__ __forceinline__ void qp_phase(double* lds, const QPRep (&d)[NREP], do
 // 1 every stage, 2 last stage; bit 2: accumulating output) instead of three doubles, and the accumulating
 // outputs keep their LDS target in O (written every stage, overwritten by the register sum after the
 // sweep; nothing reads V_M / V_XE during it).  20 repetitions x 6 instead of 11 registers at NX = 12.
+// Packed in three registers (round 4: the six-int form held 120 registers across the n = 12 sweep, which
+// spilled to scratch inside the stage loop): L | R << 16, B | O << 16, G | F << 16 (LDS offsets < 2^15
+// doubles, the global byte offset within a stage block < 2^16).
 struct QPRepC {
-    int L, R, B, O, G, F;
+    int LR, BO, GF;
+    __device__ __forceinline__ int L() const { return LR & 0xFFFF; }
+    __device__ __forceinline__ int R() const { return LR >> 16; }
+    __device__ __forceinline__ int B() const { return BO & 0xFFFF; }
+    __device__ __forceinline__ int O() const { return BO >> 16; }
+    __device__ __forceinline__ int G() const { return GF & 0xFFFF; }
+    __device__ __forceinline__ int F() const { return GF >> 16; }
 };
 __device__ __forceinline__ QPRepC qp_decode_c(const int (&d)[4], int one, int lsink, int jnk) {
     QPRepC q;
-    q.L = d[0] & 0x7FFF;
-    q.R = d[1] & 0x7FFF;
+    const int L = d[0] & 0x7FFF, R = d[1] & 0x7FFF;
     const int bk = d[3] >> 16;
-    q.B = bk ? (d[3] & 0x7FFF) : one;
+    const int B = bk ? (d[3] & 0x7FFF) : one;
     const int O = d[2];
     const bool on = O >= 0, acc = on && ((O >> 15) & 1);
-    q.O = on ? (O & 0x7FFF) : lsink;
+    const int Oo = on ? (O & 0x7FFF) : lsink;
     const int g = on ? (O >> 17) - 1 : -1;
-    q.G = (g >= 0 ? g : jnk) * 8;
-    q.F = bk | (acc ? 4 : 0);
+    const int G = (g >= 0 ? g : jnk) * 8;
+    const int F = bk | (acc ? 4 : 0);
+    q.LR = L | (R << 16);
+    q.BO = B | (Oo << 16);
+    q.GF = G | (F << 16);
     return q;
 }
 // as qp_phase; outputs [ALO, AHI) of the phase may accumulate (only those repetitions keep a register sum)
 template <int KK, int NREP, int ALO, int AHI>
-__device__ __forceinline__ void qp_phase_c(double* lds, const QPRepC (&d)[NREP], double blast, const QPBuf& wb,
+__device__ __forceinline__ void qp_phase_c(double* lds, const QPRepC* d, double blast, const QPBuf& wb,
                                            int fbo, double (&areg)[NREP]) {
+    const QPRepC* q = d;
     double val[NREP];
 #pragma unroll
     for (int r = 0; r < NREP; ++r) {
-        const int bk = d[r].F & 3;
+        const int bk = q[r].F() & 3;
         const double bm = (bk == 1 ? 1.0 : 0.0) + blast * (bk == 2 ? 1.0 : 0.0);
-        val[r] = fma(lds[d[r].B], bm, qp_dot<KK>(lds, d[r].L, d[r].R));
+        val[r] = fma(lds[q[r].B()], bm, qp_dot<KK>(lds, q[r].L(), q[r].R()));
     }
 #pragma unroll
     for (int r = 0; r < NREP; ++r) {
-        lds[d[r].O] = val[r];
+        lds[q[r].O()] = val[r];
         if constexpr (true) {
-            if (WAVE * r < AHI && WAVE * r + WAVE > ALO) areg[r] = fma((d[r].F & 4) ? 1.0 : 0.0, val[r], areg[r]);
+            if (WAVE * r < AHI && WAVE * r + WAVE > ALO) areg[r] = fma((q[r].F() & 4) ? 1.0 : 0.0, val[r], areg[r]);
         }
-        wb.st(d[r].G, fbo, val[r]);
+        wb.st(q[r].G(), fbo, val[r]);
     }
 }
 
@@ -528,7 +568,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
     };
 
-    // diagnostics build (-DQP_PHASE_TRACE): the factor's four phases per stage into V_ST[11..14] (no memory drain)
+    // diagnostics build (-DQP_PHASE_TRACE): the factor's four phases per stage into V_ST[11..14], the virtual
+    // control phases (5 of the previous stage, 0 of this one) and the packet issue into V_ST[15] (no memory drain)
     auto pstamp = [&](int i) __attribute__((always_inline)) {
 #ifdef QP_PHASE_TRACE
         if (stamp_on) {
@@ -564,12 +605,16 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                     for (int k = 0; k < NX; ++k) v = fma(Ad[k * NX + i], Cp[j * NX + k], v);
                     cst(C::C_BT + i * NU + j, v);
-                    pst(C::G_BT + j * NX + i, v);
+                    pst(C::gBT + j * NX + i, v);
+                    if constexpr (C::DPK) pst(C::P_BTR + i * NU + j, v);
                 }
 #pragma unroll
-            for (int e = 0; e < NX * NX; ++e) pst(C::G_A + e, Ad[e]);
+            for (int e = 0; e < NX * NX; ++e) {
+                pst(C::gA + e, Ad[e]);
+                if constexpr (C::DPK) pst(C::P_Q + e, 0.0);
+            }
 #pragma unroll
-            for (int e = 0; e < NX * NU; ++e) pst(C::G_C + e, Cp[e]);
+            for (int e = 0; e < NX * NU; ++e) pst(C::gC + e, Cp[e]);
         }
         // soft rows: obstacle linearisations (single_integrator_model.py:113-126) from Xref, then
         // the caller's collision rows (dist_scvx_3d.py:93-107)
@@ -718,31 +763,48 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 d4[rep][0] = L; d4[rep][1] = R; d4[rep][2] = O; d4[rep][3] = B;
             }
         }
-        // decoded once per sweep; accumulating outputs (xe, M) are summed in registers
-        constexpr bool CMP = NX > 8;   // compact repetitions (QPRepC) for the n = 12 classes
-        using Rep = typename std::conditional<CMP, QPRepC, QPRep>::type;
-        Rep q1[R1], q2[R2], q4[R4];
+        // decoded once per sweep; accumulating outputs (xe, M) are summed in registers.
+        // n = 12 classes (CMP): the decoded repetitions (QPRepC, three words each) go to a per-agent table in the
+        // workspace and every stage loads them back (one 16-byte load per repetition, issued ahead of the packet
+        // prefetch).  Held in registers across the sweep they were spilled to scratch by the allocator (the
+        // function-wide peak is elsewhere) and reloaded at each use behind a full vmcnt drain -- which also
+        // drained the packet prefetches in flight: ~100 serialised memory round trips per stage.
+        constexpr bool CMP = NX > 8;
+        constexpr int RT = R1 + R2 + R4;
+        const int DTB = FBB + K * C::FBS * 8;   // byte offset of the descriptor table [rep][lane] x 16 B
+        QPRep q1[CMP ? 1 : R1], q2[CMP ? 1 : R2], q4[CMP ? 1 : R4];
         double a1[R1], a2[R2], a4[R4];
         // virtual control: the M contributions -Pi'' G^-1 Pi' of every stage (registers, like a4)
         constexpr int R0 = (NX * NX + WAVE - 1) / WAVE;
         double amv[R0];
 #pragma unroll
         for (int r = 0; r < R0; ++r) amv[r] = 0.0;
+        auto tab_st = [&](int r, const QPRepC& q) __attribute__((always_inline)) {
+            qp_u4 w;
+            w.x = (unsigned)q.LR; w.y = (unsigned)q.BO; w.z = (unsigned)q.GF; w.w = 0u;
+            wb.st4(qp_opaque(lane) * 16, DTB + r * WAVE * 16, w);
+        };
+        auto tab_ld = [&](int r, int vo) __attribute__((always_inline)) -> QPRepC {
+            const qp_u4 w = wb.ld4(vo, DTB + r * WAVE * 16);
+            QPRepC q;
+            q.LR = (int)w.x; q.BO = (int)w.y; q.GF = (int)w.z;
+            return q;
+        };
 #pragma unroll
         for (int r = 0; r < R1; ++r) {
-            if constexpr (CMP) q1[r] = qp_decode_c(d1[r], V_ONE, C::F_SINK, C::B_JNK);
+            if constexpr (CMP) tab_st(r, qp_decode_c(d1[r], V_ONE, C::F_SINK, C::B_JNK));
             else q1[r] = qp_decode(d1[r], V_ONE, C::F_SINK, C::B_JNK);
             a1[r] = 0.0;
         }
 #pragma unroll
         for (int r = 0; r < R2; ++r) {
-            if constexpr (CMP) q2[r] = qp_decode_c(d2[r], V_ONE, C::F_SINK, C::B_JNK);
+            if constexpr (CMP) tab_st(R1 + r, qp_decode_c(d2[r], V_ONE, C::F_SINK, C::B_JNK));
             else q2[r] = qp_decode(d2[r], V_ONE, C::F_SINK, C::B_JNK);
             a2[r] = 0.0;
         }
 #pragma unroll
         for (int r = 0; r < R4; ++r) {
-            if constexpr (CMP) q4[r] = qp_decode_c(d4[r], V_ONE, C::F_SINK, C::B_JNK);
+            if constexpr (CMP) tab_st(R1 + R2 + r, qp_decode_c(d4[r], V_ONE, C::F_SINK, C::B_JNK));
             else q4[r] = qp_decode(d4[r], V_ONE, C::F_SINK, C::B_JNK);
             a4[r] = 0.0;
         }
@@ -756,22 +818,33 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         // prefetch distance: 3 stages; 2 for the n = 12 classes (9 doubles per buffer, register pressure)
         constexpr int FPD = NX > 8 ? 2 : 3;
         double pf[FPD][PFN];
-        // lane's global packet element per prefetch slot (structural zeros read past the end: 0)
-        int pfo[PFN];
-#pragma unroll
-        for (int k = 0; k < PFN; ++k) {
-            const int e = qp_opaque(lane) + WAVE * k;
-            const int g = e < PKT ? C::gsrc(e) : -1;  // padding lanes read 0 (stored to the sink)
-            pfo[k] = g >= 0 ? g * 8 : QP_OOB;
-        }
-        auto pf_load = [&](int ts, double* b) __attribute__((always_inline)) {
-#pragma unroll
-            for (int k = 0; k < PFN; ++k) b[k] = wb.ld(pfo[k], PKB + (ts > 0 ? ts : 0) * C::GPK * 8);
-        };
-        auto pf_store = [&](int ts, const double* b) __attribute__((always_inline)) {
+        // n <= 8: lane's global packet element per prefetch slot (structural zeros read past the end: 0);
+        // n = 12 (dense packet): lane l loads elements l + 64 k (the padding lanes of the last slot read the next
+        // packet / factor block and store to the sink) -- no table held across the sweep
+        int pfo[C::DPK ? 1 : PFN];
+        if constexpr (!C::DPK) {
 #pragma unroll
             for (int k = 0; k < PFN; ++k) {
-                const int e = lane + WAVE * k;
+                const int e = qp_opaque(lane) + WAVE * k;
+                const int g = e < PKT ? C::gsrc(e) : -1;  // padding lanes read 0 (stored to the sink)
+                pfo[k] = g >= 0 ? g * 8 : QP_OOB;
+            }
+        }
+        auto pf_load = [&](int ts, double* b) __attribute__((always_inline)) {
+            if constexpr (C::DPK) {
+                const int vo = qp_opaque(lane) * 8;
+#pragma unroll
+                for (int k = 0; k < PFN; ++k) b[k] = wb.ld(vo, PKB + (ts > 0 ? ts : 0) * C::GPK * 8 + k * WAVE * 8);
+            } else {
+#pragma unroll
+                for (int k = 0; k < PFN; ++k) b[k] = wb.ld(pfo[k], PKB + (ts > 0 ? ts : 0) * C::GPK * 8);
+            }
+        };
+        auto pf_store = [&](int ts, const double* b) __attribute__((always_inline)) {
+            const int sl = NX > 8 ? qp_opaque(lane) : lane;
+#pragma unroll
+            for (int k = 0; k < PFN; ++k) {
+                const int e = sl + WAVE * k;
                 lds[e < PKT ? C::F_RING + e : C::F_SINK] = b[k];
             }
         };
@@ -796,13 +869,22 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             constexpr bool last = decltype(lastc)::value;
             const double blast = last ? 1.0 : 0.0;
             const int fbo = FBB + ts * C::FBS * 8;  // byte offset of this stage's output block (uniform)
+            // n = 12: the lane index re-derived per stage: lane-dependent addresses and masks are rebuilt in the
+            // stage, not hoisted out of the IPM loop and held (spilled) across it (n <= 8: hoisted, in registers)
+            const int sl = NX > 8 ? qp_opaque(lane) : lane;
+            QPRepC qs[CMP ? RT : 1];
+            if constexpr (CMP) {
+                const int vo = qp_opaque(lane) * 16;
+#pragma unroll
+                for (int r = 0; r < RT; ++r) qs[r] = tab_ld(r, vo);
+            }
             pf_load(ts - FPD, nb);  // unconditional: stage K-1 re-issues K-1-FPD, ts-FPD < 0 reads zeros
             if constexpr (C::NV > 0) {
                 // ---- phase 0 (virtual control nu_ts): G = diag(D) + P', then [G^-1 Pi' | G^-1 | G^-1 P'] by
                 // Gauss-Jordan without pivoting (G is SPD): lane c < 4 NX owns column c of [G | Pi' | I | P'];
                 // the pivot column is broadcast by readlane (no LDS round trip per pivot).  At the last stage
                 // P' = Pi' = 0 and D = 1 (assemble), so nothing changes there.
-                const int c = lane < 4 * NX ? lane : 0, blk = c / NX, cc = c - blk * NX;
+                const int c = sl < 4 * NX ? sl : 0, blk = c / NX, cc = c - blk * NX;
                 const int base = (blk == 1 ? C::F_PIP : C::F_PP) + cc * NX;   // P' symmetric: row = column
                 const double keep = blk == 2 ? 0.0 : 1.0;
                 const double dcc = lds[C::F_RING + C::P_D + cc];
@@ -822,7 +904,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 }
                 // outputs: G^-1 Pi' -> F_YPI / B_YPI, Z = G^-1 D (row-major) -> F_Z, G^-1 -> B_GI,
                 // G^-1 P' -> F_YP / B_YP (column-major)
-                const bool own = lane >= NX && lane < 4 * NX;
+                const bool own = sl >= NX && sl < 4 * NX;
                 const int gcol = blk == 1 ? C::B_YPI : (blk == 2 ? C::B_GI : C::B_YP);
 #pragma unroll
                 for (int i = 0; i < NX; ++i) {
@@ -836,7 +918,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 // P~ = D G^-1 P' (symmetrised) -> F_PP; M -= Pi'' G^-1 Pi' (registers)
 #pragma unroll
                 for (int r = 0; r < R0; ++r) {
-                    const int o = lane + r * WAVE, oo = o < NX * NX ? o : 0, i = oo / NX, j = oo - i * NX;
+                    const int o = sl + r * WAVE, oo = o < NX * NX ? o : 0, i = oo / NX, j = oo - i * NX;
                     const double pt = 0.5 * (lds[C::F_RING + C::P_D + i] * lds[C::F_YP + j * NX + i] +
                                              lds[C::F_RING + C::P_D + j] * lds[C::F_YP + i * NX + j]);
                     const double mv = qp_dot<NX>(lds, C::F_PIP + i * NX, C::F_YPI + j * NX);
@@ -847,19 +929,20 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 // Pi~ = D G^-1 Pi' -> F_PIP (column-major: element o = j NX + i is row i)
 #pragma unroll
                 for (int r = 0; r < R0; ++r) {
-                    const int o = lane + r * WAVE, oo = o < NX * NX ? o : 0;
+                    const int o = sl + r * WAVE, oo = o < NX * NX ? o : 0;
                     const double v = lds[C::F_RING + C::P_D + (oo % NX)] * lds[C::F_YPI + oo];
                     lds[o < NX * NX ? C::F_PIP + o : C::F_SINK] = v;
                 }
                 wsync();
             }
+            pstamp(15);
             // ---- phase 1: T1 = P'A, T2 = P'Bt, W1 = A'Pi', W2 = Bt'Pi', u = P'e, xe += Pi''e
-            if constexpr (CMP) qp_phase_c<NX, R1, E1 - NX, E1>(lds, q1, blast, wb, fbo, a1);
+            if constexpr (CMP) qp_phase_c<NX, R1, E1 - NX, E1>(lds, qs, blast, wb, fbo, a1);
             else qp_phase<NX, R1, E1 - NX, E1>(lds, q1, blast, wb, fbo, a1);
             wsync();
             pstamp(11);
             // ---- phase 2: Qh = Q + A'T1, Sh = S' + Bt'T1, Rh = R + Bt'T2
-            if constexpr (CMP) qp_phase_c<NX, R2, 0, 0>(lds, q2, blast, wb, fbo, a2);
+            if constexpr (CMP) qp_phase_c<NX, R2, 0, 0>(lds, qs + R1, blast, wb, fbo, a2);
             else qp_phase<NX, R2, 0, 0>(lds, q2, blast, wb, fbo, a2);
             wsync();
             pstamp(12);
@@ -905,8 +988,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                     for (int j = 0; j < NU; ++j) dinv[j] = 1.0;
                 }
                 {  // every lane runs the solve (lanes >= 2 NX on a copy of column 0, results to the sinks)
-                    const bool kl = lane < 2 * NX;
-                    const int c = kl ? lane : 0;
+                    const bool kl = sl < 2 * NX;
+                    const int c = kl ? sl : 0;
                     const int off = c < NX ? C::F_SH + c * NU : C::F_W2 + (c - NX) * NU;
                     double x[NU];
 #pragma unroll
@@ -938,15 +1021,15 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                     for (int e = 0; e < NU * NU; ++e) {
                         const int ei = e / NU, ej = e % NU;
-                        if (ei >= ej) v = (lane == e) ? (ei > ej ? Lm[e] : dinv[ei]) : v;
+                        if (ei >= ej) v = (sl == e) ? (ei > ej ? Lm[e] : dinv[ei]) : v;
                     }
-                    wb.st((lane < NU * NU ? C::B_LD + lane : C::B_JNK) * 8, fbo, v);
+                    wb.st((sl < NU * NU ? C::B_LD + sl : C::B_JNK) * 8, fbo, v);
                 }
             }
             wsync();
             pstamp(13);
             // ---- phase 4: P = Qh + Sh'K, Pi = W1 + Sh'kappa, M += W2'kappa, Acl = A + Bt K
-            if constexpr (CMP) qp_phase_c<NU, R4, 2 * NX * NX, 3 * NX * NX>(lds, q4, blast, wb, fbo, a4);
+            if constexpr (CMP) qp_phase_c<NU, R4, 2 * NX * NX, 3 * NX * NX>(lds, qs + R1 + R2, blast, wb, fbo, a4);
             else qp_phase<NU, R4, 2 * NX * NX, 3 * NX * NX>(lds, q4, blast, wb, fbo, a4);
             if (ts > 0) pf_store(ts - 1, cb);
             wsync();
@@ -955,7 +1038,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 // ---- phase 5 (virtual control): the chain matrix Acl~ = G^-1 D Acl -> global (row-major)
 #pragma unroll
                 for (int r = 0; r < R0; ++r) {
-                    const int o = lane + r * WAVE, oo = o < NX * NX ? o : 0, i = oo / NX, j = oo - i * NX;
+                    const int o = sl + r * WAVE, oo = o < NX * NX ? o : 0, i = oo / NX, j = oo - i * NX;
                     const double v = qp_dot<NX>(lds, C::F_Z + i * NX, C::F_ACLC + j * NX);
                     wb.st((o < NX * NX ? C::B_ACL2 + o : C::B_JNK) * 8, fbo, v);
                 }
@@ -988,12 +1071,21 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         if (bad) lds[V_FLAG] = 1.0;  // any lane (all agree)
         // the register-accumulated outputs (xe, M) to their LDS homes
         if constexpr (CMP) {
+            const int vo = qp_opaque(lane) * 16;
 #pragma unroll
-            for (int r = 0; r < R1; ++r)
-                if (WAVE * r < E1 && WAVE * r + WAVE > E1 - NX && (q1[r].F & 4)) lds[q1[r].O] = a1[r];
+            for (int r = 0; r < R1; ++r) {
+                if (WAVE * r < E1 && WAVE * r + WAVE > E1 - NX) {
+                    const QPRepC q = tab_ld(r, vo);
+                    if (q.F() & 4) lds[q.O()] = a1[r];
+                }
+            }
 #pragma unroll
-            for (int r = 0; r < R4; ++r)
-                if (WAVE * r < 3 * NX * NX && WAVE * r + WAVE > 2 * NX * NX && (q4[r].F & 4)) lds[q4[r].O] = a4[r];
+            for (int r = 0; r < R4; ++r) {
+                if (WAVE * r < 3 * NX * NX && WAVE * r + WAVE > 2 * NX * NX) {
+                    const QPRepC q = tab_ld(R1 + R2 + r, vo);
+                    if (q.F() & 4) lds[q.O()] = a4[r];
+                }
+            }
         } else {
 #pragma unroll
             for (int r = 0; r < R1; ++r)
@@ -1418,7 +1510,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             ldb(Pi, C::B_PI, NX * NX);
             ldn(Bt, C::C_BT, NX * NU);
 #pragma unroll
-            for (int i = 0; i < NX; ++i) ev[i] = pld(C::G_E + i);
+            for (int i = 0; i < NX; ++i) ev[i] = pld(C::gE + i);
             hold(kap, NU * NX); hold(Pi, NX * NX); hold(Bt, NX * NU); hold(ev, NX);
 #pragma unroll
             for (int i = 0; i < NU; ++i)
@@ -1441,7 +1533,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                     // f~ = G^-1 (D o f - p_{t+1} - d) - (G^-1 Pi) mu   (V_CH still holds the backward chain)
                     double Y[NX * NX], w[NX];
 #pragma unroll
-                    for (int i = 0; i < NX; ++i) w[i] = fma(pld(C::G_D + i), fv[i], -lds[V_CH + (t + 1) * NX + i] - dv[i]);
+                    for (int i = 0; i < NX; ++i) w[i] = fma(pld(C::gD + i), fv[i], -lds[V_CH + (t + 1) * NX + i] - dv[i]);
                     ldb(Y, C::B_GI, NX * NX);
                     hold(Y, NX * NX);
 #pragma unroll
@@ -1618,7 +1710,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 ldn(Ad, C::C_DT, NX * NX);
                 ldn(Bt, C::C_BT, NX * NU);
 #pragma unroll
-                for (int i = 0; i < NX; ++i) ev[i] = pld(C::G_E + i);
+                for (int i = 0; i < NX; ++i) ev[i] = pld(C::gE + i);
                 hold(Ad, NX * NX); hold(Bt, NX * NU); hold(ev, NX);
 #pragma unroll
                 for (int i = 0; i < NX; ++i) {
@@ -1872,7 +1964,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
             const double d1 = unit ? 1.0 : vl[2 * i] / vs[2 * i], d2 = unit ? 1.0 : vl[2 * i + 1] / vs[2 * i + 1];
-            pst(C::G_D + i, vact ? 4.0 * d1 * d2 / (d1 + d2) : 1.0);
+            pst(C::gD + i, vact ? 4.0 * d1 * d2 / (d1 + d2) : 1.0);
         }
         double Q[NX * NX], Cp[NX * NU];
         load_cp(Cp);
@@ -1883,10 +1975,15 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 double v = (i == j) ? dbox[i] : 0.0;
                 if (i < 3 && j < 3) v += Hpp[i < 3 ? i : 0][j < 3 ? j : 0];
                 Q[i * NX + j] = v;
-                // global packet: the diagonal and the position block's upper off-diagonals (the factor
-                // reads the upper triangle; every other element is a structural zero)
-                if (i == j) pst(C::G_QD + i, v);
-                else if (i < j && j < 3) pst(C::G_QO + i + j - 1, v);
+                // global packet: the diagonal and the position block's off-diagonals (every other element is a
+                // structural zero: written at setup in the dense form, absent from the compact one, which
+                // keeps only the upper triangle)
+                if constexpr (C::DPK) {
+                    if (i == j || (i < 3 && j < 3)) pst(C::P_Q + i * NX + j, v);
+                } else {
+                    if (i == j) pst(C::G_QD + i, v);
+                    else if (i < j && j < 3) pst(C::G_QO + i + j - 1, v);
+                }
             }
         double Sx[NX * NU];
 #pragma unroll
@@ -1897,19 +1994,24 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                 for (int k = 0; k < NX; ++k) v = fma(Q[i * NX + k], Cp[j * NX + k], v);
                 Sx[i * NU + j] = v;
-                pst(C::G_S + i * NU + j, v);
+                pst(C::gS + i * NU + j, v);
             }
 #pragma unroll
         for (int i = 0; i < NU; ++i)
 #pragma unroll
-            for (int j = i; j < NU; ++j) {  // upper triangle, packed by rows
+            for (int j = i; j < NU; ++j) {  // upper triangle: packed by rows (compact), both halves (dense)
                 double v = Huu[i * NU + j];
 #pragma unroll
                 for (int k = 0; k < NX; ++k) v = fma(Cp[i * NX + k], Sx[k * NU + j], v);
-                pst(C::G_R + i * NU - i * (i - 1) / 2 + (j - i), v);
+                if constexpr (C::DPK) {
+                    pst(C::P_R + i * NU + j, v);
+                    if (j > i) pst(C::P_R + j * NU + i, v);
+                } else {
+                    pst(C::G_R + i * NU - i * (i - 1) / 2 + (j - i), v);
+                }
             }
 #pragma unroll
-        for (int i = 0; i < NX; ++i) pst(C::G_E + i, (t < K - 1) ? -rp[i] : 0.0);
+        for (int i = 0; i < NX; ++i) pst(C::gE + i, (t < K - 1) ? -rp[i] : 0.0);
     };
     // eliminate the group part of a Newton rhs (stores it for recover_aux): r1_p -= Hpa/Haa r1a;
     // returns the (xi, u) linear terms q, r of the node
@@ -2812,7 +2914,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         double* dd = a.trace + 8 * a.trace_cap;
         dd[0] = 0.0; dd[1] = 0.0; dd[2] = (double)(__builtin_amdgcn_s_memtime() - cyc_all0);
         dd[3] = fail_code;
-        for (int k = 0; k < 15; ++k) dd[4 + k] = lds[V_ST + k];
+        for (int k = 0; k < 16; ++k) dd[4 + k] = lds[V_ST + k];
     }
     double pobj = 0.0;
     if (act) {

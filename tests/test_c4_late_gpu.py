@@ -64,10 +64,13 @@ def test_c4_late_steps_match_dense_oracle(cuda):
     st = out["status"].cpu().numpy()
     stc = cold["status"].cpu().numpy()
     ow, oc = out["obj"].cpu().numpy(), cold["obj"].cpu().numpy()
-    # both optimal: each within 1e-8 (relative, absolute below |obj| = 1) of the optimal value, 2e-8 apart at
-    # most; a status-1 end on either side certifies only the reduced gap (5e-5 relative)
+    # both optimal: the stopping rule bounds the gap by 1e-8 relative, but the objective also moves by the primal
+    # residual (<= 1e-8 pnorm) times the multipliers, which reach the slack weights here (w_coll = 1e4 on the
+    # objective's 1e6 scale): a few 1e-6 relative (measured round 4: 3 of 3964 agents above 2e-8, max 4.4e-6,
+    # profiles/round4_r4n_pytest_gpu.log); a status-1 end on either side certifies only the reduced gap (5e-5)
     both = (st == 0) & (stc == 0)
-    np.testing.assert_allclose(ow[both], oc[both], rtol=2e-8, atol=2e-8)
+    np.testing.assert_allclose(ow[both], oc[both], rtol=2e-5, atol=2e-8)
+    assert np.mean(np.abs(ow[both] - oc[both]) <= 2e-8 * np.maximum(1.0, np.abs(oc[both]))) >= 0.99
     np.testing.assert_allclose(ow[~both], oc[~both], rtol=5e-5, atol=1e-8)
     print("warm vs cold: both optimal", int(both.sum()), "max rel diff where either is status 1",
           float(np.max(np.abs(ow[~both] - oc[~both]) / np.maximum(1.0, np.abs(oc[~both])), initial=0.0)))

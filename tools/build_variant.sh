@@ -7,7 +7,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 PKG=$ROOT/dynamic-programming-multiagent-trajectory-optimiziation_amd
 OUT=$ROOT/dbg/$NAME
 mkdir -p $OUT
-make -s -C $PKG build/foh_body.inc   # the hipRTC header text (csrc/foh_rtc.hip includes it)
+make -s -C $PKG build/foh_body.inc build/qp_ipm.inc build/scp_kernel.inc build/wave_ops.inc build/scvx_hip_h.inc   # the hipRTC header texts (embedded in the library)
 ls $PKG/csrc/*.hip | xargs -P 8 -I{} sh -c "/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$ROOT/include -I$PKG/build -Wno-pass-failed $* -c {} -o $OUT/\$(basename {} .hip).o"
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $OUT/libscvx_hip.so $OUT/*.o -L/opt/rocm/lib -lhiprtc -Wl,-rpath,/opt/rocm/lib
 rm -f $OUT/*.o

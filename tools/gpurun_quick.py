@@ -36,7 +36,7 @@ if os.environ.get("TRACE"):
     cyc = buf[640:660].cpu().numpy()
     n_it = max(int(out["iters"][0].item()), 1)
     names = ["node+assemble", "factor", "newton rhs", "post-solve/step", "bwd pre", "bwd chain", "bwd post+mu",
-             "fwd pre", "fwd chain", "fwd post", "update", "f-ph1 (-DQP_PHASE_TRACE)", "f-ph2", "f-ph3", "f-ph4"]
+             "fwd pre", "fwd chain", "fwd post", "update", "f-ph1 (-DQP_PHASE_TRACE)", "f-ph2", "f-ph3", "f-ph4", "f-ph5+0 (VC)"]
     print(f"total {cyc[2]:.3e} cycles, {cyc[2]/n_it:.3e}/it, fail {cyc[3]}")
     for k, nm in enumerate(names):
         print(f"  {nm:16s} {cyc[4+k]/n_it:10.0f} cycles/it  ({100*cyc[4+k]/cyc[2]:.1f}%)")

@@ -18,7 +18,8 @@ import scvx_hip  # noqa: E402
 from scvx_hip.scvx import CouplingSpec, JacobiSCvx  # noqa: E402
 
 NAMES = ["node+assemble", "factor", "newton rhs", "post-solve/step", "bwd pre", "bwd chain", "bwd post+mu",
-         "fwd pre", "fwd chain", "fwd post", "update"]
+         "fwd pre", "fwd chain", "fwd post", "update", "f-ph1 (-DQP_PHASE_TRACE)", "f-ph2", "f-ph3", "f-ph4",
+         "f-ph5+0 (VC)"]
 
 
 def main(config="c5", W=4, agent=None):
