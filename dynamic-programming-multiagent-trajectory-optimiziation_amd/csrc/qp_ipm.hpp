@@ -771,6 +771,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         // drained the packet prefetches in flight: ~100 serialised memory round trips per stage.
         constexpr bool CMP = NX > 8;
         constexpr int RT = R1 + R2 + R4;
+        static_assert(!CMP || RT == qp_nrep(NX, NU), "descriptor table size (qp_dtab, the host's workspace size)");
         const int DTB = FBB + K * C::FBS * 8;   // byte offset of the descriptor table [rep][lane] x 16 B
         QPRep q1[CMP ? 1 : R1], q2[CMP ? 1 : R2], q4[CMP ? 1 : R4];
         double a1[R1], a2[R2], a4[R4];
