@@ -513,6 +513,10 @@ def main():
     ap.add_argument("--tensor-update", action="store_true", help="c3: bookkeeping as tensor ops (not csrc/jacobi.hip)")
     ap.add_argument("--tie-rtol", type=float, default=1e-9,
                     help="c3 per-agent trust-region rule: relative margin of the cost-increase test (JacobiSCvx.tie_rtol)")
+    ap.add_argument("--dispatch-order", default="lpt", choices=("lpt", "none"),
+                    help="QP dispatch order of the Jacobi loop (JacobiSCvx.dispatch_order): lpt deals the agents "
+                         "longest-first by their previous solve's IPM iterations where they outnumber the resident "
+                         "waves (c4); none: agent order")
     ap.add_argument("--warm-status", type=int, default=1, choices=(0, 1),
                     help="JacobiSCvx.warm_max_status: warm-start agents whose last solve had status <= this "
                          "(1: optimal_inaccurate iterates too -- they meet the reduced tolerances; C4 80 -> 85 "
@@ -551,7 +555,7 @@ def main():
         spec = scvx_hip.QPSpec(model="di", K=K, box=BOX, obs=sc["obs"], w_obs=1e6, u_max=U_MAX, tol=args.tol,
                                max_iter=60)
         drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, tr_rule="per_agent", tie_rtol=args.tie_rtol,
-                         fused_update=not args.tensor_update, warm_max_status=args.warm_status)
+                         fused_update=not args.tensor_update, warm_max_status=args.warm_status, dispatch_order=args.dispatch_order)
         n_obs = N_OBS
     else:
         sc, w, cfg = make_coupled(args.config, world, rank, device)
@@ -561,7 +565,7 @@ def main():
         spec = scvx_hip.QPSpec(model=model, K=K, box=box, obs=cfg["obs"], w_obs=1e6, j_max=j_max, w_coll=1e4,
                                tol=args.tol, max_iter=60, **cfg["vc"])
         drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, coupling=CouplingSpec(R=cfg["R"]),
-                         tr_rule="global", warm_max_status=args.warm_status)
+                         tr_rule="global", warm_max_status=args.warm_status, dispatch_order=args.dispatch_order)
         if args.balance and world > 1:
             # one untimed step on contiguous shards measures every agent's IPM iterations; the shards are then
             # re-dealt so each rank gets the same mix (scvx_hip.scvx.balanced_order), and the run
@@ -573,7 +577,7 @@ def main():
             order = balanced_order(torch.cat(allit).cpu().numpy(), world)
             w = shard_tensors(sc, order[rank * N:(rank + 1) * N], device)
             drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, coupling=CouplingSpec(R=cfg["R"]),
-                             tr_rule="global", warm_max_status=args.warm_status)
+                             tr_rule="global", warm_max_status=args.warm_status, dispatch_order=args.dispatch_order)
     it_state = [w["X"].clone(), w["U"].clone()]   # the current iterate (X, U), rebound every step
 
     def step(marks=None):
@@ -683,7 +687,8 @@ def main():
             "data": data,
             "config": {"workload": workload, "agents_per_gpu": N, "K": K,
                        "parallelism": f"agents sharded x{world}" + (" (balanced order)" if (args.balance and world > 1
-                                                                         and args.config != "c3") else "")},
+                                                                         and args.config != "c3") else ""),
+                       "qp_dispatch": args.dispatch_order},
             "roofline": {"bound": "fp64_valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                          "traffic_unit": "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE; warm-started launches as in the "

@@ -115,13 +115,13 @@ extern "C" size_t scvx_qp_workspace_bytes(const scvx_qp_template* tpl, int N) {
     return ws_bytes(c, N, tpl->K);
 }
 
-extern "C" int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const double* disc, const double* sigma,
-                                     const double* Xref, const double* Uref, const double* x_init,
-                                     const double* x_final, const double* tr, const double* coll_rows,
-                                     const int32_t* coll_count, double* X, double* U, double* slack_coll,
-                                     double* nu, double* obj, int32_t* status, int32_t* iters,
-                                     const int32_t* warm, void* workspace,
-                                     size_t workspace_bytes, void* stream) {
+extern "C" int scvx_qp_solve_batched_ordered(const scvx_qp_template* tpl, int N, const double* disc,
+                                             const double* sigma, const double* Xref, const double* Uref,
+                                             const double* x_init, const double* x_final, const double* tr,
+                                             const double* coll_rows, const int32_t* coll_count, double* X, double* U,
+                                             double* slack_coll, double* nu, double* obj, int32_t* status,
+                                             int32_t* iters, const int32_t* warm, const int32_t* order,
+                                             void* workspace, size_t workspace_bytes, void* stream) {
     QPClass c;
     int rc = qp_check(tpl, N, c);
     if (rc != SCVX_OK) return rc;
@@ -145,6 +145,19 @@ extern "C" int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const d
     a.ws = (double*)workspace;
     a.ws_agent = (long long)(need / sizeof(double) / (size_t)N);
     a.trace = g_trace; a.trace_agent = g_trace_agent; a.trace_cap = g_trace_cap;
+    a.order = order;
     if (c.rt) return rtc_qp_launch(a, c.nb, c.no, c.nc, c.vc, (hipStream_t)stream);
     return c.mt->launch(c.cls, a, (hipStream_t)stream);
+}
+
+extern "C" int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const double* disc, const double* sigma,
+                                     const double* Xref, const double* Uref, const double* x_init,
+                                     const double* x_final, const double* tr, const double* coll_rows,
+                                     const int32_t* coll_count, double* X, double* U, double* slack_coll,
+                                     double* nu, double* obj, int32_t* status, int32_t* iters,
+                                     const int32_t* warm, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+    return scvx_qp_solve_batched_ordered(tpl, N, disc, sigma, Xref, Uref, x_init, x_final, tr, coll_rows, coll_count,
+                                         X, U, slack_coll, nu, obj, status, iters, warm, nullptr, workspace,
+                                         workspace_bytes, stream);
 }

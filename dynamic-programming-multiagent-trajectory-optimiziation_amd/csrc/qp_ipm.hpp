@@ -73,6 +73,7 @@ struct QPArgs {
     long long ws_agent;  // doubles per agent
     double* trace;       // optional per-iteration diagnostics of agent `trace_agent` (or nullptr)
     int trace_agent, trace_cap;
+    const int32_t* order;  // optional dispatch order: workgroup b solves agent order[b] (nullptr: agent b)
 };
 
 // ---- sizes shared by host (workspace / LDS bytes) and device
@@ -440,7 +441,14 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     extern __shared__ double lds[];
     const scvx_qp_template& T = a.T;
     const int K = T.K, lane = threadIdx.x, t = lane;
-    const long long agent = blockIdx.x;
+    // dispatch order: workgroups start in index order as slots free up, so when the agents outnumber the resident
+    // waves (C4: 4096 agents, 1024 at a time) the host can deal the longest solves first (scvx_qp_solve_batched_ordered);
+    // an entry outside [0, N) falls back to the workgroup's own index
+    long long agent = blockIdx.x;
+    if (a.order) {
+        const int o = a.order[blockIdx.x];
+        agent = (o >= 0 && o < a.N) ? o : (long long)blockIdx.x;
+    }
     const bool act = t < K;
     const bool ineq = act && ((t < K - 1) || T.ineq_last);
     const bool fin = T.has_final != 0;

@@ -302,12 +302,16 @@ class QPSolver:
             if tuple(t.shape) != shp:
                 raise ValueError(f"QPSolver.solve: {name} has shape {tuple(t.shape)}, expected {shp}")
 
+    supports_order = True
+
     def solve(self, disc, sigma, Xref, Uref, x_init, x_final, tr, coll_rows=None, coll_count=None, stream=None, n=None,
-              warm=None):
+              warm=None, order=None):
         """n (<= N): solve only n agents (the inputs' leading dimension); the outputs are the leading n rows
         of the solver's buffers.  warm (N,) int32 device tensor or None: agents with warm != 0 start from the
         primal-dual point of their previous solve by THIS solver (the same agent slot), e.g. the previous
-        SCvx iteration's status == 0.  Returns dict of device tensors (views of reused buffers)."""
+        SCvx iteration's status == 0.  order (n,) int32 device tensor or None: the dispatch order, a
+        permutation of range(n) (scvx_qp_solve_batched_ordered; results do not depend on it).  Returns dict
+        of device tensors (views of reused buffers)."""
         torch = _torch()
         n = self.N if n is None else int(n)
         if not 0 <= n <= self.N:
@@ -323,14 +327,18 @@ class QPSolver:
         if warm is not None and n > self._state_n:   # slots never solved by this solver start cold
             warm = warm.clone()
             warm[self._state_n:] = 0
-        rc = lib().scvx_qp_solve_batched(
+        if order is not None and (tuple(order.shape) != (n,) or order.dtype != torch.int32):
+            raise ValueError(f"QPSolver.solve: order must be an int32 ({n},) permutation, got "
+                             f"{tuple(order.shape)} {order.dtype}")
+        rc = lib().scvx_qp_solve_batched_ordered(
             ctypes.byref(self.ctpl), n, _dev(disc, name="disc"), _dev(sigma, name="sigma"),
             _dev(Xref, name="Xref"), _dev(Uref, name="Uref"), _dev(x_init, name="x_init"), _dev(xf, name="x_final"),
             _dev(tr, name="tr"), _dev(coll_rows, name="coll_rows"), _dev(coll_count, torch.int32, "coll_count"),
             _dev(self.X), _dev(self.U), _dev(self.slack), _dev(self.nu), _dev(self.obj), _dev(self.status, torch.int32),
             _dev(self.iters, torch.int32), _dev(warm, torch.int32, "warm") if warm is not None else None,
+            _dev(order, torch.int32, "order") if order is not None else None,
             _dev(self.workspace), ctypes.c_size_t(self.workspace.numel() * 8), _stream(stream))
-        check(rc, "scvx_qp_solve_batched")
+        check(rc, "scvx_qp_solve_batched_ordered")
         self._state_n = max(self._state_n, n)
         out = self._outputs()
         return out if n == self.N else {k: v[:n] for k, v in out.items()}

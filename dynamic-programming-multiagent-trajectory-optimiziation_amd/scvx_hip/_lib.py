@@ -21,7 +21,7 @@ STATUS = {0: "optimal", 1: "optimal_inaccurate", 2: "solver_error"}
 
 # every symbol declared in include/scvx_hip.h
 EXPORTS = ("scvx_version", "scvx_last_error", "scvx_foh_batched", "scvx_integrate_nonlinear_batched",
-           "scvx_qp_solve_batched", "scvx_qp_workspace_bytes", "scvx_qp_set_trace",
+           "scvx_qp_solve_batched", "scvx_qp_solve_batched_ordered", "scvx_qp_workspace_bytes", "scvx_qp_set_trace",
            "scvx_collision_rows_batched", "scvx_collision_rows_indexed", "scvx_collision_check_batched", "scvx_scp_solve_batched", "scvx_scp_workspace_bytes",
            "scvx_scp_set_waves_per_agent",
            "scvx_intersample_batched", "scvx_admm_consensus_batched", "scvx_scp_game_solve_batched",
@@ -106,6 +106,7 @@ def lib():
         L.scvx_qp_workspace_bytes.argtypes = [ctypes.POINTER(QPTemplate), i32]
         L.scvx_qp_workspace_bytes.restype = sz
         L.scvx_qp_solve_batched.argtypes = [ctypes.POINTER(QPTemplate), i32] + [vp] * 17 + [vp, sz, vp]
+        L.scvx_qp_solve_batched_ordered.argtypes = [ctypes.POINTER(QPTemplate), i32] + [vp] * 18 + [vp, sz, vp]
         L.scvx_qp_set_trace.argtypes = [vp, i32, i32]
         L.scvx_scp_set_waves_per_agent.argtypes = [i32]
         L.scvx_collision_rows_batched.argtypes = [i32, i32, i32, i32, vp, i32, i32, dbl, dbl, i32, vp, vp, vp]

@@ -202,6 +202,19 @@ int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const double* disc
                           double* U, double* slack_coll, double* nu, double* obj, int32_t* status, int32_t* iters,
                           const int32_t* warm, void* workspace, size_t workspace_bytes, void* stream);
 
+/* scvx_qp_solve_batched with a dispatch order (replaces the same call, qp_capi.hip; the reference has no
+ * counterpart -- its agents' subproblems are solved one by one, dist_scvx_3d.py:110): workgroup b solves agent
+ * order[b] (device int32 [N], a permutation of 0..N-1; NULL = agent b; an entry outside [0, N) falls back to b).
+ * Workgroups start in index order as slots free up, so when the agents outnumber the resident waves the
+ * longest solves dealt first shorten the launch (JacobiSCvx orders by the last step's IPM iterations).
+ * Results do not depend on the order. */
+int scvx_qp_solve_batched_ordered(const scvx_qp_template* tpl, int N, const double* disc, const double* sigma,
+                                  const double* Xref, const double* Uref, const double* x_init,
+                                  const double* x_final, const double* tr, const double* coll_rows,
+                                  const int32_t* coll_count, double* X, double* U, double* slack_coll, double* nu,
+                                  double* obj, int32_t* status, int32_t* iters, const int32_t* warm,
+                                  const int32_t* order, void* workspace, size_t workspace_bytes, void* stream);
+
 /* Bytes of caller-owned device scratch scvx_qp_solve_batched needs for N agents. */
 size_t scvx_qp_workspace_bytes(const scvx_qp_template* tpl, int N);
 
