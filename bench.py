@@ -688,7 +688,8 @@ def main():
             "config": {"workload": workload, "agents_per_gpu": N, "K": K,
                        "parallelism": f"agents sharded x{world}" + (" (balanced order)" if (args.balance and world > 1
                                                                          and args.config != "c3") else ""),
-                       "qp_dispatch": args.dispatch_order},
+                       "qp_dispatch": "longest-first (last-step IPM iterations)" if getattr(drv, "_lpt", False)
+                       else "agent order"},
             "roofline": {"bound": "fp64_valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                          "traffic_unit": "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE; warm-started launches as in the "
