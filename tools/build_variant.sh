@@ -1,11 +1,11 @@
 #!/bin/bash
-# Diagnostics: build libscvx_hip.so with extra -D flags into dbg/<name>/ (load it with SCVX_HIP_LIB=...).
+# Diagnostics: build libscvx_hip.so with extra -D flags into variants/<name>/ (load it with SCVX_HIP_LIB=...).
 # usage: tools/build_variant.sh <name> [-DFLAG ...]
 set -e
 NAME=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 PKG=$ROOT/dynamic-programming-multiagent-trajectory-optimiziation_amd
-OUT=$ROOT/dbg/$NAME
+OUT=$ROOT/variants/$NAME
 mkdir -p $OUT
 make -s -C $PKG build/foh_body.inc build/qp_ipm.inc build/scp_kernel.inc build/wave_ops.inc build/scvx_hip_h.inc   # the hipRTC header texts (embedded in the library)
 # QUAD_FLAGS: extra flags for the n = 12 translation unit only (qp_inst_quad.hip), as the Makefile's per-file flags
