@@ -94,7 +94,7 @@ int qp_check(const scvx_qp_template* T, int N, QPClass& c) {
 
 size_t ws_bytes(const QPClass& c, int N, int K) {
     const int nv = c.vc ? c.nx : 0, ns = c.no + c.nc, ng = c.no + (c.nc > 0 ? 1 : 0);
-    return sizeof(double) * (size_t)N * (size_t)qp_ws_doubles(c.nx, c.nu, c.nb, ns, ng, K, nv);
+    return sizeof(double) * (size_t)N * (size_t)qp_ws_doubles(c.nx, c.nu, c.nb, ns, ng, K, nv, c.nc);
 }
 }  // namespace
 

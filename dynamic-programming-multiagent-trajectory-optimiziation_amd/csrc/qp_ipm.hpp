@@ -78,12 +78,21 @@ struct QPArgs {
 
 // ---- sizes shared by host (workspace / LDS bytes) and device
 constexpr int qp_dstr(int nx, int nu) { return nx * (nx + 2 * nu + 2); }
-constexpr int qp_pkt(int nx, int nu, int nv = 0) { return 2 * nx * nx + 4 * nx * nu + nu * nu + nx + nv; }
+// stiff trust-region facets (the coupled classes, n <= 8, 2 <= m <= 4; see QPCfg::STF): the 2^m facet weights, their
+// folded sum (diagonal and upper off-diagonals of sum_f D_f g_f g_f') and their maximum ride in the packet; at most
+// m-1 of them stay explicit per stage
+constexpr bool qp_stf(int nx, int nu, int nc) { return nx <= 8 && nu >= 2 && nu <= 4 && nc > 0; }
+constexpr int qp_pm(int nx, int nu, int nc) { return qp_stf(nx, nu, nc) ? nu - 1 : 0; }
+constexpr int qp_nfd(int nx, int nu, int nc) { return qp_stf(nx, nu, nc) ? (1 << nu) + 2 + nu * (nu - 1) / 2 : 0; }
+constexpr int qp_pkt(int nx, int nu, int nv = 0, int nc = 0) {
+    return 2 * nx * nx + 4 * nx * nu + nu * nu + nx + nv + qp_nfd(nx, nu, nc);
+}
 // global packet: n <= 8 compact (Q as its diagonal + the 3 off-diagonals of the position block, S, R upper
 // packed, e, A, Bt (column-major), C_{t-1}, the virtual control's D) -- expanded to the LDS packet layout by the
 // factor's prefetch through a per-lane gather table; n = 12 dense (the LDS layout itself, QPCfg::DPK)
-constexpr int qp_gpk(int nx, int nu, int nv = 0) {
-    return nx > 8 ? qp_pkt(nx, nu, nv) : (nx + 3) + nx * nu + nu * (nu + 1) / 2 + nx + nx * nx + 2 * nx * nu + nv;
+constexpr int qp_gpk(int nx, int nu, int nv = 0, int nc = 0) {
+    return nx > 8 ? qp_pkt(nx, nu, nv, nc)
+                  : (nx + 3) + nx * nu + nu * (nu + 1) / 2 + nx + nx * nx + 2 * nx * nu + nv + qp_nfd(nx, nu, nc);
 }
 constexpr int qp_even(int x) { return (x + 1) & ~1; }
 // workspace columns (K doubles each: one per node) of a capacity class
@@ -95,8 +104,12 @@ constexpr int qp_ncol(int nx, int nu, int nb, int ns, int ng, int nv = 0) {
            ((1 << nu) + 2 * nb + ns + ng) + 1 + (nx > 8 ? 2 * ((1 << nu) + 2 * nb + ns + ng) : 0);
 }
 // factor outputs per stage (stage-major block): K, kappa, LD, W2, P, Pi, u, Acl, [virtual control: G^-1 P,
-// G^-1 Pi, G^-1, Acl~], one junk slot (the global store of lanes without an output of their own)
-constexpr int qp_fbs(int nx, int nu, int nv = 0) { return 3 * nu * nx + nu * nu + 3 * nx * nx + nx + 4 * nv * nx + 1; }
+// G^-1 Pi, G^-1, Acl~], [stiff facets: Gamma, Gamma_kappa, W, C^-1, facet indices], one junk slot (the global
+// store of lanes without an output of their own)
+constexpr int qp_fbs(int nx, int nu, int nv = 0, int nc = 0) {
+    return 3 * nu * nx + nu * nu + 3 * nx * nx + nx + 4 * nv * nx +
+           qp_pm(nx, nu, nc) * (2 * nx + nu + qp_pm(nx, nu, nc) + 1) + 1;
+}
 // per agent: columns [c][K], packets [K][GPK], factor blocks [K][FBS] -- only the K nodes: lanes >= K
 // address past the end of the buffer (loads read 0, stores are dropped), so the agent's footprint is
 // what its nodes touch (C3: 1024 agents x 199 KB stay inside the 256 MB Infinity Cache)
@@ -106,14 +119,15 @@ constexpr int qp_nrep(int nx, int nu) {
     return (2 * nx * nx + 2 * nx * nu + 2 * nx + 63) / 64 + (nx * nx + nu * nx + nu * nu + 63) / 64 + (4 * nx * nx + 63) / 64;
 }
 constexpr int qp_dtab(int nx, int nu) { return nx > 8 ? qp_nrep(nx, nu) * 64 * 2 : 0; }
-constexpr long long qp_ws_doubles(int nx, int nu, int nb, int ns, int ng, int K, int nv = 0) {
-    return (long long)K * (qp_ncol(nx, nu, nb, ns, ng, nv) + qp_gpk(nx, nu, nv) + qp_fbs(nx, nu, nv)) + qp_dtab(nx, nu);
+constexpr long long qp_ws_doubles(int nx, int nu, int nb, int ns, int ng, int K, int nv = 0, int nc = 0) {
+    return (long long)K * (qp_ncol(nx, nu, nb, ns, ng, nv) + qp_gpk(nx, nu, nv, nc) + qp_fbs(nx, nu, nv, nc)) +
+           qp_dtab(nx, nu);
 }
 // LDS doubles of a class (QPCfg::lds_doubles, written out for the host of a runtime-compiled class, which
 // has no QPCfg instantiation; QPCfg asserts that both agree)
 constexpr int qp_lds_doubles(int nx, int nu, int nb, int no, int nc, int vc, int K) {
     const int nv = vc ? nx : 0;
-    const int pkt = qp_pkt(nx, nu, nv);
+    const int pkt = qp_pkt(nx, nu, nv, nc);
     const int f_sink = pkt + 5 * nx * nx + 5 * nx * nu + nu * nu;
     const int f_end = qp_even(f_sink + (nx > 8 ? nx : 8) + 4 * nv * nx);
     const int nr = (1 << nu) + 2 * nb + no + nc + no + (nc > 0 ? 1 : 0);
@@ -124,6 +138,9 @@ constexpr int qp_lds_doubles(int nx, int nu, int nb, int no, int nc, int vc, int
 constexpr int QP_OOB = 0x40000000;
 // warm start: floor of every slack and dual of the previous iterate (scaled units; oracle/scvx_cpu.cpp)
 constexpr double QP_WARM_ETA = 1e-3;
+// stiff trust-region facet: its barrier weight D = lambda / s above QP_STIFF x the largest diagonal entry of the rest
+// of the stage's input Hessian Rhat (oracle/scvx_cpu.cpp STIFF_RATIO, the same rule)
+constexpr double QP_STIFF = 1e6;
 // fraction-to-boundary of the end game (affine step >= 0.99).  In the warm-started Jacobi loop almost every
 // solve is an end game from its first iteration: each step is a full Newton step up to this fraction, so
 // the gap falls by 1 / (1 - QP_TAU_END) per iteration.  0.999 took the C3 bulk 5 iterations, 1 - 1e-5 takes
@@ -151,15 +168,24 @@ struct QPCfg {
     // factor packet [t][PKT]: node Hessian Q|S|R, e, then the constant A (column-major) | Bt
     // column-major | Bt row-major | C_{t-1} (column-major).  Every dot product of the factor
     // phases then reads two contiguous LDS vectors.
+    // stiff trust-region facets (STF: the coupled classes, n <= 8 and 2 <= m <= 4): the node's R leaves the 2^m
+    // facets' D g g' out; their weights D_f, their folded sum and max ride in the packet (P_FD) and factor phase 3
+    // folds them back into Rhat, all but at most PM = m-1 stiff ones, which stay explicit stage unknowns (Woodbury;
+    // see the factor).  The uncoupled classes (C3) fold the facets into R as before: no stiff facet has failed a
+    // C3 solve, and the stage work costs ~13 % of an IPM iteration there (round 5 A/B).
+    static constexpr bool STF = qp_stf(NX_, NU_, NC_);
+    static constexpr int NFD = qp_nfd(NX_, NU_, NC_), PM = qp_pm(NX_, NU_, NC_), PMA = PM > 0 ? PM : 1;
+    // packet: the facet weights | their folded sum (diagonal, upper off-diagonals) | their maximum
+    static constexpr int NFO = NU_ * (NU_ - 1) / 2;
     static constexpr int P_Q = 0, P_S = P_Q + NX * NX, P_R = P_S + NX * NU, P_E = P_R + NU * NU,
                          P_A = P_E + NX, P_BT = P_A + NX * NX, P_BTR = P_BT + NX * NU, P_C = P_BTR + NX * NU,
-                         P_D = P_C + NX * NU, PKT = P_D + NV;
-    static_assert(PKT == qp_pkt(NX, NU, NV), "packet size");
+                         P_D = P_C + NX * NU, P_FD = P_D + NV, PKT = P_FD + NFD;
+    static_assert(PKT == qp_pkt(NX, NU, NV, NC), "packet size");
     // global packet (compact, n <= 8; qp_gpk): Q diagonal | Q position-block off-diagonals (0,1) (0,2) (1,2) |
     // S | R upper packed | e | A (column-major) | Bt (column-major) | C_{t-1} (column-major) | D
     static constexpr int G_QD = 0, G_QO = G_QD + NX, G_S = G_QO + 3, G_R = G_S + NX * NU,
                          G_E = G_R + NU * (NU + 1) / 2, G_A = G_E + NX, G_BT = G_A + NX * NX, G_C = G_BT + NX * NU,
-                         G_D = G_C + NX * NU;
+                         G_D = G_C + NX * NU, G_FD = G_D + NV;
     // n = 12 (DPK): the global packet has the LDS layout element for element.  The compact form needs a per-lane
     // gather table of PFN offsets live across the factor sweep; at n = 12 the register allocator spilled it to
     // scratch, and every reload waited for the packet prefetches in flight.  The dense prefetch is one
@@ -168,8 +194,8 @@ struct QPCfg {
     // halves), e, D.  (n <= 8 keeps the compact form: its 3-entry table costs nothing, the dense packet's extra
     // traffic does: C3 780 -> 742 SCvx-it/s, A/B round 4.)
     static constexpr bool DPK = NX > 8;
-    static constexpr int GPK = DPK ? PKT : G_D + NV;
-    static_assert(GPK == qp_gpk(NX, NU, NV), "global packet size");
+    static constexpr int GPK = DPK ? PKT : G_FD + NFD;
+    static_assert(GPK == qp_gpk(NX, NU, NV, NC), "global packet size");
     static_assert(NX >= 3, "the position block is 3 x 3");
     // global packet element of LDS packet element e (-1: a structural zero)
     static constexpr int gsrc(int e) {
@@ -193,11 +219,12 @@ struct QPCfg {
             return G_BT + j * NX + i;
         }
         if (e < P_D) return G_C + (e - P_C);
-        return G_D + (e - P_D);
+        if (e < P_FD) return G_D + (e - P_D);
+        return G_FD + (e - P_FD);
     }
     // global packet index of the node-phase outputs e, D and of the constant blocks
     static constexpr int gE = DPK ? P_E : G_E, gD = DPK ? P_D : G_D, gS = DPK ? P_S : G_S, gA = DPK ? P_A : G_A,
-                         gBT = DPK ? P_BT : G_BT, gC = DPK ? P_C : G_C;
+                         gBT = DPK ? P_BT : G_BT, gC = DPK ? P_C : G_C, gFD = DPK ? P_FD : G_FD;
     static_assert(NX <= 16, "the solve chains broadcast within one 16-lane row");
     // factor outputs: stage-major blocks [t][FBS] (coalesced stores from the element-parallel
     // factor; each lane-parallel pass reads its own stage's block)
@@ -214,9 +241,15 @@ struct QPCfg {
     static constexpr int B_YP = B_ACL + NX * NX, B_YPI = B_YP + NV * NX, B_GI = B_YPI + NV * NX,
                          B_ACL2 = B_GI + NV * NX;
     static constexpr int B_CH = NV > 0 ? B_ACL2 : B_ACL;  // what the solve chains read
-    static constexpr int B_JNK = B_ACL2 + NV * NX;  // junk slot (stores of lanes without an output)
+    // stiff facets (STF): Gamma = -C^-1 G' R0^-1 Sh and Gamma_kappa = -C^-1 G' R0^-1 W2 (PM x NX, row-major: the
+    // multiplier steps nu = Gamma xi + Gamma_kappa mu + gamma0), then W = R0^-1 G (NU x PM), C^-1 (PM x PM) and the
+    // stiff facets' indices (PM, -1 = empty slot)
+    static constexpr int B_GAM = B_ACL2 + NV * NX, B_GAK = B_GAM + PM * NX, B_WS = B_GAK + PM * NX,
+                         B_CI = B_WS + NU * PM, B_SF = B_CI + PM * PM;
+    static constexpr int NSMB = NU * PM + PM * PM + PM;   // W | C^-1 | indices: one small block
+    static constexpr int B_JNK = B_SF + PM;  // junk slot (stores of lanes without an output)
     static constexpr int FBS = B_JNK + 1;
-    static_assert(FBS == qp_fbs(NX, NU, NV), "factor block");
+    static_assert(FBS == qp_fbs(NX, NU, NV, NC), "factor block");
     // stage-minor workspace columns
     static constexpr int C_DT = 0;                 // disc, transposed: A (col-major) | B | C | S | z
     static constexpr int C_BT = C_DT + DSTR;       // Bt_t (row-major)
@@ -958,9 +991,84 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             // ---- phase 3: Rh = L D L' in registers (every lane); [K | kappa] = -Rh^-1 [Sh | W2]
             {
                 const bool fx = last && T.fix_last_input;
+                constexpr int PM = C::PM, PMA = C::PMA;
                 double Lm[NU * NU], dinv[NU];
 #pragma unroll
                 for (int e = 0; e < NU * NU; ++e) Lm[e] = lds[C::F_RH + e];
+                // stiff trust-region facets (STF): Rhat arrives without the facets.  Those whose weight exceeds
+                // QP_STIFF x its largest diagonal stay explicit when there are at most m-1 of them and no two are
+                // opposite (a face or an edge of the L1 ball: they leave a complement whose small curvature the fold
+                // would lose); the others fold back.  m or more stiff ones (a vertex) make every direction of u stiff:
+                // they fold too, the folded sum then loses nothing while the Woodbury form would cancel
+                // (oracle/scvx_cpu.cpp, the same rule)
+                int sfi[PMA];
+                double sfd[PMA];
+#pragma unroll
+                for (int i = 0; i < PMA; ++i) { sfi[i] = -1; sfd[i] = 1.0; }
+                bool stg = false;   // this stage keeps a stiff facet (every lane agrees)
+                if constexpr (C::STF) {
+                    constexpr int NTR = C::NTR, NFO = C::NFO, FS = C::F_RING + C::P_FD + NTR;
+                    double dnf = 0.0;
+#pragma unroll
+                    for (int j = 0; j < NU; ++j) dnf = fmax(dnf, fabs(Lm[j * NU + j]));
+                    const double thr = QP_STIFF * dnf;
+                    // common case: every facet folds (their sum, formed in the node phase)
+                    {
+                        int e = 0;
+#pragma unroll
+                        for (int i = 0; i < NU; ++i) {
+                            Lm[i * NU + i] += lds[FS];
+#pragma unroll
+                            for (int j = i + 1; j < NU; ++j, ++e) {
+                                const double o = lds[FS + 1 + e];
+                                Lm[i * NU + j] += o;
+                                Lm[j * NU + i] += o;
+                            }
+                        }
+                    }
+                    if (lds[FS + 1 + NFO] > thr && !fx) {   // rare: pick the stiff slots, fold only the others
+                        double Df[NTR];
+                        int cnt = 0;
+#pragma unroll
+                        for (int f = 0; f < NTR; ++f) {
+                            Df[f] = lds[C::F_RING + C::P_FD + f];
+                            const bool above = Df[f] > thr;
+#pragma unroll
+                            for (int i = 0; i < PM; ++i) {
+                                sfi[i] = (above && cnt == i) ? f : sfi[i];
+                                sfd[i] = (above && cnt == i) ? Df[f] : sfd[i];
+                            }
+                            cnt += above ? 1 : 0;
+                        }
+                        bool opp = false;
+#pragma unroll
+                        for (int i = 0; i < PM; ++i)
+#pragma unroll
+                            for (int k = i + 1; k < PM; ++k) opp |= sfi[i] >= 0 && sfi[k] >= 0 && (sfi[i] ^ sfi[k]) == NTR - 1;
+                        const bool use = cnt <= PM && !opp;
+#pragma unroll
+                        for (int i = 0; i < PM; ++i) {
+                            sfi[i] = use ? sfi[i] : -1;
+                            sfd[i] = use ? sfd[i] : 1.0;
+                        }
+                        if (use) {
+#pragma unroll
+                            for (int e = 0; e < NU * NU; ++e) Lm[e] = lds[C::F_RH + e];
+#pragma unroll
+                            for (int f = 0; f < NTR; ++f) {
+                                bool st = false;
+#pragma unroll
+                                for (int i = 0; i < PM; ++i) st |= sfi[i] == f;
+                                const double d = st ? 0.0 : Df[f];
+#pragma unroll
+                                for (int i = 0; i < NU; ++i)
+#pragma unroll
+                                    for (int j = 0; j < NU; ++j) Lm[i * NU + j] += (((f >> i) ^ (f >> j)) & 1) ? -d : d;
+                            }
+                        }
+                        stg = use;
+                    }
+                }
                 double dmax = 0.0;
 #pragma unroll
                 for (int j = 0; j < NU; ++j) dmax = fmax(dmax, fabs(Lm[j * NU + j]));
@@ -996,26 +1104,107 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                     for (int j = 0; j < NU; ++j) dinv[j] = 1.0;
                 }
+                // x <- R0^-1 x with R0 = L D L'
+                auto ldl_solve = [&](double* x) __attribute__((always_inline)) {
+#pragma unroll
+                    for (int i = 0; i < NU; ++i) {
+#pragma unroll
+                        for (int k = 0; k < i; ++k) x[i] -= Lm[i * NU + k] * x[k];
+                    }
+#pragma unroll
+                    for (int i = 0; i < NU; ++i) x[i] *= dinv[i];
+#pragma unroll
+                    for (int i = NU - 1; i >= 0; --i) {
+#pragma unroll
+                        for (int k = i + 1; k < NU; ++k) x[i] -= Lm[k * NU + i] * x[k];
+                    }
+                };
+                // Woodbury pieces of the stiff facets (STF): Rhat^-1 = R0^-1 - W C^-1 W', W = R0^-1 G,
+                // C = D^-1 + G'W; an empty slot has g = 0, so W = 0, C = 1 there and it changes nothing
+                double Wm[NU * PMA], Ci[PMA * PMA];
+#pragma unroll
+                for (int e = 0; e < NU * PMA; ++e) Wm[e] = 0.0;
+#pragma unroll
+                for (int e = 0; e < PMA * PMA; ++e) Ci[e] = (e / PMA == e % PMA) ? 1.0 : 0.0;
+                if (C::STF && stg) {
+#pragma unroll
+                    for (int i = 0; i < PM; ++i) {
+                        double w[NU];
+#pragma unroll
+                        for (int j = 0; j < NU; ++j) w[j] = sfi[i] < 0 ? 0.0 : (((sfi[i] >> j) & 1) ? -1.0 : 1.0);
+                        ldl_solve(w);
+#pragma unroll
+                        for (int j = 0; j < NU; ++j) Wm[j * PM + i] = w[j];
+                    }
+                    double Cm[PMA * PMA];
+#pragma unroll
+                    for (int i = 0; i < PM; ++i)
+#pragma unroll
+                        for (int k = 0; k < PM; ++k) {
+                            double v = (i == k) ? (sfi[i] < 0 ? 1.0 : 1.0 / sfd[i]) : 0.0;
+#pragma unroll
+                            for (int j = 0; j < NU; ++j)
+                                v += (sfi[i] < 0 ? 0.0 : (((sfi[i] >> j) & 1) ? -1.0 : 1.0)) * Wm[j * PM + k];
+                            Cm[i * PM + k] = v;
+                        }
+                    // C^-1 by Gauss-Jordan without pivoting (C is symmetric positive definite)
+#pragma unroll
+                    for (int e = 0; e < PM * PM; ++e) Ci[e] = (e / PM == e % PM) ? 1.0 : 0.0;
+#pragma unroll
+                    for (int k = 0; k < PM; ++k) {
+                        const double rp = 1.0 / Cm[k * PM + k];
+#pragma unroll
+                        for (int j = 0; j < PM; ++j) { Cm[k * PM + j] *= rp; Ci[k * PM + j] *= rp; }
+#pragma unroll
+                        for (int i = 0; i < PM; ++i) {
+                            if (i == k) continue;
+                            const double f = Cm[i * PM + k];
+#pragma unroll
+                            for (int j = 0; j < PM; ++j) {
+                                Cm[i * PM + j] = fma(-f, Cm[k * PM + j], Cm[i * PM + j]);
+                                Ci[i * PM + j] = fma(-f, Ci[k * PM + j], Ci[i * PM + j]);
+                            }
+                        }
+                    }
+                    bad |= !(Ci[0] == Ci[0]);
+                }
                 {  // every lane runs the solve (lanes >= 2 NX on a copy of column 0, results to the sinks)
                     const bool kl = sl < 2 * NX;
                     const int c = kl ? sl : 0;
                     const int off = c < NX ? C::F_SH + c * NU : C::F_W2 + (c - NX) * NU;
                     double x[NU];
 #pragma unroll
-                    for (int i = 0; i < NU; ++i) {
-                        double v = lds[off + i];
+                    for (int i = 0; i < NU; ++i) x[i] = lds[off + i];
+                    ldl_solve(x);
+                    if constexpr (C::STF) {
+                        // x -= W C^-1 G'x; the multiplier-step coefficients -C^-1 G'x -> Gamma / Gamma_kappa
+                        double gx[PMA], zc[PMA];
 #pragma unroll
-                        for (int k = 0; k < i; ++k) v -= Lm[i * NU + k] * x[k];
-                        x[i] = v;
-                    }
+                        for (int i = 0; i < PMA; ++i) zc[i] = 0.0;
+                        if (stg) {
 #pragma unroll
-                    for (int i = 0; i < NU; ++i) x[i] *= dinv[i];
+                        for (int i = 0; i < PM; ++i) {
+                            double v = 0.0;
 #pragma unroll
-                    for (int i = NU - 1; i >= 0; --i) {
-                        double v = x[i];
+                            for (int j = 0; j < NU; ++j)
+                                v += (sfi[i] < 0 ? 0.0 : (((sfi[i] >> j) & 1) ? -1.0 : 1.0)) * x[j];
+                            gx[i] = v;
+                        }
 #pragma unroll
-                        for (int k = i + 1; k < NU; ++k) v -= Lm[k * NU + i] * x[k];
-                        x[i] = v;
+                        for (int i = 0; i < PM; ++i) {
+                            double v = 0.0;
+#pragma unroll
+                            for (int k = 0; k < PM; ++k) v = fma(Ci[i * PM + k], gx[k], v);
+                            zc[i] = v;
+                        }
+#pragma unroll
+                        for (int j = 0; j < NU; ++j)
+#pragma unroll
+                            for (int i = 0; i < PM; ++i) x[j] = fma(-Wm[j * PM + i], zc[i], x[j]);
+                        }
+                        const int gb = c < NX ? C::B_GAM + c : C::B_GAK + c - NX;
+#pragma unroll
+                        for (int i = 0; i < PM; ++i) wb.st((kl ? gb + i * NX : C::B_JNK) * 8, fbo, fx ? 0.0 : -zc[i]);
                     }
                     const int g = c < NX ? C::B_K + c : C::B_KAP + c - NX;
 #pragma unroll
@@ -1033,6 +1222,16 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                         if (ei >= ej) v = (sl == e) ? (ei > ej ? Lm[e] : dinv[ei]) : v;
                     }
                     wb.st((sl < NU * NU ? C::B_LD + sl : C::B_JNK) * 8, fbo, v);
+                }
+                if constexpr (C::STF) {   // lane e < NSMB stores element e of W | C^-1 | stiff indices
+                    double v = 0.0;
+#pragma unroll
+                    for (int e = 0; e < NU * PM; ++e) v = (sl == e) ? Wm[e] : v;
+#pragma unroll
+                    for (int e = 0; e < PM * PM; ++e) v = (sl == NU * PM + e) ? Ci[e] : v;
+#pragma unroll
+                    for (int e = 0; e < PM; ++e) v = (sl == NU * PM + PM * PM + e) ? (double)sfi[e] : v;
+                    wb.st((sl < C::NSMB ? C::B_WS + sl : C::B_JNK) * 8, fbo, v);
                 }
             }
             wsync();
@@ -1246,9 +1445,14 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     // Virtual control: stage t sees P~ = D G^-1 P_{t+1} and p~ = p_{t+1} - (G^-1 P)'(p_{t+1} + d) in place of
     // P_{t+1}, p_{t+1} (oracle/scvx_cpu.cpp riccati_factor), the chains run on Acl~ = G^-1 D Acl, and
     // nu_t = xi_{t+1} - (A xi_t + Bt du_t + e_t) comes out of the forward chain.
-    auto solve = [&](const double* q, const double* r, const double* dv, double* dzo, double* dyo, double* dno)
-                     __attribute__((always_inline)) {
-        // ---- backward pre-pass: g = q + K'r + Acl'(P~ e - (G^-1 P)'d)
+    // rhs_s: rho of the stage's stiff facets (C::STF; 0 in empty slots), fnu: their multiplier steps (out)
+    auto solve = [&](const double* q, const double* r, const double* dv, double* dzo, double* dyo, double* dno,
+                     const double* rhs_s, double* fnu) __attribute__((always_inline)) {
+        constexpr int PM = C::PM, PMA = C::PMA;
+        double g0[PMA];   // nu's feed-forward part gamma0 = -C^-1 (G' R0^-1 rh + rho) (stiff facets)
+#pragma unroll
+        for (int i = 0; i < PMA; ++i) { g0[i] = 0.0; fnu[i] = 0.0; }
+        // ---- backward pre-pass: g = q + K'r + Acl'(P~ e - (G^-1 P)'d) [- Gamma' rho: stiff facets]
         fresh();
         if (act) {
             double g[NX], u[NX];
@@ -1271,6 +1475,15 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             hold(Ac, NX * NX);
 #pragma unroll
             for (int i = 0; i < NX; ++i) g[i] = q[i];
+            if constexpr (C::STF) {
+                double Gm[PMA * NX];
+                ldb(Gm, C::B_GAM, PM * NX);
+                hold(Gm, PM * NX);
+#pragma unroll
+                for (int i = 0; i < PM; ++i)
+#pragma unroll
+                    for (int j = 0; j < NX; ++j) g[j] = fma(-Gm[i * NX + j], rhs_s[i], g[j]);
+            }
 #pragma unroll
             for (int i = 0; i < NU; ++i)
 #pragma unroll
@@ -1465,6 +1678,35 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                 for (int k = i + 1; k < NU; ++k) v -= Ld[k * NU + i] * k0[k];
                 k0[i] = v;
+            }
+            if constexpr (C::STF) {
+                // a = R0^-1 rh (k0 here); gamma0 = -C^-1 (G'a + rho); k0 = -(a + W gamma0)
+                double sm[C::NSMB];
+                ldb(sm, C::B_WS, C::NSMB);
+                hold(sm, C::NSMB);
+                const double* Wm = sm;
+                const double* Ci = sm + NU * PM;
+                const double* sf = sm + NU * PM + PM * PM;
+                double ga[PMA];
+#pragma unroll
+                for (int i = 0; i < PM; ++i) {
+                    const int f = (int)sf[i];
+                    double v = rhs_s[i];
+#pragma unroll
+                    for (int j = 0; j < NU; ++j) v += (f < 0 ? 0.0 : (((f >> j) & 1) ? -1.0 : 1.0)) * k0[j];
+                    ga[i] = v;
+                }
+#pragma unroll
+                for (int i = 0; i < PM; ++i) {
+                    double v = 0.0;
+#pragma unroll
+                    for (int k = 0; k < PM; ++k) v = fma(-Ci[i * PM + k], ga[k], v);
+                    g0[i] = fixed_u ? 0.0 : v;
+                }
+#pragma unroll
+                for (int j = 0; j < NU; ++j)
+#pragma unroll
+                    for (int i = 0; i < PM; ++i) k0[j] = fma(Wm[j * PM + i], g0[i], k0[j]);
             }
 #pragma unroll
             for (int i = 0; i < NU; ++i) k0[i] = fixed_u ? 0.0 : -k0[i];
@@ -1713,6 +1955,21 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             }
 #pragma unroll
             for (int j = 0; j < NU; ++j) dzo[NX + j] = du[j];
+            if constexpr (C::STF) {
+                // the stiff facets' multiplier steps nu = Gamma xi + Gamma_kappa mu + gamma0 (no D (g'du - rho): the
+                // product of a ~1e12 weight and a cancelling difference)
+                double Gm[PMA * NX], Gk[PMA * NX];
+                ldb(Gm, C::B_GAM, PM * NX);
+                ldb(Gk, C::B_GAK, PM * NX);
+                hold(Gm, PM * NX); hold(Gk, PM * NX);
+#pragma unroll
+                for (int i = 0; i < PM; ++i) {
+                    double v = g0[i];
+#pragma unroll
+                    for (int k = 0; k < NX; ++k) v = fma(Gm[i * NX + k], xi[k], fma(Gk[i * NX + k], mu[k], v));
+                    fnu[i] = v;
+                }
+            }
             if constexpr (NV > 0) {
                 // dnu_t = xi_{t+1} - (A xi_t + Bt du_t + e_t)
                 double Ad[NX * NX], Bt[NX * NU], ev[NX];
@@ -1900,7 +2157,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     // Node Hessian (row scaling D_r = l/s or 1, SOC block Wi2uu) -> packet Q, S, R (xi/u
     // coordinates); group elimination factors -> columns C_GRP.  Also writes e = -rp.
     auto assemble = [&](bool unit, const double* Wi2uu, const double* rp) __attribute__((always_inline)) {
-        double dbox[NX], Hpp[3][3], Huu[NU * NU];
+        double dbox[NX], Hpp[3][3], Huu[NU * NU], Dfc[C::STF ? C::NTR : 1];
 #pragma unroll
         for (int i = 0; i < NX; ++i) dbox[i] = 2.0 * (wfs + wpx);
 #pragma unroll
@@ -1916,10 +2173,14 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         for (int r = 0; r < NR; ++r) {
             const double Dr = row_on(r) ? (unit ? 1.0 : l_(r) / s_(r)) : 0.0;
             if (r < C::R_BOX) {
+                if constexpr (C::STF) {
+                    Dfc[r] = Dr;   // folded below, all but the stiff ones
+                } else {
 #pragma unroll
-                for (int i = 0; i < NU; ++i)
+                    for (int i = 0; i < NU; ++i)
 #pragma unroll
-                    for (int j = 0; j < NU; ++j) Huu[i * NU + j] += (((r >> i) ^ (r >> j)) & 1) ? -Dr : Dr;
+                        for (int j = 0; j < NU; ++j) Huu[i * NU + j] += (((r >> i) ^ (r >> j)) & 1) ? -Dr : Dr;
+                }
             } else if (r < C::R_OBS) {
                 const int idx = bidx[(r - C::R_BOX) >> 1];
 #pragma unroll
@@ -2005,13 +2266,43 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 Sx[i * NU + j] = v;
                 pst(C::gS + i * NU + j, v);
             }
+        double Ru[NU * NU];
+#pragma unroll
+        for (int i = 0; i < NU; ++i)
+#pragma unroll
+            for (int j = i; j < NU; ++j) {
+                double v = Huu[i * NU + j];
+#pragma unroll
+                for (int k = 0; k < NX; ++k) v = fma(Cp[i * NX + k], Sx[k * NU + j], v);
+                Ru[i * NU + j] = v;
+            }
+        if constexpr (C::STF) {
+            // the facets' weights, their folded sum sum_f D_f g_f g_f' (the diagonal is sum_f D_f; off-diagonal (i, j) the
+            // sum of D_f signed by the parity of facet bits i and j) and their max, for factor phase 3
+            double dsum = 0.0, dfm = 0.0, osum[C::NFO > 0 ? C::NFO : 1];
+#pragma unroll
+            for (int e = 0; e < C::NFO; ++e) osum[e] = 0.0;
+#pragma unroll
+            for (int f = 0; f < C::NTR; ++f) {
+                pst(C::gFD + f, Dfc[f]);
+                dsum += Dfc[f];
+                dfm = fmax(dfm, Dfc[f]);
+                int e = 0;
+#pragma unroll
+                for (int i = 0; i < NU; ++i)
+#pragma unroll
+                    for (int j = i + 1; j < NU; ++j, ++e) osum[e] += (((f >> i) ^ (f >> j)) & 1) ? -Dfc[f] : Dfc[f];
+            }
+            pst(C::gFD + C::NTR, dsum);
+#pragma unroll
+            for (int e = 0; e < C::NFO; ++e) pst(C::gFD + C::NTR + 1 + e, osum[e]);
+            pst(C::gFD + C::NTR + 1 + C::NFO, dfm);
+        }
 #pragma unroll
         for (int i = 0; i < NU; ++i)
 #pragma unroll
             for (int j = i; j < NU; ++j) {  // upper triangle: packed by rows (compact), both halves (dense)
-                double v = Huu[i * NU + j];
-#pragma unroll
-                for (int k = 0; k < NX; ++k) v = fma(Cp[i * NX + k], Sx[k * NU + j], v);
+                const double v = Ru[i * NU + j];
                 if constexpr (C::DPK) {
                     pst(C::P_R + i * NU + j, v);
                     if (j > i) pst(C::P_R + j * NU + i, v);
@@ -2218,11 +2509,14 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         set_boundary(z);
         if (!factor()) { status = SCVX_STATUS_NUMERICAL; fail_code = 1.0; }
         __syncthreads();  // factor columns (global) -> lane-parallel solve passes
-        double dz[NZ], dy[NX], da[NGA], dv0[NVA], dnv[NVA];
+        double dz[NZ], dy[NX], da[NGA], dv0[NVA], dnv[NVA], rs0[C::PMA], fn0[C::PMA];
         // virtual control at unit scaling from nu = e = 0: nu's rhs is 0 (the two rows cancel), e's is -w_nu
 #pragma unroll
         for (int i = 0; i < NVA; ++i) dv0[i] = 0.0;
-        solve(q, rr, dv0, dz, dy, dnv);
+        // (unit scaling: every facet folds, D = 1 is never stiff next to Rhat)
+#pragma unroll
+        for (int i = 0; i < C::PMA; ++i) rs0[i] = 0.0;
+        solve(q, rr, dv0, dz, dy, dnv, rs0, fn0);
         recover_aux(dz, da);
         load_state();
 #pragma unroll
@@ -2591,6 +2885,10 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         double sgmu = 0.0;
         double dz[NZ], dy[NX], da[NGA], dsq[NQ], dlq[NQ], cpv[NR];
         double dnv[NVA], dne[NVA], vcpv[2 * NVA];   // virtual control directions, predictor products
+        // stiff facets of this node's stage (C::STF): their indices (-1: empty slot) and multiplier steps
+        double sfr[C::PMA], fnu[C::PMA];
+#pragma unroll
+        for (int i = 0; i < C::PMA; ++i) { sfr[i] = -1.0; fnu[i] = 0.0; }
         auto rco_of = [&](int r, bool corr) __attribute__((always_inline)) -> double {
             const double v = -s_(r) * l_(r);
             return corr ? v - cpv[r] + sgmu : v;
@@ -2616,10 +2914,15 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             issue_soc();
             ldn(r1, C::C_RD, NZ);
             if (corr) ldn(cpv, C::C_CP, NR);
+            if constexpr (C::STF) ldb(sfr, C::B_SF, C::PM);
             hold_state();
             hold_soc();
             hold(r1, NZ);
             if (corr) hold(cpv, NR);
+            if constexpr (C::STF) hold(sfr, C::PM);
+            double rhs_s[C::PMA];
+#pragma unroll
+            for (int i = 0; i < C::PMA; ++i) rhs_s[i] = 0.0;
 #pragma unroll
             for (int i = 0; i < NZ; ++i) r1[i] = act ? -r1[i] : 0.0;
 #pragma unroll
@@ -2633,7 +2936,21 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                     row_eval(r, z, av, gz, h);
                     const double rcr = gz + s_(r) - h;
                     row_accA(r, -l_(r), r1a);  // -rd, group part: -(w_g - sum lambda)
-                    row_accT(r, -(rco_of(r, corr) + l_(r) * rcr) / s_(r), r1, r1a);
+                    double c = -(rco_of(r, corr) + l_(r) * rcr) / s_(r);
+                    if constexpr (C::STF) {
+                        if (r < C::R_BOX) {   // a stiff facet: its rho = -(rco / l + rc) goes to the stage system
+                            const double rho_f = -(rco_of(r, corr) / l_(r) + rcr);
+                            bool st = false;
+#pragma unroll
+                            for (int i = 0; i < C::PM; ++i) {
+                                const bool m_ = sfr[i] == (double)r;
+                                rhs_s[i] = m_ ? rho_f : rhs_s[i];
+                                st |= m_;
+                            }
+                            c = st ? 0.0 : c;
+                        }
+                    }
+                    row_accT(r, c, r1, r1a);
                 }
             }
 #pragma unroll
@@ -2680,7 +2997,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 }
             }
             stamp(2);
-            solve(q, rr, dvl, dz, dy, dnv);
+            solve(q, rr, dvl, dz, dy, dnv, rhs_s, fnu);
             // post-solve: group and SOC directions (state reloaded: nothing crossed the sweeps)
             fresh();
             issue_state();
@@ -2732,6 +3049,12 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             const double rcr = gz + s_(r) - h;
             dsr = -rcr - gd;
             dlr = (rco_of(r, corr) + l_(r) * (rcr + gd)) / s_(r);
+            if constexpr (C::STF) {
+                if (r < C::R_BOX) {   // a stiff facet's multiplier step comes from the stage system
+#pragma unroll
+                    for (int i = 0; i < C::PM; ++i) dlr = sfr[i] == (double)r ? fnu[i] : dlr;
+                }
+            }
         };
         // One pass over the rows for the step length: the ratio test without divisions (the best
         // candidate kept as a fraction bn / bd, bd > 0, compared by cross-multiplication; one division

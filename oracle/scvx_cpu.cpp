@@ -377,9 +377,48 @@ struct Riccati {
     std::vector<Mat> LG, YP, YPi;
     std::vector<Vec> dnu;
     std::vector<Mat> Pe, Pie;   // effective next-stage P~, Pi~ of stage t (= P_{t+1}, Pi_{t+1} without nu)
+    // trust-region facets (the 2^m rows g_f'u <= h_f of ||u - ubar||_1 <= tr at nodes t < K-1), kept out of the
+    // node Hessians: Df[t] their barrier weights lambda/s (empty: the stage has none).  Stage t folds D g g' of
+    // every facet into its input block Rh EXCEPT the stiff ones (D_f > STIFF_RATIO max diag of the rest, when
+    // 1 <= #stiff <= m-1), which stay explicit stage unknowns of the quasi-definite system
+    //   [R0 G; G' -D^-1] [u; nu] = [-y; rho]
+    // solved by the Woodbury identity Rh^-1 = R0^-1 - W C^-1 W', W = R0^-1 G, C = D^-1 + G'W (nu = the facets'
+    // multiplier step).  The folded sum R0 + D g g' with D ~ 1e12 next to an O(1e-4) curvature cannot be
+    // represented in float64 (the C4 late-step optimal_inaccurate); R0, W and C can.
+    std::vector<Vec> Df;
+    std::vector<std::vector<int>> stiff;
+    std::vector<Mat> W, LC, Sh, rhsk;
+    std::vector<Vec> rh;
     Mat M;
     bool ok = true;
 };
+
+// trust-region facet f's coefficient on input j (setup_agent's sign pattern)
+static inline double facet_g(int f, int j) { return ((f >> j) & 1) ? -1.0 : 1.0; }
+constexpr double STIFF_RATIO = 1e6;
+static bool stiff_enabled() {
+    static int e = -1;
+    if (e < 0) { const char* v = std::getenv("SCVX_TWIN_STIFF"); e = v ? std::atoi(v) : 1; }
+    return e != 0;
+}
+// Rh^-1 Y for a stage with stiff facets (Woodbury), or L^-T L^-1 Y
+static Mat stage_solve(const Riccati& R, int t, const Mat& Y) {
+    Mat X = chol_solve_mat(R.L[t], Y);
+    if (R.stiff[t].empty()) return X;
+    const Mat& W = R.W[t];
+    const int p = (int)R.stiff[t].size(), m = W.r;
+    Mat GX(p, X.c);   // G' X0
+    for (int a = 0; a < p; ++a)
+        for (int c = 0; c < X.c; ++c) {
+            double v = 0.0;
+            for (int j = 0; j < m; ++j) v += facet_g(R.stiff[t][a], j) * X(j, c);
+            GX(a, c) = v;
+        }
+    Mat Z = chol_solve_mat(R.LC[t], GX);
+    Mat WZ = mul(W, Z);
+    for (size_t e = 0; e < X.a.size(); ++e) X.a[e] -= WZ.a[e];
+    return X;
+}
 
 // factor the Riccati recursion for node Hessians H_t ((n+m+nnu) square, in (x,u,nu) coordinates)
 //
@@ -406,6 +445,13 @@ static void riccati_factor(const Agent& ag, const std::vector<Mat>& H, Riccati& 
     R.dnu.assign(K, Vec());
     R.Pe.assign(K, Mat());
     R.Pie.assign(K, Mat());
+    R.Df.resize(K);
+    R.stiff.assign(K, std::vector<int>());
+    R.W.assign(K, Mat());
+    R.LC.assign(K, Mat());
+    R.Sh.assign(K, Mat());
+    R.rhsk.assign(K, Mat());
+    R.rh.assign(K, Vec());
     R.M = Mat(n, n);
     R.ok = true;
     for (int t = 0; t < K - 1; ++t) {
@@ -460,6 +506,36 @@ static void riccati_factor(const Agent& ag, const std::vector<Mat>& H, Riccati& 
                 for (int j = 0; j < m; ++j) Rh(i, j) = (i == j) ? 1.0 : 0.0;
                 for (int j = 0; j < n; ++j) Sh(i, j) = 0.0;
             }
+        } else if (!R.Df[t].empty()) {   // trust-region facets: fold all but the stiff ones
+            const Vec& Df = R.Df[t];
+            const int nf = (int)Df.size();
+            double dmax = 0.0;   // the stage's Rhat without the facets
+            for (int j = 0; j < m; ++j) dmax = std::max(dmax, std::fabs(Rh(j, j)));
+            // stiff set (the kernel's rule, qp_ipm.hpp factor phase 3): the facets with D above STIFF_RATIO x the
+            // largest diagonal of the stage's Rhat without them, kept explicit when there are at most m-1 of them and no two are
+            // opposite (a face or an edge of the L1 ball: they leave a complement whose small curvature the fold
+            // would lose).  m or more (a vertex) make every direction of u stiff: the folded sum loses nothing
+            // there, while the Woodbury form would cancel (measured on the C4 dumps: 407 -> 85 optimal of 444).
+            std::vector<int> st;
+            if (stiff_enabled() && ag.T->j_max > 0 && n <= 8 && m >= 2 && m <= 4) {   // the kernel's QPCfg::STF
+                for (int f = 0; f < nf; ++f)
+                    if (Df[f] > STIFF_RATIO * dmax) st.push_back(f);
+                bool opp = false;
+                for (size_t a = 0; a < st.size(); ++a)
+                    for (size_t b = a + 1; b < st.size(); ++b) opp = opp || ((st[a] ^ st[b]) == nf - 1);
+                if ((int)st.size() > m - 1 || opp) st.clear();
+            }
+            if (!st.empty() && std::getenv("SCVX_DEBUG_STIFF")) {
+                std::fprintf(stderr, "   stiff t %d dmax %.3e:", t, dmax);
+                for (int f : st) std::fprintf(stderr, " f%d D %.3e", f, Df[f]);
+                std::fprintf(stderr, "\n");
+            }
+            for (int f = 0; f < nf; ++f) {
+                if (std::find(st.begin(), st.end(), f) != st.end()) continue;
+                for (int i = 0; i < m; ++i)
+                    for (int j = 0; j < m; ++j) Rh(i, j) += Df[f] * facet_g(f, i) * facet_g(f, j);
+            }
+            R.stiff[t] = st;
         }
         Mat L = Rh;
         // LDL' of Rh with the kernel's rule (phase 3): pivots that rounding pushed below 1e-13 max|diag| are
@@ -499,7 +575,19 @@ static void riccati_factor(const Agent& ag, const std::vector<Mat>& H, Riccati& 
             return;
         }
         R.L[t] = L;
-        Mat Kg = chol_solve_mat(L, Sh);
+        R.Sh[t] = Sh;
+        if (!R.stiff[t].empty()) {   // Woodbury pieces: W = R0^-1 G, C = D^-1 + G'W (Cholesky)
+            const int p = (int)R.stiff[t].size();
+            Mat G(m, p);
+            for (int a = 0; a < p; ++a)
+                for (int j = 0; j < m; ++j) G(j, a) = facet_g(R.stiff[t][a], j);
+            R.W[t] = chol_solve_mat(L, G);
+            Mat C = mul(tr(G), R.W[t]);
+            for (int a = 0; a < p; ++a) C(a, a) += 1.0 / R.Df[t][R.stiff[t][a]];
+            if (!chol(C)) { R.ok = false; return; }
+            R.LC[t] = C;
+        }
+        Mat Kg = stage_solve(R, t, Sh);
         for (double& v : Kg.a) v = -v;
         R.Kg[t] = Kg;
         Mat P = add(Qh, mul(tr(Sh), Kg));
@@ -513,7 +601,8 @@ static void riccati_factor(const Agent& ag, const std::vector<Mat>& H, Riccati& 
                     for (int i = 0; i < m; ++i)
                         for (int j = 0; j < n; ++j) rhs(i, j) = ag.C[K - 2](j, i);
                 if (ag.nd[t].fixed_u) rhs = Mat(m, n);
-                Mat kap = chol_solve_mat(L, rhs);
+                R.rhsk[t] = rhs;
+                Mat kap = stage_solve(R, t, rhs);
                 for (double& v : kap.a) v = -v;
                 R.kap[t] = kap;
                 Mat I(n, n);
@@ -524,7 +613,8 @@ static void riccati_factor(const Agent& ag, const std::vector<Mat>& H, Riccati& 
                 const Mat& Pin = R.Pie[t];
                 Mat rhs = mul(tr(R.Bt[t]), Pin);
                 if (ag.nd[t].fixed_u) rhs = Mat(m, n);
-                Mat kap = chol_solve_mat(L, rhs);
+                R.rhsk[t] = rhs;
+                Mat kap = stage_solve(R, t, rhs);
                 for (double& v : kap.a) v = -v;
                 R.kap[t] = kap;
                 R.Pi[t] = add(mul(tr(ag.A[t]), Pin), mul(tr(Sh), kap));
@@ -535,9 +625,12 @@ static void riccati_factor(const Agent& ag, const std::vector<Mat>& H, Riccati& 
 }
 
 // Solve  min 1/2 dz'H dz - r1'dz  s.t. A dz = r2  ; returns dz (per node n+m+nnu), dy (K-1)*n, dyi, dyf
+// Facets kept out of r1 (stages with R.Df[t] set): ftr[t][f] = their folded rhs term (rco + lam rc)/s, frho[t][f] =
+// -(rco/lam + rc); fnu[t][f] returns the stiff facets' multiplier steps.
 static bool riccati_solve(const Agent& ag, const std::vector<Mat>& H, Riccati& R, const std::vector<Vec>& r1,
                           const Vec& xi0, const std::vector<Vec>& e, const Vec& r2fin, std::vector<Vec>& dz,
-                          Vec& dy, Vec& dyi, Vec& dyf) {
+                          Vec& dy, Vec& dyi, Vec& dyf, const std::vector<Vec>* ftr = nullptr,
+                          const std::vector<Vec>* frho = nullptr, std::vector<Vec>* fnu = nullptr) {
     (void)H;
     int n = ag.n, m = ag.m, K = ag.K;
     const bool fin = ag.T->has_final;
@@ -569,12 +662,32 @@ static bool riccati_solve(const Agent& ag, const std::vector<Mat>& H, Riccati& R
         }
         if (ag.nd[t].fixed_u)
             for (int j = 0; j < m; ++j) rh[j] = 0.0;
-        Vec k = rh;
-        chol_solve(R.L[t], k.data());
-        for (double& v : k) v = -v;
+        const std::vector<int>& st = R.stiff[t];
+        if (ftr && !R.Df[t].empty() && !ag.nd[t].fixed_u)
+            for (int f = 0; f < (int)R.Df[t].size(); ++f)
+                if (std::find(st.begin(), st.end(), f) == st.end())
+                    for (int j = 0; j < m; ++j) rh[j] += facet_g(f, j) * (*ftr)[t][f];
+        R.rh[t] = rh;
+        Mat rhm(m, 1);
+        for (int j = 0; j < m; ++j) rhm(j, 0) = rh[j];
+        Mat km = stage_solve(R, t, rhm);
+        Vec k(m);
+        for (int j = 0; j < m; ++j) k[j] = -km(j, 0);
+        Vec wc;   // W C^-1 rho
+        if (!st.empty()) {
+            Vec z((int)st.size());
+            for (size_t a = 0; a < st.size(); ++a) z[a] = (*frho)[t][st[a]];
+            chol_solve(R.LC[t], z.data());
+            wc = matvec(R.W[t], z);
+            for (int j = 0; j < m; ++j) k[j] += wc[j];
+        }
         R.k0[t] = k;
         Vec p = qh, kt = matTvec(R.Kg[t], rh);
         for (int i = 0; i < n; ++i) p[i] += kt[i];
+        if (!st.empty()) {
+            Vec c = matTvec(R.Sh[t], wc);
+            for (int i = 0; i < n; ++i) p[i] += c[i];
+        }
         R.p0[t] = p;
         if (fin) {
             if (t == K - 1) {
@@ -629,6 +742,25 @@ static bool riccati_solve(const Agent& ag, const std::vector<Mat>& H, Riccati& R
         }
         for (int i = 0; i < n; ++i) dz[t][i] = x[i];
         for (int j = 0; j < m; ++j) dz[t][n + j] = v[j];
+        if (fnu && !R.stiff[t].empty()) {   // nu = C^-1 (G'x0 - rho), x0 = -R0^-1 (rh + Sh xi + rhsk mu)
+            const std::vector<int>& st = R.stiff[t];
+            Vec y = R.rh[t], sx = matvec(R.Sh[t], xi);
+            for (int j = 0; j < m; ++j) y[j] += sx[j];
+            if (fin) {
+                Vec g = matvec(R.rhsk[t], mu);
+                for (int j = 0; j < m; ++j) y[j] += g[j];
+            }
+            chol_solve(R.L[t], y.data());
+            Vec z(st.size());
+            for (size_t a = 0; a < st.size(); ++a) {
+                double gx = 0.0;
+                for (int j = 0; j < m; ++j) gx -= facet_g(st[a], j) * y[j];
+                z[a] = gx - (*frho)[t][st[a]];
+            }
+            chol_solve(R.LC[t], z.data());
+            (*fnu)[t].assign(R.Df[t].size(), 0.0);
+            for (size_t a = 0; a < st.size(); ++a) (*fnu)[t][st[a]] = z[a];
+        }
         if (t < K - 1) {
             Vec a = matvec(ag.A[t], xi), b = matvec(R.Bt[t], v);
             Vec xn(n);
@@ -1042,7 +1174,16 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out, const double*
                     for (int j = 0; j < m; ++j) Hf(n + i, n + j) += l.soc.Wi2(1 + i, 1 + j);
             }
             int nz = n + m + N.nnu, na = N.na;
-            l.Hxu = node_zz(N, l.D, nz);
+            R.Df.resize(K);
+            R.Df[t].clear();
+            if (t < K - 1 && !N.fixed_u && N.nr >= (1 << m) && T->j_max > 0 && n <= 8 && m >= 2 && m <= 4) {   // STF: facets folded per stage
+                Vec D0 = l.D;
+                R.Df[t].assign(l.D.begin(), l.D.begin() + (1 << m));
+                for (int f = 0; f < (1 << m); ++f) D0[f] = 0.0;
+                l.Hxu = node_zz(N, D0, nz);
+            } else {
+                l.Hxu = node_zz(N, l.D, nz);
+            }
             if (N.soc)
                 for (int i = 0; i < m; ++i)
                     for (int j = 0; j < m; ++j) l.Hxu(n + i, n + j) += l.soc.Wi2(1 + i, 1 + j);
@@ -1065,14 +1206,22 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out, const double*
             auto newton = [&](const std::vector<Vec>& rco, const std::vector<Vec>& rcq, std::vector<Vec>& dz,
                               std::vector<Vec>& ds, std::vector<Vec>& dl, std::vector<Vec>& dsq,
                               std::vector<Vec>& dlq, Vec& dy, Vec& dyi, Vec& dyf) -> bool {
-                std::vector<Vec> r1(K), r1a(K), tq(K);
+                std::vector<Vec> r1(K), r1a(K), tq(K), ftr(K), frho(K), fnu(K);
                 for (int t = 0; t < K; ++t) {
                     Node& N = ag.nd[t];
                     NodeLin& l = L[t];
                     Vec rf(N.nv);
                     for (int j = 0; j < N.nv; ++j) rf[j] = -l.rd[j];
+                    const int nf = (int)R.Df[t].size();   // facets handled per stage (riccati_solve)
+                    ftr[t].assign(nf, 0.0);
+                    frho[t].assign(nf, 0.0);
                     for (int r = 0; r < N.nr; ++r) {
                         double tr_ = (rco[t][r] + N.lam[r] * l.rc[r]) / N.s[r];
+                        if (r < nf) {
+                            ftr[t][r] = tr_;
+                            frho[t][r] = -(rco[t][r] / N.lam[r] + l.rc[r]);
+                            continue;
+                        }
                         for (int j = 0; j < N.nv; ++j) rf[j] -= N.G(r, j) * tr_;
                     }
                     if (N.soc) {
@@ -1103,7 +1252,7 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out, const double*
                 Vec r2f(n);
                 for (int i = 0; i < n; ++i) r2f[i] = -rpf[i];
                 std::vector<Vec> dzx;
-                if (!riccati_solve(ag, H, R, r1, xi0, e, r2f, dzx, dy, dyi, dyf)) return false;
+                if (!riccati_solve(ag, H, R, r1, xi0, e, r2f, dzx, dy, dyi, dyf, &ftr, &frho, &fnu)) return false;
                 if (std::getenv("SCVX_DEBUG")) {
                     double e1 = 0.0, e2 = 0.0;
                     for (int t = 0; t < K; ++t) {
@@ -1160,6 +1309,9 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out, const double*
                         for (int j = 0; j < N.nv; ++j) g += N.G(r, j) * dz[t][j];
                         ds[t][r] = -l.rc[r] - g;
                         dl[t][r] = (rco[t][r] + N.lam[r] * (l.rc[r] + g)) / N.s[r];
+                        if (!fnu[t].empty() && r < (int)fnu[t].size() &&
+                            std::find(R.stiff[t].begin(), R.stiff[t].end(), r) != R.stiff[t].end())
+                            dl[t][r] = fnu[t][r];   // stiff facet: its multiplier step from the stage system
                     }
                     if (N.soc) {
                         Vec gq(m + 1, 0.0);
@@ -1242,6 +1394,18 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out, const double*
             static const double tau_end = std::getenv("SCVX_TAU_END") ? std::atof(std::getenv("SCVX_TAU_END")) : 0.99999;
             const double eta = (aa >= 0.99) ? tau_end : 0.99;
             double al = std::min(1.0, eta * max_step(ds, dl, dsq, dlq));
+            {   // the kernel's NaN / Inf probe of the direction (fail code 4): keep the current iterate
+                double pr = 0.0;
+                for (int t = 0; t < K; ++t) {
+                    for (double v : dz[t]) pr += 0.0 * v;
+                    for (double v : ds[t]) pr += 0.0 * v;
+                    for (double v : dl[t]) pr += 0.0 * v;
+                    for (double v : dsq[t]) pr += 0.0 * v;
+                    for (double v : dlq[t]) pr += 0.0 * v;
+                }
+                for (double v : dy) pr += 0.0 * v;
+                if (!(pr + al == pr + al) || !(al > 0.0)) { status = fail_status; break; }
+            }
             if (near && al < 1e-2) { status = SCVX_STATUS_MAX_ITER; break; }  // stall at reduced accuracy (kernel)
             if (std::getenv("SCVX_DEBUG")) {
                 std::fprintf(stderr, "   alpha_aff %.3e sigma %.3e alpha %.3e\n", aa, sig, al);

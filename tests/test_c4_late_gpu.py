@@ -6,10 +6,12 @@ Why status 1 there: an active trust-region facet of ||w_
 D = lambda / s ~ 1e12 to the node's input Hessian, whose sum with the O(1e-4) objective curvature cannot be
 represented in float64; the normal-equation Riccati then clamps a pivot (kernel and CPU twin alike) and the dual
 residual stalls near 1e-8.  The same subproblems solved cold end the same way, so it is not the warm start.
+Round 5 keeps such facets out of the normal equations (explicit stage unknowns, Woodbury form: QPCfg::STF in
+qp_ipm.hpp, Riccati::stiff in oracle/scvx_cpu.cpp): 444 -> 25-62 status-1 solves at the worst step.
 
 Checked at step 18 (tr = 2^-4 x 0.25) of the loop, on the step's own inputs (discretisation, culled rows):
-  * no solve fails (status 2) and >= 85 % end at the full tolerance (status 0) at every step (measured: 89 % at
-    the worst step, >= 98 % before the trust region shrinks below 1/32);
+  * no solve fails (status 2) and >= 98 % end at the full tolerance (status 0) at every step (measured round 5:
+    98.5 % at the worst step, >= 99.4 % at every other; round 4, before the stiff-facet stage system: 89 %);
   * status-1 solves against the dense reference-form oracle (oracle/qp_dense.py, dist_scvx_3d.py:51-111 as
     written): optimal value within 1e-7 relative, violation < 1e-5 (Clarabel's reduced feasibility, as
     tests/test_coupled_gpu.py); status-0 solves: value 1e-7, violation 1e-7;
@@ -50,9 +52,11 @@ def test_c4_late_steps_match_dense_oracle(cuda):
             break
         X, U = Xn, Un
     print("status-0 fraction per step:", [round(f, 4) for f in fr0])
-    # measured (round 4): >= 98 % at steps 0-14, 96 / 99 / 89 / 97 % at steps 15-18 -- short of the 99 % goal
-    # (the normal-equation Riccati's float64 limit); every status-1 solve is checked below
-    assert min(fr0) >= 0.85, fr0
+    # measured: round 4 >= 98 % at steps 0-14, 96 / 99 / 89 / 97 % at steps 15-18; round 5, with the stiff
+    # trust-region facets kept out of the normal equations (QPCfg::STF), >= 99.4 % at every step but step 17
+    # (98.4-98.5 %; pytest_r5e/r5f) -- the remaining status-1 solves lose accuracy in the state-side Riccati
+    # (P = Qh - Sh' Rh^-1 Sh of collision-stiff nodes); every status-1 solve is checked below
+    assert min(fr0) >= 0.98, fr0
     # the last step's subproblems: its inputs are still in the driver
     trn = trp.cpu().numpy()
     assert trn[0] <= 0.25 / 16      # the radius has halved four times by step 18 (profiles/round4_r4a_c4_drift.log)
@@ -72,7 +76,9 @@ def test_c4_late_steps_match_dense_oracle(cuda):
     np.testing.assert_allclose(ow[both], oc[both], rtol=2e-5, atol=2e-8)
     assert np.mean(np.abs(ow[both] - oc[both]) <= 2e-8 * np.maximum(1.0, np.abs(oc[both]))) >= 0.99
     np.testing.assert_allclose(ow[~both], oc[~both], rtol=5e-5, atol=1e-8)
-    print("warm vs cold: both optimal", int(both.sum()), "max rel diff where either is status 1",
+    print("warm vs cold: both optimal", int(both.sum()), "max rel diff there",
+          float(np.max(np.abs(ow[both] - oc[both]) / np.maximum(1.0, np.abs(oc[both])), initial=0.0)),
+          "max rel diff where either is status 1",
           float(np.max(np.abs(ow[~both] - oc[~both]) / np.maximum(1.0, np.abs(oc[~both])), initial=0.0)))
     dn, Xh, Uh = drv.disc.cpu().numpy(), X.cpu().numpy(), U.cpu().numpy()
     sig, xf = drv.sigma.cpu().numpy(), drv.x_final.cpu().numpy()

@@ -4,7 +4,8 @@ iterations, warm-started count; for the steps with the most status-1 solves, the
 status-1 agents replayed from a snapshot of the solver workspace (the exact warm-started solve), their
 cold re-solve on the GPU, and an npz dump of the subproblems (gpurun_out/c4_drift_*.npz) for the
 dense oracle / CPU twin on the host.
-usage: python tools/c4_drift.py [steps] [dump_steps, comma separated]"""
+usage: [DUMP_ALL=1] python tools/c4_drift.py [steps] [dump_steps, comma separated] [n_dump]
+(DUMP_ALL=1: every status-1 subproblem of a dump step + 64 status-0 ones -> gpurun_out/c4_late_step*.npz)"""
 import ctypes
 import os
 import sys
@@ -17,6 +18,7 @@ sys.path.insert(0, REPO)
 
 
 def main(steps=25, dump_steps="12,18", n_dump=4, cap=64):
+    n_dump = int(n_dump)
     import torch
     import bench
     import scvx_hip
@@ -54,7 +56,18 @@ def main(steps=25, dump_steps="12,18", n_dump=4, cap=64):
               f"mean(st1) {it[s1].mean() if s1.size else 0:.1f} warm(st1) "
               f"{int(warm_in[s1].sum().item()) if (warm_in is not None and s1.size) else 0} check {drv.last_check}",
               flush=True)
-        if k in dump_steps and s1.size:
+        if k in dump_steps and s1.size and int(os.environ.get("DUMP_ALL", "0")):
+            # every status-1 subproblem of the step (<= 600) + 64 status-0 ones, for the CPU twin on the host
+            s0 = np.nonzero(st == 0)[0]
+            allp = np.concatenate([s1[:600], s0[:: max(1, s0.size // 64)][:64]])
+            os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+            np.savez_compressed(os.path.join(REPO, "gpurun_out", f"c4_late_step{k}.npz"), agents=allp, status=st[allp],
+                                iters=it[allp], disc=drv.disc[allp].cpu().numpy(), sigma=drv.sigma[allp].cpu().numpy(),
+                                X=X[allp].cpu().numpy(), U=U[allp].cpu().numpy(),
+                                x_init=drv.x_init[allp].cpu().numpy(), x_final=drv.x_final[allp].cpu().numpy(),
+                                tr=trp[allp].cpu().numpy(), rows=drv.rows[allp].cpu().numpy(),
+                                count=drv.count[allp].cpu().numpy(), obj=drv.solver.obj[allp].cpu().numpy())
+        if k in dump_steps and s1.size and n_dump > 0:
             pick = s1[:: max(1, s1.size // n_dump)][:n_dump]
             rows, count = drv.rows.clone(), drv.count.clone()
             # cold re-solve of the same subproblems
