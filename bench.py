@@ -162,12 +162,13 @@ def host_info():
     return info
 
 
-def cpu_jacobi(sc, n_sample, threads, warmup, steps, tol=1e-8, max_seconds=30.0, warm_status=1):
+def cpu_jacobi(sc, n_sample, threads, warmup, steps, tol=1e-8, max_seconds=30.0, warm_status=1, tr_rule="per_agent"):
     """The CPU restatement of the timed region, like for like: the same warm-started Jacobi loop as the GPU
     line (JacobiSCvx with the bench's settings) on the first n_sample agents -- per step the FOH
     (oracle/foh_ref.c), the QP twin (oracle/scvx_cpu.cpp, the kernel's algorithm, started from the previous
     step's primal-dual point exactly as the kernel's warm rule: warm = last status <= warm_status) and the per-agent
-    trust-region bookkeeping of csrc/jacobi.hip (tie margin 1e-9).  `warmup` untimed steps, then up to `steps`
+    trust-region bookkeeping of csrc/jacobi.hip (tie margin 1e-9; tr_rule "global": the reference's one radius, halved
+    when the summed cost rises, JacobiSCvx's global rule).  `warmup` untimed steps, then up to `steps`
     timed steps (fewer if max_seconds runs out first).  Returns (SCvx iterations/s scaled to the N=1024-agent
     workload, timed steps, seconds, mean IPM iterations per agent over the timed steps)."""
     from oracle import foh_oracle, qp_cpu
@@ -177,6 +178,7 @@ def cpu_jacobi(sc, n_sample, threads, warmup, steps, tol=1e-8, max_seconds=30.0,
     sig, xi, xf = sc["sigma"][:n], sc["x_init"][:n], sc["x_final"][:n]
     tr = np.full(n, TR0)
     prev = np.full(n, np.inf)
+    prev_total = np.inf
     wstate = np.zeros((n, qp_cpu.warm_doubles(tpl)))
     warm = None
     disc = np.zeros((n, K - 1, 6 * (6 + 6 + 2)))
@@ -190,7 +192,11 @@ def cpu_jacobi(sc, n_sample, threads, warmup, steps, tol=1e-8, max_seconds=30.0,
         X = np.where(ok[:, None, None], o["X"], X)
         U = np.where(ok[:, None, None], o["U"], U)
         cost = (U[:, :-1] ** 2).sum(axis=(1, 2))
-        tr = np.where(cost > prev * (1.0 + 1e-9), 0.5 * tr, tr)
+        if tr_rule == "global":
+            tr = tr * (0.5 if cost.sum() > prev_total else 1.0)
+            prev_total = cost.sum()
+        else:
+            tr = np.where(cost > prev * (1.0 + 1e-9), 0.5 * tr, tr)
         tr = np.where(ok, tr, 0.5 * tr)
         prev = cost
         warm = (o["status"] <= warm_status).astype(np.int32)
@@ -203,16 +209,17 @@ def cpu_jacobi(sc, n_sample, threads, warmup, steps, tol=1e-8, max_seconds=30.0,
     return timed * (n / N_AGENTS) / t_el, timed, t_el, it_sum / (timed * n)
 
 
-def cpu_baselines(sc, n_sample, tol, warmup, steps, warm_status=1):
+def cpu_baselines(sc, n_sample, tol, warmup, steps, warm_status=1, tr_rule="per_agent"):
     """All-core and single-core CPU figures of the restatement on the GPU line's own loop (cpu_jacobi).  "All
     cores" is every CPU this process may run on: nproc, capped by the cgroup CPU quota when one is set (the GPU
     box grants 16 CPUs of a 256-thread host; more OpenMP threads than that only time-slice)."""
     info = host_info()
     quota = info.get("cgroup_cpu_quota")
     threads = max(1, min(info["nproc"], int(quota))) if quota else info["nproc"]
-    v_all, steps_all, el, it_all = cpu_jacobi(sc, n_sample, threads, warmup, steps, tol=tol, warm_status=warm_status)
+    v_all, steps_all, el, it_all = cpu_jacobi(sc, n_sample, threads, warmup, steps, tol=tol, warm_status=warm_status,
+                                              tr_rule=tr_rule)
     n1 = min(n_sample, 64)
-    v_one, steps1, el1, it1 = cpu_jacobi(sc, n1, 1, warmup, steps, tol=tol, warm_status=warm_status)
+    v_one, steps1, el1, it1 = cpu_jacobi(sc, n1, 1, warmup, steps, tol=tol, warm_status=warm_status, tr_rule=tr_rule)
     return dict(value=v_all, unit="SCvx-iterations/s (N=1024-agent equivalent)", cores=threads, kind="port",
                 sample=f"warm-started steady state, steps {warmup + 1}-{warmup + steps_all} of the GPU line's Jacobi "
                        f"loop ({warmup} untimed warm-up steps first) on {n_sample} of the {N_AGENTS} agents: FOH C + "
@@ -473,14 +480,54 @@ def stage_times(marks_per_step):
     return {k: float(np.median(v)) for k, v in stages.items()}, steps
 
 
+def dry_run_shards(args, world, rank):
+    """The coupled configs' shard arithmetic on CPU: every rank builds the full problem (make_coupled, host data
+    only), keeps its block -- contiguous, or with --balance the block of scvx_hip.scvx.balanced_order over a
+    deterministic stand-in for the first step's IPM iterations -- and the ranks all_gather their agent indices and a
+    checksum of their initial states, so rank 0 can check that the shards tile the agents exactly once and that every
+    rank holds the data of its own agents."""
+    import torch
+    import torch.distributed as dist
+    from scvx_hip.scvx import balanced_order
+    sc, w, cfg = make_coupled(args.config, world, rank, torch.device("cpu"))
+    N_total, n_loc = cfg["N_total"], cfg["n_loc"]
+    idx = np.arange(rank * n_loc, (rank + 1) * n_loc)
+    if args.balance and world > 1:
+        iters = 3 + (np.arange(N_total) * 2654435761 % 97) % 29     # stand-in iteration counts, 3..31
+        order = balanced_order(iters, world)
+        idx = order[rank * n_loc:(rank + 1) * n_loc]
+        w = shard_tensors(sc, idx, torch.device("cpu"))
+    mine = torch.tensor(idx, dtype=torch.int64)
+    chk = torch.tensor([float(w["X"].sum()), float(w["x_final"].sum())], dtype=torch.float64)
+    if world > 1:
+        allidx = [torch.empty_like(mine) for _ in range(world)]
+        allchk = [torch.empty_like(chk) for _ in range(world)]
+        dist.all_gather(allidx, mine)
+        dist.all_gather(allchk, chk)
+    else:
+        allidx, allchk = [mine], [chk]
+    ok = True
+    if rank == 0:
+        cat = torch.cat(allidx).numpy()
+        ok = bool(np.array_equal(np.sort(cat), np.arange(N_total)))
+        for r in range(world):
+            ir = allidx[r].numpy()
+            ok = ok and bool(np.isclose(allchk[r][0].item(), sc["X"][ir].sum(), rtol=1e-12, atol=1e-9))
+            ok = ok and bool(np.isclose(allchk[r][1].item(), sc["x_final"][ir].sum(), rtol=1e-12, atol=1e-9))
+    return dict(N_total=N_total, agents_per_rank=n_loc, balanced=bool(args.balance and world > 1),
+                shard_first_agents=[int(a[0]) for a in allidx], shards_tile_agents=ok)
+
+
 def dry_run(args, world, rank):
     """--dry-run: the launcher / rendezvous / barrier / max-over-ranks timing path on CPU (gloo), with
-    no GPU work -- used by tests/test_bench_cpu.py to check that --gpus N really runs N ranks."""
+    no GPU work -- used by tests/test_bench_cpu.py to check that --gpus N really runs N ranks; for c4 / c5
+    also the shard arithmetic of the coupled configs (dry_run_shards)."""
     import torch
     import torch.distributed as dist
     if world > 1:
         dist.init_process_group("gloo")
         dist.barrier()
+    shards = dry_run_shards(args, world, rank) if args.config in ("c4", "c5") else None
     t0 = time.perf_counter()
     for _ in range(args.steps):
         time.sleep(0.001)
@@ -489,8 +536,11 @@ def dry_run(args, world, rank):
         dist.barrier()
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     if rank == 0:
-        print(json.dumps({"metric": "dry-run", "value": None, "n_gpus": world, "steps": args.steps,
-                          "ms_per_step": 1e3 * el_t.item() / args.steps, "dry_run": True}), flush=True)
+        line = {"metric": "dry-run", "value": None, "n_gpus": world, "steps": args.steps,
+                "ms_per_step": 1e3 * el_t.item() / args.steps, "dry_run": True, "config": {"workload": args.config}}
+        if shards is not None:
+            line["config"].update(shards)
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -511,6 +561,10 @@ def main():
                          "1e-8), the solver of the reference's dist_scvx_3d.py:110")
     ap.add_argument("--dry-run", action="store_true", help="launcher/rendezvous check on CPU, no GPU work")
     ap.add_argument("--tensor-update", action="store_true", help="c3: bookkeeping as tensor ops (not csrc/jacobi.hip)")
+    ap.add_argument("--tr-rule", default="per_agent", choices=("per_agent", "global"),
+                    help="c3 trust-region rule: per_agent (each agent's radius halves on its own cost increase, the "
+                         "headline) or global (the reference's one radius, halved when the summed cost rises: "
+                         "Distributed_opt/dist_scvx_3d.py:248-252)")
     ap.add_argument("--tie-rtol", type=float, default=1e-9,
                     help="c3 per-agent trust-region rule: relative margin of the cost-increase test (JacobiSCvx.tie_rtol)")
     ap.add_argument("--dispatch-order", default="lpt", choices=("lpt", "none"),
@@ -554,7 +608,7 @@ def main():
         model, box, j_max, n, m = "di", BOX, 0, 6, 3
         spec = scvx_hip.QPSpec(model="di", K=K, box=BOX, obs=sc["obs"], w_obs=1e6, u_max=U_MAX, tol=args.tol,
                                max_iter=60)
-        drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, tr_rule="per_agent", tie_rtol=args.tie_rtol,
+        drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, tr_rule=args.tr_rule, tie_rtol=args.tie_rtol,
                          fused_update=not args.tensor_update, warm_max_status=args.warm_status, dispatch_order=args.dispatch_order)
         n_obs = N_OBS
     else:
@@ -652,7 +706,7 @@ def main():
         cpu = None
         if not args.no_cpu and args.config == "c3":
             cpu = cpu_baselines(sc, min(args.cpu_sample, N), tol=args.tol, warmup=args.warmup, steps=args.steps,
-                                warm_status=args.warm_status)
+                                warm_status=args.warm_status, tr_rule=args.tr_rule)
         if args.config == "c3":
             value, scaling = world * args.steps / el, "weak"
             metric = "SCvx-iterations/sec, N agents x K=50 nodes (N=1024 per GPU)"
@@ -689,7 +743,11 @@ def main():
                        "parallelism": f"agents sharded x{world}" + (" (balanced order)" if (args.balance and world > 1
                                                                          and args.config != "c3") else ""),
                        "qp_dispatch": "longest-first (last-step IPM iterations)" if getattr(drv, "_lpt", False)
-                       else "agent order"},
+                       else "agent order",
+                       "tr_rule": drv.tr_rule,
+                       # JacobiSCvx's default is 0 (warm-start only optimal solves); the bench warm-starts
+                       # optimal_inaccurate ones too (C3 / C5 end every solve optimal: no effect there)
+                       "warm_max_status": args.warm_status},
             "roofline": {"bound": "fp64_valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                          "traffic_unit": "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE; warm-started launches as in the "

@@ -71,11 +71,10 @@ int qp_check(const scvx_qp_template* T, int N, QPClass& c) {
     c = QPClass{};
     c.nx = T->n_x; c.nu = T->n_u;
     if (T->model_id == SCVX_MODEL_RUNTIME) {
-        // the kernel's limits: the 3 x 3 position block (n_x >= 3), the solve chains' 16-lane broadcast and the
-        // virtual control's Gauss-Jordan over 4 n_x lanes (n_x <= 16), 2^n_u trust-region facets (n_u <= 4)
-        if (T->n_x < 3 || T->n_x > 16 || T->n_u < 1 || T->n_u > 4)
-            return set_error(SCVX_EUNSUPPORTED, "qp: runtime model needs 3 <= n_x <= 16 and 1 <= n_u <= 4");
-        if (T->j_max > 32) return set_error(SCVX_EUNSUPPORTED, "qp: j_max <= 32");
+        // the kernel's limits (subproblem_rtc.hpp, shared with scvx_rtc_subproblem_compile)
+        if (const char* bad = rtc_qp_class_error(T->n_x, T->n_u, T->n_box, T->n_obs, T->j_max, T->w_nu > 0.0 ? 1 : 0,
+                                                 T->K))
+            return set_error(SCVX_EUNSUPPORTED, bad);
         c.rt = true;
         c.nb = T->n_box; c.no = T->n_obs; c.nc = T->j_max; c.vc = T->w_nu > 0.0 ? 1 : 0;
         return SCVX_OK;

@@ -121,8 +121,7 @@ static int scp_launch(const scvx_scp_template* T, int N, const double* disc, con
     } else if (T->model_id == SCVX_MODEL_RUNTIME) {
         // any other model (its FOH from scvx_rtc_model_create): the kernel instantiated for (n_x, n_u) at the
         // first solve; the node vector z = [xi | g | game states | u | nu] stays within the kernel's 16
-        if (T->n_x < 1 || T->n_x > 8 || T->n_u < 1 || 2 * T->n_x + SCP_NG + ne + T->n_u > 16)
-            return set_error(SCVX_EUNSUPPORTED, "scp: runtime model needs 2 n_x + n_u + 4 (+ game states) <= 16");
+        if (const char* bad = rtc_scp_class_error(T->n_x, T->n_u, ne)) return set_error(SCVX_EUNSUPPORTED, bad);
         if (T->has_soc && T->n_u > 3) return set_error(SCVX_EUNSUPPORTED, "scp: SOC rows need n_u + 1 <= 4");
         return rtc_scp_launch(a, ne, two ? 2 : 1, st);
     } else {

@@ -133,6 +133,7 @@ int compile_inst(const Inst& i, Instance** out) {
 }
 
 int launch(const Inst& i, void** args, unsigned grid, unsigned block, size_t lds, hipStream_t st) {
+    if (lds > 65536) return scvx::set_error(SCVX_EUNSUPPORTED, "subproblem rtc: class needs more than 64 KiB of LDS");
     hipFunction_t f = nullptr;
     {
         std::lock_guard<std::mutex> g(g_mu);
@@ -140,7 +141,6 @@ int launch(const Inst& i, void** args, unsigned grid, unsigned block, size_t lds
         if (int rc = compile_inst(i, &in)) return rc;
         if (int rc = function_of(in, &f)) return rc;
     }
-    if (lds > 65536) return scvx::set_error(SCVX_EUNSUPPORTED, "subproblem rtc: class needs more than 64 KiB of LDS");
     hipError_t e = hipModuleLaunchKernel(f, grid, 1, 1, block, 1, 1, (unsigned)lds, st, args, nullptr);
     if (e != hipSuccess) {
         std::string msg = std::string("subproblem rtc launch: ") + hipGetErrorString(e);
@@ -176,8 +176,10 @@ extern "C" int scvx_rtc_subproblem_compile(int kind, const int* cls, int ncls, s
         return scvx::set_error(SCVX_EINVAL, "scvx_rtc_subproblem_compile: kind 0 takes 6 class ints, kind 1 takes 4");
     for (int i = 0; i < ncls; ++i)
         if (cls[i] < 0 || cls[i] > 64) return scvx::set_error(SCVX_EINVAL, "scvx_rtc_subproblem_compile: class out of range");
-    if (cls[0] < 1 || cls[0] > 16 || cls[1] < 1 || cls[1] > 8)
-        return scvx::set_error(SCVX_EUNSUPPORTED, "scvx_rtc_subproblem_compile: n_x in 1..16, n_u in 1..8");
+    // the solve entry points' own limits (subproblem_rtc.hpp), checked before a ~10 s compile
+    const char* bad = kind == 0 ? scvx::rtc_qp_class_error(cls[0], cls[1], cls[2], cls[3], cls[4], cls[5], 2)
+                                : scvx::rtc_scp_class_error(cls[0], cls[1], cls[2]);
+    if (bad) return scvx::set_error(SCVX_EUNSUPPORTED, bad);
     const Inst i = kind == 0 ? qp_inst(cls[0], cls[1], cls[2], cls[3], cls[4], cls[5])
                              : scp_inst(cls[0], cls[1], cls[2], cls[3]);
     std::lock_guard<std::mutex> g(g_mu);

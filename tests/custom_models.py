@@ -7,6 +7,8 @@ FirstOrderHold (tests/golden/make_rtc_foh_goldens.py).
   KinematicCar     x = [px, py, theta, v], u = [a, delta]:  f = [v cos th, v sin th, v tan(delta)/L, a]
   DampedDI2D       x = [p (2), v (2)], u = a (2):           f = [v, a - c v]
   CartPole         x = [s, phi, ds, dphi], u = [F]:         the frictionless cart-pole (rational in cos)
+  UnicycleAccel    x = [px, py, th, v, w], u = [a, alpha]:  f = [v cos th, v sin th, w, a, alpha] (odd n_x = 5)
+  TripleInt3D      x = [p (3), v (3), a (3)], u = jerk (3): f = [v, a - c v, u]  (n_x = 9: the kernel's n > 8 path)
 """
 import sympy as sp
 
@@ -61,6 +63,23 @@ class CartPole(_SympyModel):
         dds = (u[0] + mp * s * (l * x[3] ** 2 + g * c)) / den
         ddphi = (-u[0] * c - mp * l * x[3] ** 2 * c * s - (mc + mp) * g * s) / (l * den)
         return [x[2], x[3], dds, ddphi]
+
+
+class UnicycleAccel(_SympyModel):
+    x_names, u_names = "px py th v w", "a alpha"
+
+    @staticmethod
+    def dynamics(x, u):
+        return [x[3] * sp.cos(x[2]), x[3] * sp.sin(x[2]), x[4], u[0], u[1]]
+
+
+class TripleInt3D(_SympyModel):
+    x_names, u_names = "px py pz vx vy vz ax ay az", "jx jy jz"
+    params = {"c": 0.2}
+
+    @staticmethod
+    def dynamics(x, u, c):
+        return [x[3], x[4], x[5], x[6] - c * x[3], x[7] - c * x[4], x[8] - c * x[5], u[0], u[1], u[2]]
 
 
 MODELS = {"car": KinematicCar, "damped_di": DampedDI2D, "cartpole": CartPole}

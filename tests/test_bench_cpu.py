@@ -30,6 +30,19 @@ def test_single_rank_default():
     assert line["n_gpus"] == 1
 
 
+def test_dry_run_c4_shards_at_8_ranks():
+    """bench.py --dry-run --gpus 8 --config c4: the 4096-agent lattice over 8 gloo ranks (the driver's 8-GPU run),
+    contiguous and --balance shards: 512 agents per rank, the shards tile the agents exactly once and every rank
+    holds its own agents' data (bench.dry_run_shards)."""
+    for extra in ((), ("--balance",)):
+        line = _run("--gpus", "8", "--steps", "2", "--warmup", "1", "--dry-run", "--config", "c4", *extra)
+        c = line["config"]
+        assert line["n_gpus"] == 8 and c["N_total"] == 4096 and c["agents_per_rank"] == 512
+        assert c["shards_tile_agents"] is True and c["balanced"] == bool(extra)
+        if not extra:
+            assert c["shard_first_agents"] == [512 * r for r in range(8)]
+
+
 def test_world_size_mismatch_is_refused():
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run"],

@@ -136,6 +136,17 @@ def test_dist_scvx_3d_jacobi_sweep_matches_dense_oracle(cuda):
             for t in range(d.T - 1):
                 dX[t + 1] = d.Ad @ dX[t] + d.Bd @ dU[t]
             assert np.abs((got_X - Xn) - dX).max() < 1e-5
+            # a direct bound on the state error: |dX_t| <= sum_s ||Ad^(t-1-s) Bd||_2 |dU_s| <= G ||dU||_F by
+            # Cauchy-Schwarz, G^2 = max_t sum_{s<t} ||Ad^(t-1-s) Bd||_2^2 (the input-to-state gain over the horizon)
+            gains, Phi = [], np.eye(6)
+            for _ in range(d.T - 1):
+                gains.append(np.linalg.norm(Phi @ d.Bd, 2) ** 2)
+                Phi = d.Ad @ Phi
+            G = np.sqrt(np.sum(gains))
+            bound_x = G * np.sqrt(np.sum(dU[:-1] ** 2)) + 1e-6
+            err_x = np.abs(got_X - Xn).max()
+            print(f"{nm}: max |dU| {np.abs(dU[:-1]).max():.2e}  max |dX| {err_x:.2e}  bound {bound_x:.2e}")
+            assert err_x <= bound_x, (nm, err_x, bound_x)
         np.testing.assert_array_equal(X1[nm][-1, 6:9], X0[nm][-1, 6:9])  # pinned unused row
 
 

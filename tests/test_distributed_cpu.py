@@ -227,3 +227,34 @@ def test_balanced_shard_order_matches_single_process():
     inv = np.argsort(order)
     np.testing.assert_allclose(X_single[inv], X_contig, rtol=0, atol=1e-3)
     assert [c["overflow"] for c in ck_single] == [c["overflow"] for c in ck_contig] == [0] * ITERS
+
+
+@pytest.mark.parametrize("balanced", [False, True])
+def test_world4_culled_coupling_matches_single_process(balanced):
+    """The C4 path at world 4 (gloo; the 8-GPU driver run deals 512 agents per rank the same way): the culled
+    coupling rows, the full-row check and the re-solve of violating agents, the global trust-region rule's scalar
+    all_reduce -- contiguous or balanced shards (scvx_hip.scvx.balanced_order over 4 ranks).  Bit-identical iterates,
+    radii and per-step check counts to one process owning all agents in the same order."""
+    from scvx_hip.scvx import balanced_order
+    order = None
+    if balanced:
+        order = balanced_order(np.array([9, 5, 5, 12, 5, 6, 14, 5]), 4)
+        assert sorted(order.tolist()) == list(range(N_CULL))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    _run_culled(0, 1, 0, q, order)
+    _, X_single, tr_single, ck_single, st = q.get()
+    assert st < 2
+    port = _free_port()
+    procs = [ctx.Process(target=_run_culled, args=(r, 4, port, q, order)) for r in range(4)]
+    for p in procs:
+        p.start()
+    res = dict((r, (x, tr, ck, s_)) for r, x, tr, ck, s_ in (q.get(timeout=300) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    np.testing.assert_array_equal(np.concatenate([res[r][0] for r in range(4)]), X_single)
+    np.testing.assert_array_equal(np.concatenate([res[r][1] for r in range(4)]), tr_single)
+    for k in range(ITERS):
+        for key in ("violated", "resolved", "overflow"):
+            assert sum(res[r][2][k][key] for r in range(4)) == ck_single[k][key], (k, key)

@@ -121,3 +121,62 @@ def test_jacobi_qp_of_a_user_model_matches_twin_and_dense(cuda):
         # objective's largest weight (w_obs = 1e6), so their optimal values agree to ~1e-8 of it, not of obj
         assert abs(og[ag] - objd) <= 1e-7 * max(1.0, abs(objd)), (ag, og[ag], objd)
         assert max(qd.constraint_violation(prob, Xg[ag], Ug[ag]).values()) < 1e-7
+
+
+@pytest.mark.parametrize("name,vc", [("unicycle_accel", True), ("triple_int", False), ("triple_int", True)])
+def test_jacobi_qp_of_other_user_classes(cuda, name, vc):
+    """The runtime QP classes the kernel builds for other (n_x, n_u): an odd n_x <= 8 with virtual control
+    (UnicycleAccel, (5, 2)) and an n_x in 9..16 other than the built-in 12 (TripleInt3D, (9, 3): the dense packet /
+    workspace row-state / descriptor-table path of the n > 8 classes), with and without virtual control.  Against
+    the CPU twin on every agent (objective 1e-8 relative) and the dense reference-form oracle on a sample
+    (objective 1e-7, violation 1e-7; virtual-control solutions are unique only up to the L1 penalty's
+    degeneracy, so the value and feasibility are what is compared there, as tests/test_virtual_control_gpu.py)."""
+    import torch
+    from oracle import problems as pb, qp_cpu, qp_dense as qd
+    from scvx_hip import QPSolver, QPSpec
+    from scvx_hip.rtc import DeviceModel
+    mdl = cm.UnicycleAccel() if name == "unicycle_accel" else cm.TripleInt3D()
+    n, m = mdl.n_x, mdl.n_u
+    dm = DeviceModel.from_callables(*mdl.get_equations(), n, m)
+    N, K, sigma, tr = 12, 30, 8.0, 0.5
+    rng = np.random.default_rng(11)
+    pd = 2 if n == 5 else 3
+    a = np.linspace(0.0, 1.0, K)
+    x0 = np.zeros((N, n)); xf = np.zeros((N, n))
+    lo, hi = (4, 6) if n == 5 else (2, 3)
+    x0[:, :pd] = rng.uniform(-hi, -lo, (N, pd)); xf[:, :pd] = rng.uniform(lo, hi, (N, pd))
+    if n == 5:
+        xf[:, 2] = np.arctan2(xf[:, 1] - x0[:, 1], xf[:, 0] - x0[:, 0])
+        x0[:, 2] = xf[:, 2]
+    X = (1 - a)[None, :, None] * x0[:, None] + a[None, :, None] * xf[:, None]
+    if n == 5:
+        X[:, 1:-1, 3] = np.linalg.norm(xf[:, :2] - x0[:, :2], axis=1)[:, None] / sigma
+    U = np.zeros((N, K, m))
+    T = lambda v: torch.tensor(np.ascontiguousarray(v), dtype=torch.float64, device=cuda)  # noqa: E731
+    disc = dm.foh(T(X), T(U), T(np.full(N, sigma)))
+    box = [(0, -12.0, 12.0), (1, -12.0, 12.0)]
+    obs = [(np.array([0.0, 0.5] + ([0.0] if pd == 3 else [])), 1.5 if n == 5 else 1.0)]
+    extra = dict(w_nu=1e4, w_prox=1.0) if vc else {}
+    spec = QPSpec(model=dm, K=K, pos_dim=pd, box=box, obs=obs, w_obs=1e6, has_final=False, w_final=50.0, tol=1e-10,
+                  max_iter=80, **extra)
+    out = QPSolver(spec, N, device=cuda).solve(disc, T(np.full(N, sigma)), T(X), T(U), T(x0), T(xf), T(np.full(N, tr)))
+    st = out["status"].cpu().numpy()
+    assert (st == 0).all(), st
+    dn = disc.cpu().numpy()
+    tpl = qp_cpu.make_template(n, m, K, pos_dim=pd, box=box, obs=obs, w_obs=1e6, has_final=False, w_final=50.0,
+                               tol=1e-10, max_iter=80, model_id=255, **extra)
+    cpu = qp_cpu.solve_batched(tpl, dn, np.full(N, sigma), X, U, x0, xf, np.full(N, tr))
+    assert (cpu["status"] == 0).all(), cpu["status"]
+    og, Xg, Ug = out["obj"].cpu().numpy(), out["X"].cpu().numpy(), out["U"].cpu().numpy()
+    np.testing.assert_allclose(og, cpu["obj"], rtol=1e-8)
+    nug = out["nu"].cpu().numpy() if vc else None
+    for ag in (0, 7):
+        A, B, C, S, z = pb.unpack_disc(dn[ag], n, m)
+        prob = dict(A=A, B=B, C=C, c=S * sigma + z, Xref=X[ag], Uref=U[ag], x_final=xf[ag], w_final=50.0, tr=tr,
+                    box=box, obs=obs, w_obs=1e6, fix_last_input=True, pos_dim=pd, **extra)
+        with np.errstate(all="ignore"):
+            Xd, Ud, objd, info = qd.solve_agent(prob, sparse=True, tol=1e-11, maxit=150)
+        assert info["status"] == "optimal", (ag, info["status"])
+        assert abs(og[ag] - objd) <= 1e-7 * max(1.0, abs(objd)), (ag, og[ag], objd)
+        viol = qd.constraint_violation(prob, Xg[ag], Ug[ag], nu=nug[ag] if vc else None)
+        assert max(viol.values()) < 1e-7, (ag, viol)
