@@ -43,7 +43,6 @@ extern "C" size_t scvx_scp_workspace_bytes(const scvx_scp_template* T, int N) {
     return sizeof(double) * (size_t)N * (size_t)L.stride * (size_t)(T->K + 1);  // + the per-lane junk block
 }
 
-static int g_scp_waves = 0;  // scvx_scp_set_waves_per_agent: 0 automatic, 1 or 2 forced
 
 static int scp_launch(const scvx_scp_template* T, int N, const double* disc, const double* Xref, const double* Uref,
                       const double* sigma_ref, const double* tr, const double* x_init, const double* x_final,
@@ -100,8 +99,8 @@ static int scp_launch(const scvx_scp_template* T, int N, const double* disc, con
             simds = 4 * cus;
         if (simds <= 0) simds = 1024;
     }
-    // the template's own mapping; 0 falls back to the process default (scvx_scp_set_waves_per_agent)
-    const int wsel = T->waves_per_agent ? T->waves_per_agent : g_scp_waves;
+    // the template's own mapping: 0 automatic, 1 or 2 forced
+    const int wsel = T->waves_per_agent;
     const bool two = wsel == 2 || (wsel == 0 && T->K > WAVE && 2LL * N <= simds);
     if (T->model_id == SCVX_MODEL_UNICYCLE && T->n_x == 3 && T->n_u == 2) {
         if (T->has_soc) return set_error(SCVX_EUNSUPPORTED, "scp: SOC rows need n_u + 1 <= 4");
@@ -131,11 +130,6 @@ static int scp_launch(const scvx_scp_template* T, int N, const double* disc, con
     return check_launch("scp_ipm_kernel");
 }
 
-extern "C" int scvx_scp_set_waves_per_agent(int waves) {
-    if (waves < 0 || waves > 2) return set_error(SCVX_EINVAL, "scp: waves per agent must be 0, 1 or 2");
-    g_scp_waves = waves;
-    return SCVX_OK;
-}
 
 extern "C" int scvx_scp_solve_batched(const scvx_scp_template* T, int N, const double* disc, const double* Xref,
                                       const double* Uref, const double* sigma_ref, const double* tr,

@@ -389,9 +389,8 @@ class SCPSpec:
     w_in: float = 0.0
     n_slab: int = 0
     r_slab: float = 0.0
-    # launch mapping of this template's solves: 0 = the library's default (automatic: two waves per agent when
-    # K > 64 and the launch leaves SIMDs idle), 1 or 2 forced -- per template, so concurrent callers never
-    # share it (the process-wide scvx_scp_set_waves_per_agent is only the default for 0)
+    # launch mapping of this template's solves: 0 = automatic (two waves per agent when K > 64 and the launch
+    # leaves SIMDs idle), 1 or 2 forced -- per template, so concurrent callers never share it
     waves_per_agent: int = 0
 
     def to_c(self):

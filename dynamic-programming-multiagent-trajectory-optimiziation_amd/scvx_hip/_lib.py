@@ -11,7 +11,7 @@ LIB_PATH = os.environ.get("SCVX_HIP_LIB") or os.path.join(HERE, "libscvx_hip.so"
 
 # the C-ABI revision these bindings are written for (SCVX_HIP_VERSION of include/scvx_hip.h): a library of
 # another revision would take these argument lists with shifted pointers, so lib() refuses it
-SCVX_HIP_VERSION = 4
+SCVX_HIP_VERSION = 5
 SCVX_MAX_BOX, SCVX_MAX_OBS, SCVX_MAX_NBR = 4, 16, 32
 SCVX_IS_MAX_PROJ, SCVX_IS_MAX_STATE = 3, 12
 MODEL_IDS = {"di": 0, "unicycle": 1, "si": 2, "quad": 3}
@@ -23,7 +23,6 @@ STATUS = {0: "optimal", 1: "optimal_inaccurate", 2: "solver_error"}
 EXPORTS = ("scvx_version", "scvx_last_error", "scvx_foh_batched", "scvx_integrate_nonlinear_batched",
            "scvx_qp_solve_batched", "scvx_qp_solve_batched_ordered", "scvx_qp_workspace_bytes", "scvx_qp_set_trace",
            "scvx_collision_rows_batched", "scvx_collision_rows_indexed", "scvx_collision_check_batched", "scvx_scp_solve_batched", "scvx_scp_workspace_bytes",
-           "scvx_scp_set_waves_per_agent",
            "scvx_intersample_batched", "scvx_admm_consensus_batched", "scvx_scp_game_solve_batched",
            "scvx_slab_update_batched", "scvx_jacobi_update_batched", "scvx_rtc_model_create",
            "scvx_rtc_model_source", "scvx_rtc_model_log", "scvx_rtc_model_destroy", "scvx_rtc_foh_batched",
@@ -108,7 +107,6 @@ def lib():
         L.scvx_qp_solve_batched.argtypes = [ctypes.POINTER(QPTemplate), i32] + [vp] * 17 + [vp, sz, vp]
         L.scvx_qp_solve_batched_ordered.argtypes = [ctypes.POINTER(QPTemplate), i32] + [vp] * 18 + [vp, sz, vp]
         L.scvx_qp_set_trace.argtypes = [vp, i32, i32]
-        L.scvx_scp_set_waves_per_agent.argtypes = [i32]
         L.scvx_collision_rows_batched.argtypes = [i32, i32, i32, i32, vp, i32, i32, dbl, dbl, i32, vp, vp, vp]
         L.scvx_collision_rows_indexed.argtypes = [i32, i32, i32, i32, vp, vp, i32, dbl, dbl, i32, vp, vp, vp]
         L.scvx_collision_check_batched.argtypes = [i32, i32, i32, i32, vp, i32, i32, dbl, vp, vp, dbl, vp, vp, vp]

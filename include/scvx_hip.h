@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SCVX_HIP_VERSION 4
+#define SCVX_HIP_VERSION 5
 
 #define SCVX_OK 0
 #define SCVX_EINVAL (-1)
@@ -204,7 +204,9 @@ int scvx_qp_solve_batched(const scvx_qp_template* tpl, int N, const double* disc
 
 /* scvx_qp_solve_batched with a dispatch order (replaces the same call, qp_capi.hip; the reference has no
  * counterpart -- its agents' subproblems are solved one by one, dist_scvx_3d.py:110): workgroup b solves agent
- * order[b] (device int32 [N], a permutation of 0..N-1; NULL = agent b; an entry outside [0, N) falls back to b).
+ * order[b] (device int32 [N], a permutation of 0..N-1; NULL = agent b).  A non-permutation is undefined
+ * behaviour: an entry outside [0, N) is replaced by b, which can duplicate an agent (two workgroups then share
+ * its workspace and outputs) and leave another unsolved.
  * Workgroups start in index order as slots free up, so when the agents outnumber the resident waves the
  * longest solves dealt first shorten the launch (JacobiSCvx orders by the last step's IPM iterations).
  * Results do not depend on the order. */
@@ -316,8 +318,9 @@ typedef struct scvx_scp_template {
     double w_in;            /* inertia_weight       * ||X - X_prev||_F^2              (:99-100) */
     int32_t n_slab;         /* slab rows z_{j,k}'(p_k - P_{j,k}) >= r_slab per node (:121-124), <= SCVX_MAX_NBR */
     double r_slab;          /* collision_radius */
-    /* launch mapping of this template's solves (version 4): 0 = the process default of
-     * scvx_scp_set_waves_per_agent (itself automatic unless set), 1 or 2 waves per agent forced */
+    /* launch mapping of this template's solves (version 4; version 5 dropped the process-wide default setter):
+     * 0 = automatic -- two waves per agent when K > 64 and the launch leaves SIMDs idle (2 N <= 4 x CUs), so the
+     * node phases of a K <= 128 agent run in one pass; 1 or 2 waves per agent forced */
     int32_t waves_per_agent;
 } scvx_scp_template;
 
@@ -339,13 +342,7 @@ int scvx_scp_solve_batched(const scvx_scp_template* tpl, int N, const double* di
  * N agents (depends on the game fields: the game kernel carries extra Riccati states). */
 size_t scvx_scp_workspace_bytes(const scvx_scp_template* tpl, int N);
 
-/* Waves per agent of the SCP kernels (scvx_scp_solve_batched / scvx_scp_game_solve_batched): 0 (default) =
- * automatic -- two when K > 64 and the launch leaves SIMDs idle (2 N <= 4 x CUs), so the node phases of a
- * K <= 128 agent run in one pass; 1 or 2 forces the mapping.  This setter is a process-wide DEFAULT, read
- * only by templates whose own `waves_per_agent` is 0; concurrent callers that need a mapping set it in
- * their template (version 4) and never touch the default.  Returns SCVX_OK, or SCVX_EINVAL for another
- * value.  (No reference counterpart: a launch parameter.) */
-int scvx_scp_set_waves_per_agent(int waves);
+
 
 /* ------------------------------------------------------------------------------------------
  * Batched Nash best response: AgentBestResponse.setup/solve (SCvx/optimization/agent_best_response.py:
