@@ -11,6 +11,10 @@ The batched entry point is `segment_minima(foh, X, U, obstacles, T, sigma)`: eve
 obstacle of a trajectory in one launch, i.e. the data of the reference's per-segment loop in
 SCvx/models/game_si_model.py:156-176 (`t*`, `h0`, `grad_x`, `grad_u` per minimum).
 
+Any model the FirstOrderHold runs on the GPU is served: the built-in device models, and every other BaseModel
+through its runtime-compiled DeviceModel (scvx_hip.rtc; the scan kernel is compiled next to the model's f,
+scvx_rtc_intersample_batched) -- as the reference's scan integrates model.get_equations()'s f for any model.
+
 A user-supplied Python callable `f` (not a `SegmentRollout`) can only run on the host.  For it, the
 scan and the central differences are evaluated on the host by the same rules.
 """
@@ -20,7 +24,6 @@ import numpy as np
 
 import scvx_hip
 
-from ..discretization.first_order_hold import builtin_model
 
 
 def _t(a, device):
@@ -33,7 +36,7 @@ class SegmentRollout:
     tau in [0, t dt_phys], dt_phys = foh.dt * sigma (make_segment_f, :104-126)."""
 
     def __init__(self, foh, u0, u1, sigma):
-        self.model = builtin_model(foh.model, "SegmentRollout")
+        self.model = foh._name   # a built-in model name or the model's runtime-compiled DeviceModel
         self.params = getattr(foh.model, "scvx_params", None)
         self.device = getattr(foh, "_device", "cuda")
         self.u0 = np.asarray(u0, float).reshape(-1)
@@ -49,7 +52,10 @@ class SegmentRollout:
         X = _t(np.stack([xk, xk])[None], self.device)
         U = _t(np.stack([self.u0, self.u0 + t * (self.u1 - self.u0)])[None], self.device)
         s = _t([t * self.dt_phys], self.device)
-        out = scvx_hip.integrate_nonlinear(self.model, X, U, s, True, params=self.params)
+        if isinstance(self.model, str):
+            out = scvx_hip.integrate_nonlinear(self.model, X, U, s, True, params=self.params)
+        else:
+            out = self.model.integrate_nonlinear(X, U, s, True, params=self.params)
         return out[0, 1].cpu().numpy()
 
 
@@ -134,7 +140,7 @@ def segment_minima(foh, X: np.ndarray, U: np.ndarray, obstacles: Sequence, T, si
     """All segments x obstacles of one trajectory (X (n,K), U (m,K)) in one kernel launch:
     {(k, obstacle_index): [(t*, h0, grad_x, grad_u), ...]} -- what game_si_model.py:156-176
     computes with K-1 make_segment_f / find_critical_times / linearize_h rounds."""
-    model = builtin_model(foh.model, "segment_minima")
+    model = foh._name   # a built-in model name or the model's runtime-compiled DeviceModel
     dev = getattr(foh, "_device", "cuda")
     K = X.shape[1]
     out = scvx_hip.intersample_batched(model, _t(np.asarray(X, float).T[None], dev), _t(np.asarray(U, float).T[None], dev),

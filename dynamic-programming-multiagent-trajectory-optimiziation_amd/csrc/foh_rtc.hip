@@ -25,13 +25,21 @@
 
 #include "common.hpp"
 #include "foh_body.hpp"  // ModelParams (the launch argument)
+#include "intersample_body.hpp"  // ISArgs, intersample_check
 #include "scvx_hip.h"
 
 namespace {
 
-// csrc/foh_body.hpp as a string literal (build/foh_body.inc, generated by the Makefile)
+// csrc/foh_body.hpp, csrc/intersample_body.hpp and include/scvx_hip.h as string literals (build/*.inc, generated
+// by the Makefile)
 const char* const kFohBody =
 #include "foh_body.inc"
+    ;
+const char* const kIsBody =
+#include "intersample_body.inc"
+    ;
+const char* const kScvxHdrF =
+#include "scvx_hip_h.inc"
     ;
 
 bool is_zero(const char* e) {
@@ -97,12 +105,17 @@ std::string generate(int n, int m, const char* const* f, const char* const* A, c
     s += "extern \"C\" __global__ __launch_bounds__(256) void scvx_rtc_nonlinear(const double* X, const double* U,\n"
          "        const double* sigma, double* Xout, int K, int N, int nsub, int piecewise, scvx::ModelParams P) {\n"
          "    scvx::nonlinear_body<UserModel>(X, U, sigma, Xout, K, N, nsub, piecewise, P);\n}\n";
+    if (n <= SCVX_IS_MAX_STATE) {   // the inter-sample scan (csrc/intersample_body.hpp) on this model's f
+        s += "#include \"intersample_body.hpp\"\n";
+        s += "extern \"C\" __global__ __launch_bounds__(256) void scvx_rtc_intersample(scvx::ISArgs a) {\n"
+             "    scvx::intersample_body<UserModel>(a);\n}\n";
+    }
     return s;
 }
 
 struct Loaded {
     hipModule_t mod = nullptr;
-    hipFunction_t foh = nullptr, nl = nullptr;
+    hipFunction_t foh = nullptr, nl = nullptr, is = nullptr;
 };
 
 }  // namespace
@@ -135,6 +148,10 @@ int load(const scvx_rtc_model* cm, Loaded* out) {
         (void)hipModuleUnload(L.mod);
         return scvx::set_error(SCVX_ELAUNCH, "rtc: kernels missing from the code object");
     }
+    if (md->n <= SCVX_IS_MAX_STATE && hipModuleGetFunction(&L.is, L.mod, "scvx_rtc_intersample") != hipSuccess) {
+        (void)hipModuleUnload(L.mod);
+        return scvx::set_error(SCVX_ELAUNCH, "rtc: intersample kernel missing from the code object");
+    }
     md->loaded[dev] = L;
     *out = L;
     return SCVX_OK;
@@ -162,9 +179,9 @@ extern "C" int scvx_rtc_model_create(int n_x, int n_u, const char* const* f_expr
     md->m = n_u;
     md->src = generate(n_x, n_u, f_exprs, A_exprs, B_exprs, prelude);
     hiprtcProgram prog;
-    const char* hdr_src[1] = {kFohBody};
-    const char* hdr_name[1] = {"foh_body.hpp"};
-    if (hiprtcCreateProgram(&prog, md->src.c_str(), "scvx_user_model.hip", 1, hdr_src, hdr_name) !=
+    const char* hdr_src[3] = {kFohBody, kIsBody, kScvxHdrF};
+    const char* hdr_name[3] = {"foh_body.hpp", "intersample_body.hpp", "scvx_hip.h"};
+    if (hiprtcCreateProgram(&prog, md->src.c_str(), "scvx_user_model.hip", 3, hdr_src, hdr_name) !=
         HIPRTC_SUCCESS) {
         delete md;
         return scvx::set_error(SCVX_EINVAL, "rtc: hiprtcCreateProgram failed");
@@ -253,6 +270,36 @@ extern "C" int scvx_rtc_integrate_nonlinear_batched(const scvx_rtc_model* model,
     hipError_t e = hipModuleLaunchKernel(L.nl, grid, 1, 1, block, 1, 1, 0, (hipStream_t)stream, args, nullptr);
     if (e != hipSuccess) {
         std::string msg = std::string("rtc nl launch: ") + hipGetErrorString(e);
+        return scvx::set_error(SCVX_ELAUNCH, msg.c_str());
+    }
+    return SCVX_OK;
+}
+
+extern "C" int scvx_rtc_intersample_batched(const scvx_rtc_model* model, const double* params, int n_params,
+                                            const scvx_intersample_template* tpl, int K, int N, const double* X,
+                                            const double* U, const double* sigma, int32_t* n_crit, double* t_crit,
+                                            double* h0, double* grad_x, double* grad_u, void* stream) {
+    if (!model || model->code.empty() || !tpl) return scvx::set_error(SCVX_EINVAL, "rtc intersample: bad args");
+    if (const char* bad = scvx::intersample_check(*tpl, K, N, model->n)) return scvx::set_error(SCVX_EINVAL, bad);
+    scvx::ModelParams P;
+    if (int rc = params_of(params, n_params, &P)) return rc;
+    if (N == 0 || tpl->n_obs == 0) return SCVX_OK;
+    if (!X || !U || !sigma || !n_crit || !t_crit || !h0 || !grad_x || !grad_u)
+        return scvx::set_error(SCVX_EINVAL, "rtc intersample: null buffer");
+    Loaded L;
+    if (int rc = load(model, &L)) return rc;
+    scvx::ISArgs a{};
+    a.T = *tpl;
+    a.K = K; a.N = N;
+    a.X = X; a.U = U; a.sigma = sigma;
+    a.n_crit = n_crit; a.t_crit = t_crit; a.h0 = h0; a.grad_x = grad_x; a.grad_u = grad_u;
+    a.P = P;
+    const long long nwork = (long long)N * (K - 1) * tpl->n_obs;
+    const unsigned grid = (unsigned)((nwork + 255) / 256);
+    void* args[] = {(void*)&a};
+    hipError_t e = hipModuleLaunchKernel(L.is, grid, 1, 1, 256, 1, 1, 0, (hipStream_t)stream, args, nullptr);
+    if (e != hipSuccess) {
+        std::string msg = std::string("rtc intersample launch: ") + hipGetErrorString(e);
         return scvx::set_error(SCVX_ELAUNCH, msg.c_str());
     }
     return SCVX_OK;

@@ -588,23 +588,27 @@ def intersample_batched(model, X, U, sigma, obstacles, proj=None, dt=1.0, seg_dt
     """Inter-sample obstacle minima for every (agent, segment, obstacle) (scvx_intersample_batched;
     SCvx/utils/intersample_collision.py as called per segment by SCvx/models/game_si_model.py:156-176).
 
-    X (N,K,n), U (N,K,m), sigma (N,) float64 device tensors; obstacles [(center (pd,), radius)];
-    proj (pd, n) projection T (default: the first pd state rows); dt as find_critical_times;
-    seg_dt = FirstOrderHold.dt (default 1/(K-1)).  Returns device tensors n_crit (N,K-1,O) int32 and
-    t_crit / h0 (N,K-1,O,max_crit), grad_x (...,n), grad_u (...,m); entries past n_crit are unset."""
+    model: a built-in model name, or a scvx_hip.rtc.DeviceModel (any user model: scvx_rtc_intersample_batched,
+    the same scan on its runtime-compiled f).  X (N,K,n), U (N,K,m), sigma (N,) float64 device tensors;
+    obstacles [(center (pd,), radius)]; proj (pd, n) projection T (default: the first pd state rows); dt as
+    find_critical_times; seg_dt = FirstOrderHold.dt (default 1/(K-1)).  Returns device tensors n_crit (N,K-1,O)
+    int32 and t_crit / h0 (N,K-1,O,max_crit), grad_x (...,n), grad_u (...,m); entries past n_crit are unset."""
     import numpy as np
     torch = _torch()
-    n, m = MODEL_DIMS[model]
+    rt = not isinstance(model, str)
+    n, m = model.dims if rt else MODEL_DIMS[model]
     N, K = X.shape[0], X.shape[1]
     if X.shape != (N, K, n) or U.shape != (N, K, m) or sigma.shape != (N,):
         raise ValueError(f"intersample_batched: X (N,K,{n}), U (N,K,{m}), sigma (N,) expected")
     O = len(obstacles)
     if O > _lib.SCVX_MAX_OBS:
         raise ValueError("too many obstacles")
+    if n > _lib.SCVX_IS_MAX_STATE:
+        raise ValueError(f"intersample_batched: n_x {n} > {_lib.SCVX_IS_MAX_STATE}")
     pd = len(np.asarray(obstacles[0][0]).reshape(-1)) if O else 1
     Tm = np.eye(n)[:pd] if proj is None else np.asarray(proj, float).reshape(pd, n)
     t = _lib.IntersampleTemplate()
-    t.model_id, t.n_obs, t.proj_rows = MODEL_IDS[model], O, pd
+    t.model_id, t.n_obs, t.proj_rows = (_lib.SCVX_MODEL_RUNTIME if rt else MODEL_IDS[model]), O, pd
     for o, (c, r) in enumerate(obstacles):
         c = np.asarray(c, float).reshape(-1)
         if c.size != pd:
@@ -617,7 +621,7 @@ def intersample_batched(model, X, U, sigma, obstacles, proj=None, dt=1.0, seg_dt
             t.proj[i * _lib.SCVX_IS_MAX_STATE + j] = float(Tm[i, j])
     t.dt, t.seg_dt = float(dt), float(1.0 / (K - 1) if seg_dt is None else seg_dt)
     t.eps, t.tol, t.num_samples, t.max_crit = float(eps), float(tol), int(num_samples), int(max_crit)
-    t.nsub = int(nsub or DEFAULT_NSUB[model])
+    t.nsub = int(nsub or (model.nsub if rt else DEFAULT_NSUB[model]))
     dev = X.device
     f64 = torch.float64
     shp = (N, K - 1, max(O, 1))
@@ -626,11 +630,15 @@ def intersample_batched(model, X, U, sigma, obstacles, proj=None, dt=1.0, seg_dt
                h0=torch.zeros(shp + (max_crit,), dtype=f64, device=dev),
                grad_x=torch.zeros(shp + (max_crit, n), dtype=f64, device=dev),
                grad_u=torch.zeros(shp + (max_crit, m), dtype=f64, device=dev))
-    keep, pp = _params(model, params)
-    rc = lib().scvx_intersample_batched(ctypes.byref(t), pp, K, N, _dev(X, name="X"), _dev(U, name="U"),
-                                        _dev(sigma, name="sigma"), _dev(out["n_crit"], torch.int32),
-                                        _dev(out["t_crit"]), _dev(out["h0"]), _dev(out["grad_x"]),
-                                        _dev(out["grad_u"]), _stream(stream))
-    check(rc, "scvx_intersample_batched")
-    del keep
+    bufs = (_dev(X, name="X"), _dev(U, name="U"), _dev(sigma, name="sigma"), _dev(out["n_crit"], torch.int32),
+            _dev(out["t_crit"]), _dev(out["h0"]), _dev(out["grad_x"]), _dev(out["grad_u"]), _stream(stream))
+    if rt:
+        pa, npar = model._pp(params)
+        rc = lib().scvx_rtc_intersample_batched(model._h.ptr, pa.ctypes.data, npar, ctypes.byref(t), K, N, *bufs)
+        check(rc, "scvx_rtc_intersample_batched")
+    else:
+        keep, pp = _params(model, params)
+        rc = lib().scvx_intersample_batched(ctypes.byref(t), pp, K, N, *bufs)
+        check(rc, "scvx_intersample_batched")
+        del keep
     return {k: v[:, :, :O] for k, v in out.items()}

@@ -26,7 +26,7 @@ EXPORTS = ("scvx_version", "scvx_last_error", "scvx_foh_batched", "scvx_integrat
            "scvx_intersample_batched", "scvx_admm_consensus_batched", "scvx_scp_game_solve_batched",
            "scvx_slab_update_batched", "scvx_jacobi_update_batched", "scvx_rtc_model_create",
            "scvx_rtc_model_source", "scvx_rtc_model_log", "scvx_rtc_model_destroy", "scvx_rtc_foh_batched",
-           "scvx_rtc_integrate_nonlinear_batched", "scvx_rtc_subproblem_compile")
+           "scvx_rtc_integrate_nonlinear_batched", "scvx_rtc_subproblem_compile", "scvx_rtc_intersample_batched")
 SCVX_MAX_MODEL_PARAMS, SCVX_RTC_MAX_NX, SCVX_RTC_MAX_NU = 16, 16, 8
 
 
@@ -128,6 +128,7 @@ def lib():
         L.scvx_rtc_model_destroy.argtypes = [vp]
         L.scvx_rtc_foh_batched.argtypes = [vp, vp, i32, i32, i32, vp, vp, vp, i32, vp, vp]
         L.scvx_rtc_integrate_nonlinear_batched.argtypes = [vp, vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp]
+        L.scvx_rtc_intersample_batched.argtypes = [vp, vp, i32, ctypes.POINTER(IntersampleTemplate), i32, i32] + [vp] * 9
         sized = ("scvx_last_error", "scvx_qp_workspace_bytes", "scvx_scp_workspace_bytes", "scvx_rtc_model_source",
                  "scvx_rtc_model_log")
         for fn in EXPORTS:

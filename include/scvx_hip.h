@@ -410,6 +410,15 @@ int scvx_intersample_batched(const scvx_intersample_template* tpl, const double*
                              const double* X, const double* U, const double* sigma, int32_t* n_crit,
                              double* t_crit, double* h0, double* grad_x, double* grad_u, void* stream);
 
+/* scvx_intersample_batched for a runtime-compiled user model (scvx_rtc_model_create; n_x <= SCVX_IS_MAX_STATE):
+ * the same scan on the model's own f, so the inter-sample search of any BaseModel runs on the GPU (the reference's
+ * SCvx/utils/intersample_collision.py:104-126 integrates model.get_equations()'s f with odeint for any model).
+ * tpl->model_id is ignored; params / n_params as scvx_rtc_foh_batched.  (version 5) */
+int scvx_rtc_intersample_batched(const scvx_rtc_model* model, const double* params, int n_params,
+                                 const scvx_intersample_template* tpl, int K, int N, const double* X, const double* U,
+                                 const double* sigma, int32_t* n_crit, double* t_crit, double* h0, double* grad_x,
+                                 double* grad_u, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * ADMM consensus / dual update of the multi-agent coordinators: replaces the host loop of
  * SCvx/optimization/admm_coordinator.py:80-96 (si_admm_coordinator.py:91-102).  For agent i and

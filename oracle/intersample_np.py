@@ -28,7 +28,12 @@ def _rollout(f, x0, u0, u1, dtp, t, nsub):
 
 def segment(model, xk, u0, u1, dtp, T, center, radius, dt=1.0, num_samples=100, eps=1e-4, tol=1e-6, nsub=16):
     """Minima of one (segment, obstacle): list of (t*, h0, grad_x, grad_u)."""
-    f = models_np.MODELS[model][2]()[0]
+    return segment_f(models_np.MODELS[model][2]()[0], xk, u0, u1, dtp, T, center, radius, dt, num_samples, eps, tol,
+                     nsub)
+
+
+def segment_f(f, xk, u0, u1, dtp, T, center, radius, dt=1.0, num_samples=100, eps=1e-4, tol=1e-6, nsub=16):
+    """segment() for any model given as its numpy f(x, u) (a BaseModel's get_equations()[0])."""
     T = np.asarray(T, float)
     c = np.asarray(center, float)
 

@@ -162,7 +162,11 @@ def test_first_order_hold_routes_custom_models():
     car.scvx_device_model = dm
     assert device_model(car) is dm
     with pytest.raises(NotImplementedError, match="runtime-compiled FOH path only"):
-        builtin_model(car, "segment_minima")            # the inter-sample search: built-in models only
+        builtin_model(car, "SCVXSolver")                # the kernels compiled per built-in model class
+    from SCvx.discretization.first_order_hold import FirstOrderHold
+    from SCvx.utils.intersample_collision import SegmentRollout
+    seg = SegmentRollout(FirstOrderHold(car, 20), np.zeros(2), np.ones(2), 2.0)
+    assert seg.model is dm                              # the inter-sample search: on the model's DeviceModel
     sp = SCProblem(car)                                 # the subproblem kernels take any (n_x, n_u) (hipRTC)
     assert sp._dev_model is dm
     from SCvx.discretization.first_order_hold import same_device_model
