@@ -20,9 +20,11 @@ from typing import Optional, Sequence, Tuple
 from . import _lib
 from ._lib import MODEL_DIMS, MODEL_IDS, STATUS, QPTemplate, SCPTemplate, ScvxError, check, lib
 
-# RK4 substeps per FOH interval.  1 is exact for the (linear) integrators; 16 keeps the
-# unicycle / quadrotor within 1e-7 of the reference's LSODA (tests/test_foh_oracle.py).
-DEFAULT_NSUB = {"di": 1, "si": 1, "unicycle": 16, "quad": 16}
+# RK4 substeps per FOH interval: the smallest count that keeps each model within 1e-7 of the reference's LSODA
+# goldens (tests/test_foh_gpu.py, tests/test_foh_oracle.py).  1 is exact for the (linear) integrators; the
+# quadrotor holds at 10 (round 5, oracle/foh_ref.c on tests/golden/foh_quad_K50_s5.npz: max relative error 1.2e-7 at
+# 8, 7.7e-8 at 9, 5.2e-8 at 10, 9e-10 at 16 -- 16 was 2.7 ms of a 47.5 ms C5 step), the unicycle keeps 16.
+DEFAULT_NSUB = {"di": 1, "si": 1, "unicycle": 16, "quad": 10}
 QUAD_PARAMS = (1.0, 9.81, 0.02, 0.02, 0.04)
 
 __all__ = ["model_dims", "model_id", "default_nsub", "foh_batched", "integrate_nonlinear", "collision_rows", "collision_check", "qp_solve_batched", "QPSpec", "SCPSpec", "SCPSolver", "slab_update",

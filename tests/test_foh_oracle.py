@@ -9,7 +9,7 @@ import pytest
 from oracle import foh_oracle
 
 GOLD = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "foh_*.npz")))
-NSUB = {"di": 1, "si": 1, "unicycle": 16, "quad": 16}
+NSUB = {"di": 1, "si": 1, "unicycle": 16, "quad": 10}   # scvx_hip.DEFAULT_NSUB
 
 
 def rel(a, b):
