@@ -582,6 +582,12 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     constexpr int V_M = C::L_M, V_PI0 = C::L_PI0, V_XE = C::L_XE, V_XI0 = C::L_XI0, V_R2F = C::L_R2F,
                   V_YI = C::L_YI, V_YF = C::L_YF, V_DYI = C::L_DYI, V_DYF = C::L_DYF, V_PIV = C::L_PIV,
                   V_ONE = C::L_ONE, V_FLAG = C::L_FLAG, V_ST = C::L_ST, V_S = C::L_S, V_L = C::L_L;
+    // STF: 1 once a stage of the last factor sweep kept a stiff facet (the solve and the Newton passes skip the
+    // stage-system terms otherwise: every stage's slots are empty then)
+    constexpr int V_SANY = C::L_FLAG + 1;
+    auto stf_any = [&]() __attribute__((always_inline)) -> bool {
+        return __builtin_amdgcn_readfirstlane((int)(lds[V_SANY] != 0.0)) != 0;
+    };
     const int V_G = C::L_VAR, V_CH = V_G + K * NX, V_PHI = V_CH + (K + 1) * NX;
     // chunked chains (C::CHK): transitions t = 0..K-2 in chunks of CL; lane = 8 ch + ce carries element ce of
     // chunk ch, whose transitions are [cs0, cs1)
@@ -852,7 +858,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
         for (int e = lane; e < NX * NX; e += WAVE) { lds[C::F_PP + e] = 0.0; lds[C::F_PIP + e] = 0.0; lds[V_M + e] = 0.0; }
         if (lane < NX) lds[V_XE + lane] = 0.0;
-        if (lane == 0) lds[V_FLAG] = 0.0;
+        if (lane == 0) { lds[V_FLAG] = 0.0; lds[V_SANY] = 0.0; }
         __syncthreads();  // the node phase wrote the packets (global) from other lanes
         // packets stream through one LDS slot (a stage's packet is overwritten by the next one after its
         // last read), loads issued 3 stages ahead (register buffers pf[0..2], so the stage loop is
@@ -921,6 +927,10 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 for (int r = 0; r < RT; ++r) qs[r] = tab_ld(r, vo);
             }
             pf_load(ts - FPD, nb);  // unconditional: stage K-1 re-issues K-1-FPD, ts-FPD < 0 reads zeros
+            // STF: the node's largest facet weight if it is a stiff candidate (assemble), else 0 -- read before the
+            // phases, off phase 3's chain
+            double dfmr = 0.0;
+            if constexpr (C::STF) dfmr = lds[C::F_RING + C::P_FD + C::NTR + 1 + C::NFO];
             if constexpr (C::NV > 0) {
                 // ---- phase 0 (virtual control nu_ts): G = diag(D) + P', then [G^-1 Pi' | G^-1 | G^-1 P'] by
                 // Gauss-Jordan without pivoting (G is SPD): lane c < 4 NX owns column c of [G | Pi' | I | P'];
@@ -1005,9 +1015,12 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 double sfd[PMA];
 #pragma unroll
                 for (int i = 0; i < PMA; ++i) { sfi[i] = -1; sfd[i] = 1.0; }
-                bool stg = false;   // this stage keeps a stiff facet (every lane agrees)
+                bool stg = false;   // this stage keeps a stiff facet (uniform: a scalar branch)
                 if constexpr (C::STF) {
-                    constexpr int NTR = C::NTR, NFO = C::NFO, FS = C::F_RING + C::P_FD + NTR;
+                    constexpr int NTR = C::NTR, FS = C::F_RING + C::P_FD + NTR;
+                    // only a candidate node (assemble: its facets left out of R, dfm > 0) takes the facet branch; every
+                    // lane reads the same packet word, and readfirstlane makes the branches scalar (not predicated)
+                    if (__builtin_amdgcn_readfirstlane((int)(dfmr > 0.0))) {
                     double dnf = 0.0;
 #pragma unroll
                     for (int j = 0; j < NU; ++j) dnf = fmax(dnf, fabs(Lm[j * NU + j]));
@@ -1026,7 +1039,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                             }
                         }
                     }
-                    if (lds[FS + 1 + NFO] > thr && !fx) {   // rare: pick the stiff slots, fold only the others
+                    if (__builtin_amdgcn_readfirstlane((int)(dfmr > thr && !fx))) {   // rare: pick the stiff slots, fold only the others
                         double Df[NTR];
                         int cnt = 0;
 #pragma unroll
@@ -1066,7 +1079,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                                     for (int j = 0; j < NU; ++j) Lm[i * NU + j] += (((f >> i) ^ (f >> j)) & 1) ? -d : d;
                             }
                         }
-                        stg = use;
+                        stg = __builtin_amdgcn_readfirstlane((int)use) != 0;
+                        if (stg && sl == 0) lds[V_SANY] = 1.0;
+                    }
                     }
                 }
                 double dmax = 0.0;
@@ -1476,13 +1491,15 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
             for (int i = 0; i < NX; ++i) g[i] = q[i];
             if constexpr (C::STF) {
-                double Gm[PMA * NX];
-                ldb(Gm, C::B_GAM, PM * NX);
-                hold(Gm, PM * NX);
+                if (stf_any()) {
+                    double Gm[PMA * NX];
+                    ldb(Gm, C::B_GAM, PM * NX);
+                    hold(Gm, PM * NX);
 #pragma unroll
-                for (int i = 0; i < PM; ++i)
+                    for (int i = 0; i < PM; ++i)
 #pragma unroll
-                    for (int j = 0; j < NX; ++j) g[j] = fma(-Gm[i * NX + j], rhs_s[i], g[j]);
+                        for (int j = 0; j < NX; ++j) g[j] = fma(-Gm[i * NX + j], rhs_s[i], g[j]);
+                }
             }
 #pragma unroll
             for (int i = 0; i < NU; ++i)
@@ -1679,7 +1696,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 for (int k = i + 1; k < NU; ++k) v -= Ld[k * NU + i] * k0[k];
                 k0[i] = v;
             }
-            if constexpr (C::STF) {
+            if constexpr (C::STF) if (stf_any()) {
                 // a = R0^-1 rh (k0 here); gamma0 = -C^-1 (G'a + rho); k0 = -(a + W gamma0)
                 double sm[C::NSMB];
                 ldb(sm, C::B_WS, C::NSMB);
@@ -1955,7 +1972,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             }
 #pragma unroll
             for (int j = 0; j < NU; ++j) dzo[NX + j] = du[j];
-            if constexpr (C::STF) {
+            if constexpr (C::STF) if (stf_any()) {
                 // the stiff facets' multiplier steps nu = Gamma xi + Gamma_kappa mu + gamma0 (no D (g'du - rho): the
                 // product of a ~1e12 weight and a cancelling difference)
                 double Gm[PMA * NX], Gk[PMA * NX];
@@ -2278,7 +2295,10 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             }
         if constexpr (C::STF) {
             // the facets' weights, their folded sum sum_f D_f g_f g_f' (the diagonal is sum_f D_f; off-diagonal (i, j) the
-            // sum of D_f signed by the parity of facet bits i and j) and their max, for factor phase 3
+            // sum of D_f signed by the parity of facet bits i and j) and their max.  A facet can be stiff in its stage
+            // (phase 3: above QP_STIFF x Rhat's largest diagonal) only if it is above QP_STIFF x R's (Rhat = R +
+            // Bt'P Bt >= R): the other nodes (nearly all of them) fold their facets into R here and store dfm = 0, so
+            // their stages run phase 3 without the facet branch
             double dsum = 0.0, dfm = 0.0, osum[C::NFO > 0 ? C::NFO : 1];
 #pragma unroll
             for (int e = 0; e < C::NFO; ++e) osum[e] = 0.0;
@@ -2293,10 +2313,23 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                     for (int j = i + 1; j < NU; ++j, ++e) osum[e] += (((f >> i) ^ (f >> j)) & 1) ? -Dfc[f] : Dfc[f];
             }
-            pst(C::gFD + C::NTR, dsum);
+            double rdm = 0.0;
 #pragma unroll
-            for (int e = 0; e < C::NFO; ++e) pst(C::gFD + C::NTR + 1 + e, osum[e]);
-            pst(C::gFD + C::NTR + 1 + C::NFO, dfm);
+            for (int i = 0; i < NU; ++i) rdm = fmax(rdm, fabs(Ru[i * NU + i]));
+            const bool cand = dfm > QP_STIFF * rdm;
+            {
+                int e = 0;
+#pragma unroll
+                for (int i = 0; i < NU; ++i) {
+                    Ru[i * NU + i] += cand ? 0.0 : dsum;
+#pragma unroll
+                    for (int j = i + 1; j < NU; ++j, ++e) Ru[i * NU + j] += cand ? 0.0 : osum[e];
+                }
+            }
+            pst(C::gFD + C::NTR, cand ? dsum : 0.0);
+#pragma unroll
+            for (int e = 0; e < C::NFO; ++e) pst(C::gFD + C::NTR + 1 + e, cand ? osum[e] : 0.0);
+            pst(C::gFD + C::NTR + 1 + C::NFO, cand ? dfm : 0.0);
         }
 #pragma unroll
         for (int i = 0; i < NU; ++i)
@@ -2914,12 +2947,13 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             issue_soc();
             ldn(r1, C::C_RD, NZ);
             if (corr) ldn(cpv, C::C_CP, NR);
-            if constexpr (C::STF) ldb(sfr, C::B_SF, C::PM);
+            const bool sany = C::STF && stf_any();   // uniform: a stage of this factor kept a stiff facet
+            if constexpr (C::STF) if (sany) ldb(sfr, C::B_SF, C::PM);
             hold_state();
             hold_soc();
             hold(r1, NZ);
             if (corr) hold(cpv, NR);
-            if constexpr (C::STF) hold(sfr, C::PM);
+            if constexpr (C::STF) if (sany) hold(sfr, C::PM);
             double rhs_s[C::PMA];
 #pragma unroll
             for (int i = 0; i < C::PMA; ++i) rhs_s[i] = 0.0;

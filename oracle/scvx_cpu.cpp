@@ -517,7 +517,13 @@ static void riccati_factor(const Agent& ag, const std::vector<Mat>& H, Riccati& 
             // would lose).  m or more (a vertex) make every direction of u stiff: the folded sum loses nothing
             // there, while the Woodbury form would cancel (measured on the C4 dumps: 407 -> 85 optimal of 444).
             std::vector<int> st;
-            if (stiff_enabled() && ag.T->j_max > 0 && n <= 8 && m >= 2 && m <= 4) {   // the kernel's QPCfg::STF
+            // candidate nodes only (the kernel's assemble): some D_f above STIFF_RATIO x the largest diagonal of the
+            // node's own R (Rhat = R + Bt'P Bt >= R, so no other node can have a stiff facet); the kernel folds the
+            // other nodes' facets into R before phase 2, the twin here -- the same sum in another rounding order
+            double rdm = 0.0, dfm = 0.0;
+            for (int j = 0; j < m; ++j) rdm = std::max(rdm, std::fabs(Rm(j, j)));
+            for (int f = 0; f < nf; ++f) dfm = std::max(dfm, Df[f]);
+            if (stiff_enabled() && ag.T->j_max > 0 && n <= 8 && m >= 2 && m <= 4 && dfm > STIFF_RATIO * rdm) {
                 for (int f = 0; f < nf; ++f)
                     if (Df[f] > STIFF_RATIO * dmax) st.push_back(f);
                 bool opp = false;
