@@ -1001,6 +1001,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             // ---- phase 3: Rh = L D L' in registers (every lane); [K | kappa] = -Rh^-1 [Sh | W2]
             {
                 const bool fx = last && T.fix_last_input;
+                // the phase body is compiled twice for the stiff-facet classes: CAND for a candidate node (the facet
+                // branch, the stage system) and the plain body for every other stage (the straight-line code of the
+                // classes without facets), one scalar branch between them
+                auto ph3 = [&](auto candc) __attribute__((always_inline)) {
+                constexpr bool CAND = decltype(candc)::value;
                 constexpr int PM = C::PM, PMA = C::PMA;
                 double Lm[NU * NU], dinv[NU];
 #pragma unroll
@@ -1016,11 +1021,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                 for (int i = 0; i < PMA; ++i) { sfi[i] = -1; sfd[i] = 1.0; }
                 bool stg = false;   // this stage keeps a stiff facet (uniform: a scalar branch)
-                if constexpr (C::STF) {
+                if constexpr (C::STF && CAND) {
                     constexpr int NTR = C::NTR, FS = C::F_RING + C::P_FD + NTR;
-                    // only a candidate node (assemble: its facets left out of R, dfm > 0) takes the facet branch; every
-                    // lane reads the same packet word, and readfirstlane makes the branches scalar (not predicated)
-                    if (__builtin_amdgcn_readfirstlane((int)(dfmr > 0.0))) {
+                    // a candidate node (assemble: its facets left out of R, dfm > 0); every lane reads the same packet
+                    // words, and readfirstlane makes the branches scalar (not predicated)
+                    {
                     double dnf = 0.0;
 #pragma unroll
                     for (int j = 0; j < NU; ++j) dnf = fmax(dnf, fabs(Lm[j * NU + j]));
@@ -1064,7 +1069,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                             sfi[i] = use ? sfi[i] : -1;
                             sfd[i] = use ? sfd[i] : 1.0;
                         }
-                        if (use) {
+                        if (use) {   // Rhat + the non-stiff facets, one at a time (the twin's order)
 #pragma unroll
                             for (int e = 0; e < NU * NU; ++e) Lm[e] = lds[C::F_RH + e];
 #pragma unroll
@@ -1141,7 +1146,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 for (int e = 0; e < NU * PMA; ++e) Wm[e] = 0.0;
 #pragma unroll
                 for (int e = 0; e < PMA * PMA; ++e) Ci[e] = (e / PMA == e % PMA) ? 1.0 : 0.0;
-                if (C::STF && stg) {
+                if (C::STF && CAND && stg) {
 #pragma unroll
                     for (int i = 0; i < PM; ++i) {
                         double w[NU];
@@ -1196,7 +1201,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                         double gx[PMA], zc[PMA];
 #pragma unroll
                         for (int i = 0; i < PMA; ++i) zc[i] = 0.0;
-                        if (stg) {
+                        if (CAND && stg) {
 #pragma unroll
                         for (int i = 0; i < PM; ++i) {
                             double v = 0.0;
@@ -1247,6 +1252,13 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                     for (int e = 0; e < PM; ++e) v = (sl == NU * PM + PM * PM + e) ? (double)sfi[e] : v;
                     wb.st((sl < C::NSMB ? C::B_WS + sl : C::B_JNK) * 8, fbo, v);
+                }
+                };
+                if constexpr (C::STF) {
+                    if (__builtin_amdgcn_readfirstlane((int)(dfmr > 0.0))) ph3(std::true_type{});
+                    else ph3(std::false_type{});
+                } else {
+                    ph3(std::false_type{});
                 }
             }
             wsync();

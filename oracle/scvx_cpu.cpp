@@ -1394,6 +1394,81 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out, const double*
                 }
             }
             if (!newton(rco, rcq, dz, ds, dl, dsq, dlq, dy, dyi, dyf)) { status = fail_status; break; }
+            // experiment knob SCVX_TWIN_REFINE=k: k steps of iterative refinement of the corrector direction on the
+            // linearised KKT system (its dual and dynamics residuals at the full-step point; the row and
+            // complementarity equations hold by construction), each a re-solve with the same factorisation
+            static const int refine = std::getenv("SCVX_TWIN_REFINE") ? std::atoi(std::getenv("SCVX_TWIN_REFINE")) : 0;
+            bool ref_ok = true;
+            for (int rr = 0; rr < refine && ref_ok; ++rr) {
+                auto zt = [&](int t, int j) { return ag.nd[t].z[j] + dz[t][j]; };
+                std::vector<Vec> rdt(K), rpt(K - 1, Vec(n)), zero_c(K), zero_q(K), rc_save(K), rcs_save(K), rd_save(K);
+                Vec rpit(n), rpft(n, 0.0);
+                for (int i = 0; i < n; ++i) rpit[i] = zt(0, i) - ag.x_init[i];
+                if (T->has_final)
+                    for (int i = 0; i < n; ++i) rpft[i] = zt(K - 1, i) - ag.x_final[i];
+                for (int t = 0; t < K - 1; ++t)
+                    for (int i = 0; i < n; ++i) {
+                        double v = zt(t + 1, i) - ag.c[t][i];
+                        for (int k = 0; k < n; ++k) v -= ag.A[t](i, k) * zt(t, k);
+                        for (int j = 0; j < m; ++j) v -= ag.B[t](i, j) * zt(t, n + j) + ag.C[t](i, j) * zt(t + 1, n + j);
+                        if (ag.nd[t].nnu) v -= zt(t, n + m + i);
+                        rpt[t][i] = v;
+                    }
+                double emax = 0.0;
+                for (int t = 0; t < K; ++t) {
+                    Node& N = ag.nd[t];
+                    Vec& r = rdt[t];
+                    r.assign(N.nv, 0.0);
+                    for (int j = 0; j < N.nv; ++j) r[j] = N.pdiag[j] * zt(t, j) + N.q[j];
+                    for (int q = 0; q < N.nr; ++q)
+                        for (int j = 0; j < N.nv; ++j) r[j] += N.G(q, j) * (N.lam[q] + dl[t][q]);
+                    if (N.soc)
+                        for (int j = 0; j < m; ++j) r[n + j] -= N.lsoc[1 + j] + dlq[t][1 + j];
+                    if (t == 0)
+                        for (int i = 0; i < n; ++i) r[i] += ag.y_init[i] + dyi[i];
+                    if (t == K - 1 && T->has_final)
+                        for (int i = 0; i < n; ++i) r[i] += ag.y_fin[i] + dyf[i];
+                    if (t >= 1) {
+                        const size_t o = (size_t)(t - 1) * n;
+                        for (int i = 0; i < n; ++i) r[i] += ag.y[o + i] + dy[o + i];
+                        for (int j = 0; j < m; ++j)
+                            for (int i = 0; i < n; ++i) r[n + j] -= ag.C[t - 1](i, j) * (ag.y[o + i] + dy[o + i]);
+                    }
+                    if (t < K - 1) {
+                        const size_t o = (size_t)t * n;
+                        for (int k = 0; k < n; ++k)
+                            for (int i = 0; i < n; ++i) r[k] -= ag.A[t](i, k) * (ag.y[o + i] + dy[o + i]);
+                        for (int j = 0; j < m; ++j)
+                            for (int i = 0; i < n; ++i) r[n + j] -= ag.B[t](i, j) * (ag.y[o + i] + dy[o + i]);
+                        for (int i = 0; i < N.nnu; ++i) r[n + m + i] -= ag.y[o + i] + dy[o + i];
+                    }
+                    if (N.fixed_u)
+                        for (int j = 0; j < m; ++j) r[n + j] = 0.0;
+                    for (double v : r) emax = std::max(emax, std::fabs(v));
+                    zero_c[t].assign(N.nr, 0.0);
+                    zero_q[t].assign(N.soc ? m + 1 : 0, 0.0);
+                    rd_save[t] = L[t].rd; rc_save[t] = L[t].rc; rcs_save[t] = L[t].rcs;
+                    L[t].rd = r;
+                    std::fill(L[t].rc.begin(), L[t].rc.end(), 0.0);
+                    std::fill(L[t].rcs.begin(), L[t].rcs.end(), 0.0);
+                }
+                if (std::getenv("SCVX_DEBUG")) std::fprintf(stderr, "   refine %d: dual residual of the direction %.3e\n", rr, emax);
+                std::swap(rp, rpt); std::swap(rpi, rpit); std::swap(rpf, rpft);
+                std::vector<Vec> dz2, ds2, dl2, dsq2, dlq2;
+                Vec dy2, dyi2, dyf2;
+                ref_ok = newton(zero_c, zero_q, dz2, ds2, dl2, dsq2, dlq2, dy2, dyi2, dyf2);
+                std::swap(rp, rpt); std::swap(rpi, rpit); std::swap(rpf, rpft);
+                for (int t = 0; t < K; ++t) { L[t].rd = rd_save[t]; L[t].rc = rc_save[t]; L[t].rcs = rcs_save[t]; }
+                if (!ref_ok) break;
+                for (int t = 0; t < K; ++t) {
+                    for (size_t j = 0; j < dz[t].size(); ++j) dz[t][j] += dz2[t][j];
+                    for (size_t j = 0; j < ds[t].size(); ++j) { ds[t][j] += ds2[t][j]; dl[t][j] += dl2[t][j]; }
+                    for (size_t j = 0; j < dsq[t].size(); ++j) { dsq[t][j] += dsq2[t][j]; dlq[t][j] += dlq2[t][j]; }
+                }
+                for (size_t i = 0; i < dy.size(); ++i) dy[i] += dy2[i];
+                for (int i = 0; i < n; ++i) { dyi[i] += dyi2[i]; dyf[i] += dyf2[i]; }
+            }
+            if (!ref_ok) { status = fail_status; break; }
             // step fraction (kernel: the same rule, QP_TAU_END): 0.99 of the way to the boundary, 1 - 1e-5 once
             // the affine predictor takes a (nearly) full step -- the end game, where the fraction alone caps
             // the gap reduction per iteration at 1 / (1 - fraction).  SCVX_TAU_END: experiment knob
