@@ -11,13 +11,13 @@ qp_ipm.hpp, Riccati::stiff in oracle/scvx_cpu.cpp): 444 -> 25-62 status-1 solves
 
 Checked at step 18 (tr = 2^-4 x 0.25) of the loop, on the step's own inputs (discretisation, culled rows):
   * no solve fails (status 2) and >= 98 % end at the full tolerance (status 0) at every step (measured round 5:
-    98.5 % at the worst step, >= 99.4 % at every other; round 4, before the stiff-facet stage system: 89 %);
+    98.4-98.6 % at the worst step, >= 99.3 % at every other; round 4, before the stiff-facet stage system: 89 %);
   * status-1 solves against the dense reference-form oracle (oracle/qp_dense.py, dist_scvx_3d.py:51-111 as
     written): optimal value within 1e-7 relative, violation < 1e-5 (Clarabel's reduced feasibility, as
     tests/test_coupled_gpu.py); status-0 solves: value 1e-7, violation 1e-7;
-  * the warm-started solve equals the cold solve of the same subproblem in value: 2e-8 relative where both
-    end optimal (both within the 1e-8 gap test), 5e-5 where either ends at the reduced tolerances (measured
-    3.5e-6 at most)."""
+  * the warm-started solve equals the cold solve of the same subproblem in value where both end optimal: 2e-8
+    relative for 99 % of them (both within the 1e-8 gap test), 1e-6 for every one (the primal residual priced
+    by the slack multipliers); 5e-5 where either ends at the reduced tolerances (measured 5.1e-6 at most)."""
 import numpy as np
 import pytest
 
@@ -70,10 +70,11 @@ def test_c4_late_steps_match_dense_oracle(cuda):
     ow, oc = out["obj"].cpu().numpy(), cold["obj"].cpu().numpy()
     # both optimal: the stopping rule bounds the gap by 1e-8 relative, but the objective also moves by the primal
     # residual (<= 1e-8 pnorm) times the multipliers, which reach the slack weights here (w_coll = 1e4 on the
-    # objective's 1e6 scale): a few 1e-6 relative (measured round 4: 3 of 3964 agents above 2e-8, max 4.4e-6,
-    # profiles/round4_r4n_pytest_gpu.log); a status-1 end on either side certifies only the reduced gap (5e-5)
+    # objective's 1e6 scale) (measured round 4, before the stiff-facet stage system: 3 of 3964 agents above 2e-8,
+    # max 4.4e-6, profiles/round4_r4n_pytest_gpu.log; round 5: max 5.7e-8 to 1.9e-7 over the builds of the round,
+    # profiles/round5_r5o_pytest.log); a status-1 end on either side certifies only the reduced gap (5e-5)
     both = (st == 0) & (stc == 0)
-    np.testing.assert_allclose(ow[both], oc[both], rtol=2e-5, atol=2e-8)
+    np.testing.assert_allclose(ow[both], oc[both], rtol=1e-6, atol=2e-8)
     assert np.mean(np.abs(ow[both] - oc[both]) <= 2e-8 * np.maximum(1.0, np.abs(oc[both]))) >= 0.99
     np.testing.assert_allclose(ow[~both], oc[~both], rtol=5e-5, atol=1e-8)
     print("warm vs cold: both optimal", int(both.sum()), "max rel diff there",
