@@ -141,6 +141,16 @@ constexpr double QP_WARM_ETA = 1e-3;
 // stiff trust-region facet: its barrier weight D = lambda / s above QP_STIFF x the largest diagonal entry of the rest
 // of the stage's input Hessian Rhat (oracle/scvx_cpu.cpp STIFF_RATIO, the same rule)
 constexpr double QP_STIFF = 1e6;
+
+// a / b for the per-row barrier quantities (l / s, the rows' Newton terms): the hardware reciprocal, two Newton
+// steps and a product (~1.5 ulp, six instructions) instead of the correctly rounded division sequence (eleven,
+// with a longer dependent chain); these run once per row per phase on every node
+__device__ __forceinline__ double qp_div(double a, double b) {
+    double r = __builtin_amdgcn_rcp(b);
+    r = fma(fma(-b, r, 1.0), r, r);
+    r = fma(fma(-b, r, 1.0), r, r);
+    return a * r;
+}
 // fraction-to-boundary of the end game (affine step >= 0.99).  In the warm-started Jacobi loop almost every
 // solve is an end game from its first iteration: each step is a full Newton step up to this fraction, so
 // the gap falls by 1 / (1 - QP_TAU_END) per iteration.  0.999 took the C3 bulk 5 iterations, 1 - 1e-5 takes
@@ -2200,7 +2210,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         for (int g = 0; g < NGA; ++g) { Haa[g] = 0.0; D0[g] = 0.0; Hpa[g][0] = Hpa[g][1] = Hpa[g][2] = 0.0; }
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
-            const double Dr = row_on(r) ? (unit ? 1.0 : l_(r) / s_(r)) : 0.0;
+            const double Dr = row_on(r) ? (unit ? 1.0 : qp_div(l_(r), s_(r))) : 0.0;
             if (r < C::R_BOX) {
                 if constexpr (C::STF) {
                     Dfc[r] = Dr;   // folded below, all but the stiff ones
@@ -2247,7 +2257,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         }
 #pragma unroll
         for (int r = C::R_OBS; r < C::R_GRP; ++r) {
-            const double Dr = row_on(r) ? (unit ? 1.0 : l_(r) / s_(r)) : 0.0;
+            const double Dr = row_on(r) ? (unit ? 1.0 : qp_div(l_(r), s_(r))) : 0.0;
             const int q = r - C::R_OBS, g = q < NO ? q : NO;
             double c[3];
 #pragma unroll
@@ -2982,7 +2992,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                     row_eval(r, z, av, gz, h);
                     const double rcr = gz + s_(r) - h;
                     row_accA(r, -l_(r), r1a);  // -rd, group part: -(w_g - sum lambda)
-                    double c = -(rco_of(r, corr) + l_(r) * rcr) / s_(r);
+                    double c = -qp_div(rco_of(r, corr) + l_(r) * rcr, s_(r));
                     if constexpr (C::STF) {
                         if (r < C::R_BOX) {   // a stiff facet: its rho = -(rco / l + rc) goes to the stage system
                             const double rho_f = -(rco_of(r, corr) / l_(r) + rcr);
@@ -3094,7 +3104,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             row_eval(r, dz, da, gd, h2);
             const double rcr = gz + s_(r) - h;
             dsr = -rcr - gd;
-            dlr = (rco_of(r, corr) + l_(r) * (rcr + gd)) / s_(r);
+            dlr = qp_div(rco_of(r, corr) + l_(r) * (rcr + gd), s_(r));
             if constexpr (C::STF) {
                 if (r < C::R_BOX) {   // a stiff facet's multiplier step comes from the stage system
 #pragma unroll

@@ -51,8 +51,9 @@ def test_dist_scvx_3d_first_iteration_matches_dense_oracle(cuda):
         U = out["U"][i].cpu().numpy()
         S = out["slack_coll"][i].cpu().numpy()
         viol = qd.constraint_violation(prob, X, U, S)
-        # Clarabel's primal test is relative: tol (1e-9) x (||b|| + ||x|| + ||s||), positions here reach ~20
-        assert max(viol.values()) < 5e-8, viol
+        # Clarabel's primal test is relative: tol (1e-9) x (||b|| + ||x|| + ||s||), positions and the box bounds
+        # here reach ~22 and the box slacks ~44: up to ~1e-7 (measured 5.6e-8 on the terminal state)
+        assert max(viol.values()) < 1e-7, viol
         obj = out["obj"][i].item()
         assert abs(obj - objd) <= 1e-8 * max(1.0, abs(objd))
         if objd < 1e3:  # slack-free agents: the quadratic part pins the trajectory
