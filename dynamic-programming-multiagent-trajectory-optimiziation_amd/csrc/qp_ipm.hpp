@@ -2242,7 +2242,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         double hp[NGA][3];
 #pragma unroll
         for (int g = 0; g < NGA; ++g) {
-            const double ih = (g < NG && grp_on(g)) ? 1.0 / Haa[g] : 0.0;
+            const double ih = (g < NG && grp_on(g)) ? qp_div(1.0, Haa[g]) : 0.0;
 #pragma unroll
             for (int i = 0; i < 3; ++i) hp[g][i] = Hpa[g][i] * ih;
             if (g < NG) {
@@ -2272,8 +2272,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         // (D = l/s of the rows nu - e <= 0, -nu - e <= 0; 2 at unit scaling); 1 at the last node (no nu)
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
-            const double d1 = unit ? 1.0 : vl[2 * i] / vs[2 * i], d2 = unit ? 1.0 : vl[2 * i + 1] / vs[2 * i + 1];
-            pst(C::gD + i, vact ? 4.0 * d1 * d2 / (d1 + d2) : 1.0);
+            const double d1 = unit ? 1.0 : qp_div(vl[2 * i], vs[2 * i]), d2 = unit ? 1.0 : qp_div(vl[2 * i + 1], vs[2 * i + 1]);
+            pst(C::gD + i, vact ? qp_div(4.0 * d1 * d2, d1 + d2) : 1.0);
         }
         double Q[NX * NX], Cp[NX * NU];
         load_cp(Cp);
@@ -2957,9 +2957,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             const double g1 = dnv[i] - dne[i], g2 = -dnv[i] - dne[i];
             const double rc1 = vn[i] - ve[i] + vs[2 * i], rc2 = -vn[i] - ve[i] + vs[2 * i + 1];
             dsr[0] = -rc1 - g1;
-            dlr[0] = (vrco(2 * i, corr) + vl[2 * i] * (rc1 + g1)) / vs[2 * i];
+            dlr[0] = qp_div(vrco(2 * i, corr) + vl[2 * i] * (rc1 + g1), vs[2 * i]);
             dsr[1] = -rc2 - g2;
-            dlr[1] = (vrco(2 * i + 1, corr) + vl[2 * i + 1] * (rc2 + g2)) / vs[2 * i + 1];
+            dlr[1] = qp_div(vrco(2 * i + 1, corr) + vl[2 * i + 1] * (rc2 + g2), vs[2 * i + 1]);
         };
         // Newton direction for the complementarity rhs (rows: rco_of, SOC: rcq2); directions out
         auto newton = [&](bool corr, const double* rcq2) __attribute__((always_inline)) {
@@ -3044,11 +3044,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                 for (int i = 0; i < NV; ++i) {
                     const double rc1 = vn[i] - ve[i] + vs[2 * i], rc2 = -vn[i] - ve[i] + vs[2 * i + 1];
-                    const double c1 = -(vrco(2 * i, corr) + vl[2 * i] * rc1) / vs[2 * i];
-                    const double c2 = -(vrco(2 * i + 1, corr) + vl[2 * i + 1] * rc2) / vs[2 * i + 1];
+                    const double c1 = -qp_div(vrco(2 * i, corr) + vl[2 * i] * rc1, vs[2 * i]);
+                    const double c2 = -qp_div(vrco(2 * i + 1, corr) + vl[2 * i + 1] * rc2, vs[2 * i + 1]);
                     const double rn = -vrd[2 * i] + c1 - c2, re = -vrd[2 * i + 1] - c1 - c2;
-                    const double d1 = vl[2 * i] / vs[2 * i], d2 = vl[2 * i + 1] / vs[2 * i + 1];
-                    dvl[i] = vact ? -(rn - (d2 - d1) / (d1 + d2) * re) : 0.0;
+                    const double d1 = qp_div(vl[2 * i], vs[2 * i]), d2 = qp_div(vl[2 * i + 1], vs[2 * i + 1]);
+                    dvl[i] = vact ? -(rn - qp_div(d2 - d1, d1 + d2) * re) : 0.0;
                     cst(C::C_VRE + i, re);
                 }
             }
@@ -3073,8 +3073,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 if (corr) hold(vcpv, 2 * NV);
 #pragma unroll
                 for (int i = 0; i < NV; ++i) {
-                    const double d1 = vl[2 * i] / vs[2 * i], d2 = vl[2 * i + 1] / vs[2 * i + 1];
-                    dne[i] = vact ? (vre[i] - (d2 - d1) * dnv[i]) / (d1 + d2) : 0.0;
+                    const double d1 = qp_div(vl[2 * i], vs[2 * i]), d2 = qp_div(vl[2 * i + 1], vs[2 * i + 1]);
+                    dne[i] = vact ? qp_div(vre[i] - (d2 - d1) * dnv[i], d1 + d2) : 0.0;
                     dnv[i] = vact ? dnv[i] : 0.0;
                 }
 #pragma unroll
