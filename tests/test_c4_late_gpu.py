@@ -71,7 +71,7 @@ def test_c4_late_steps_match_dense_oracle(cuda):
     # both optimal: the stopping rule bounds the gap by 1e-8 relative, but the objective also moves by the primal
     # residual (<= 1e-8 pnorm) times the multipliers, which reach the slack weights here (w_coll = 1e4 on the
     # objective's 1e6 scale) (measured round 4, before the stiff-facet stage system: 3 of 3964 agents above 2e-8,
-    # max 4.4e-6, profiles/round4_r4n_pytest_gpu.log; round 5: max 5.7e-8 to 1.9e-7 over the builds of the round,
+    # max 4.4e-6, profiles/round4_r4n_pytest_gpu.log; round 5: max 5.7e-8 to 2.1e-7 over the builds of the round,
     # profiles/round5_r5o_pytest.log); a status-1 end on either side certifies only the reduced gap (5e-5)
     both = (st == 0) & (stc == 0)
     np.testing.assert_allclose(ow[both], oc[both], rtol=1e-6, atol=2e-8)
