@@ -2462,13 +2462,13 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
     };
     // NT scaling W = eta [[w0, w1'], [w1, I + w1 w1'/(1 + w0)]], W^-1 the same with -w1, 1/eta
     auto w_apply = [&](const double* w, double eta, bool inv, const double* x, double* yv) __attribute__((always_inline)) {
-        const double sgn = inv ? -1.0 : 1.0, sc = inv ? 1.0 / eta : eta;
+        const double sgn = inv ? -1.0 : 1.0, sc = inv ? qp_div(1.0, eta) : eta;
         double d = 0.0;
 #pragma unroll
         for (int j = 1; j < NQ; ++j) d += w[j] * x[j];
         d *= sgn;
         yv[0] = sc * (w[0] * x[0] + d);
-        const double f = x[0] + d / (1.0 + w[0]);
+        const double f = x[0] + qp_div(d, 1.0 + w[0]);
 #pragma unroll
         for (int j = 1; j < NQ; ++j) yv[j] = sc * (x[j] + sgn * w[j] * f);
     };
@@ -2900,11 +2900,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             const double ns = sqrt(Js), nz = sqrt(Jz);
             double sbv[NQ], zbv[NQ], dot = 0.0;
 #pragma unroll
-            for (int j = 0; j < NQ; ++j) { sbv[j] = sq[j] / ns; zbv[j] = lq[j] / nz; dot += sbv[j] * zbv[j]; }
+            for (int j = 0; j < NQ; ++j) { sbv[j] = qp_div(sq[j], ns); zbv[j] = qp_div(lq[j], nz); dot += sbv[j] * zbv[j]; }
             const double gam = sqrt((1.0 + dot) / 2.0);
 #pragma unroll
-            for (int j = 0; j < NQ; ++j) wv[j] = (sbv[j] + (j == 0 ? zbv[j] : -zbv[j])) / (2.0 * gam);
-            eta = sqrt(sqrt(Js / Jz));
+            for (int j = 0; j < NQ; ++j) wv[j] = qp_div(sbv[j] + (j == 0 ? zbv[j] : -zbv[j]), 2.0 * gam);
+            eta = sqrt(sqrt(qp_div(Js, Jz)));
             w_apply(wv, eta, false, lq, ltq);
             // (W^-2)_uu = rows/cols 1.. of W^-1 W^-1
             double Wi[NQ * NQ];
@@ -3016,10 +3016,10 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                 double J = ltq[0] * ltq[0], r0 = ltq[0] * rcq2[0], w2[NQ], w3[NQ];
 #pragma unroll
                 for (int j = 1; j < NQ; ++j) { J -= ltq[j] * ltq[j]; r0 -= ltq[j] * rcq2[j]; }
-                r0 /= J;
+                r0 = qp_div(r0, J);
                 rho[0] = r0;
 #pragma unroll
-                for (int j = 1; j < NQ; ++j) rho[j] = (rcq2[j] - r0 * ltq[j]) / ltq[0];
+                for (int j = 1; j < NQ; ++j) rho[j] = qp_div(rcq2[j] - r0 * ltq[j], ltq[0]);
                 w_apply(wv, eta, true, rcq, w2);
 #pragma unroll
                 for (int j = 0; j < NQ; ++j) w2[j] += rho[j];
