@@ -8,15 +8,21 @@ trust region 0.25 (:207), 8 static spherical obstacles as linearized soft halfsp
 
 One SCvx iteration (= one "step") = batched FOH discretization (scvx_foh_batched) + batched
 trust-region QP/SOCP solve to tolerance (scvx_qp_solve_batched) + trust-region bookkeeping, all
-on device; inputs resident in HBM.  Multi-GPU (--gpus N under torch.distributed.run): weak scaling,
-each rank owns its own 1024 agents (C3 has no inter-agent coupling, so there is no data-path
-collective); `value` counts the N_gpus * 1024-agent SCvx iterations completed per second.
+on device; inputs resident in HBM.  The headline `value` runs the reference's outer rule
+(dist_scvx_3d.py:248-252: one trust radius, halved when the summed cost rises); the same invocation
+then times this build's per-agent rule (each agent's radius halves on its own cost increase) from the
+same initial iterate, with its own warmup, reported under `other_rule` (`--rules one` skips it).
+Multi-GPU (--gpus N under torch.distributed.run): weak scaling, each rank owns its own 1024 agents; the
+only exchange is the global rule's summed cost (one scalar all_reduce per step, RCCL); `value` counts
+the N_gpus * 1024-agent SCvx iterations completed per second.
 
 Also reported: roofline of the dominant kernel (qp_ipm_kernel, FP64 FLOP rate vs the FP64 peak,
 timed with HIP events on the launch stream) and a CPU baseline (the C++ restatement of the same
-algorithm, oracle/scvx_cpu.cpp + oracle/foh_ref.c, on a bounded agent sample).
+algorithm, oracle/scvx_cpu.cpp + oracle/foh_ref.c, on a bounded agent sample, the headline's rule).
 
 Optional workloads (--config; the default c3 is the headline line the driver records):
+  c2  BASELINE.json configs[1]: N=128 double-integrator agents per GPU (seed 0, no
+      obstacles, no SOC, box |x|,|y| <= 12), both rules as c3.
   c4  N=4096 double-integrator agents in total on a 16^3 lattice (spacing 6 > 2R, R=2.3) with
       permuted goals, pairwise collision coupling (dist_scvx_3d.py:93-107, one shared slack per node,
       the j_max=8 nearest neighbours per node kept), global trust-region rule (:248-252).  Agents
@@ -109,10 +115,10 @@ def committed_traffic(kernel_prefix="scvx::qp_ipm_kernel<scvx::QPCfg<6, 3, 2, 8,
     return None, None
 
 
-def make_workload(N, seed, device):
+def make_workload(N, seed, device, obstacles=N_OBS):
     import torch
     from scvx_hip import workloads
-    sc = workloads.synthetic_di(N, K=K, seed=seed, sigma=SIGMA, obstacles=N_OBS)
+    sc = workloads.synthetic_di(N, K=K, seed=seed, sigma=SIGMA, obstacles=obstacles)
     t = {k: torch.tensor(sc[k], device=device) for k in ("X", "U", "x_init", "x_final", "sigma")}
     return sc, t
 
@@ -162,17 +168,23 @@ def host_info():
     return info
 
 
-def cpu_jacobi(sc, n_sample, threads, warmup, steps, tol=1e-8, max_seconds=30.0, warm_status=1, tr_rule="per_agent"):
+def cpu_jacobi(sc, n_sample, threads, warmup, steps, tol=1e-8, max_seconds=30.0, warm_status=1, tr_rule="per_agent",
+               soc=True):
     """The CPU restatement of the timed region, like for like: the same warm-started Jacobi loop as the GPU
     line (JacobiSCvx with the bench's settings) on the first n_sample agents -- per step the FOH
     (oracle/foh_ref.c), the QP twin (oracle/scvx_cpu.cpp, the kernel's algorithm, started from the previous
     step's primal-dual point exactly as the kernel's warm rule: warm = last status <= warm_status) and the per-agent
     trust-region bookkeeping of csrc/jacobi.hip (tie margin 1e-9; tr_rule "global": the reference's one radius, halved
-    when the summed cost rises, JacobiSCvx's global rule).  `warmup` untimed steps, then up to `steps`
+    when the summed cost rises, JacobiSCvx's global rule -- summed over the n_sample agents simulated here: with
+    n_sample = N on one GPU that is the GPU line's own sum; at --gpus > 1 the GPU line all-reduces the sum over every
+    rank's agents, so there the CPU leg's halving decisions are a one-rank approximation).  `warmup` untimed steps,
+    then up to `steps`
     timed steps (fewer if max_seconds runs out first).  Returns (SCvx iterations/s scaled to the N=1024-agent
     workload, timed steps, seconds, mean IPM iterations per agent over the timed steps)."""
     from oracle import foh_oracle, qp_cpu
-    tpl = qp_cpu.make_template(6, 3, K, box=BOX, obs=sc["obs"], w_obs=1e6, u_max=U_MAX, tol=tol, max_iter=60)
+    n_agents = sc["X"].shape[0]   # the GPU line's agents per GPU: the rate is scaled to that workload
+    tpl = qp_cpu.make_template(6, 3, K, box=BOX, obs=sc["obs"], w_obs=1e6, u_max=U_MAX if soc else None, tol=tol,
+                               max_iter=60)
     n = n_sample
     X, U = sc["X"][:n].copy(), sc["U"][:n].copy()
     sig, xi, xf = sc["sigma"][:n], sc["x_init"][:n], sc["x_final"][:n]
@@ -206,10 +218,10 @@ def cpu_jacobi(sc, n_sample, threads, warmup, steps, tol=1e-8, max_seconds=30.0,
             it_sum += int(o["iters"].sum())
             if t_el >= max_seconds:
                 break
-    return timed * (n / N_AGENTS) / t_el, timed, t_el, it_sum / (timed * n)
+    return timed * (n / n_agents) / t_el, timed, t_el, it_sum / (timed * n)
 
 
-def cpu_baselines(sc, n_sample, tol, warmup, steps, warm_status=1, tr_rule="per_agent"):
+def cpu_baselines(sc, n_sample, tol, warmup, steps, warm_status=1, tr_rule="per_agent", obstacles=True, soc=True):
     """All-core and single-core CPU figures of the restatement on the GPU line's own loop (cpu_jacobi).  "All
     cores" is every CPU this process may run on: nproc, capped by the cgroup CPU quota when one is set (the GPU
     box grants 16 CPUs of a 256-thread host; more OpenMP threads than that only time-slice)."""
@@ -217,12 +229,16 @@ def cpu_baselines(sc, n_sample, tol, warmup, steps, warm_status=1, tr_rule="per_
     quota = info.get("cgroup_cpu_quota")
     threads = max(1, min(info["nproc"], int(quota))) if quota else info["nproc"]
     v_all, steps_all, el, it_all = cpu_jacobi(sc, n_sample, threads, warmup, steps, tol=tol, warm_status=warm_status,
-                                              tr_rule=tr_rule)
+                                              tr_rule=tr_rule, soc=soc)
     n1 = min(n_sample, 64)
-    v_one, steps1, el1, it1 = cpu_jacobi(sc, n1, 1, warmup, steps, tol=tol, warm_status=warm_status, tr_rule=tr_rule)
-    return dict(value=v_all, unit="SCvx-iterations/s (N=1024-agent equivalent)", cores=threads, kind="port",
+    v_one, steps1, el1, it1 = cpu_jacobi(sc, n1, 1, warmup, steps, tol=tol, warm_status=warm_status, tr_rule=tr_rule,
+                                         soc=soc)
+    N_ = sc["X"].shape[0]
+    return dict(value=v_all, unit=f"SCvx-iterations/s (N={N_}-agent equivalent)", cores=threads, kind="port",
+                tr_rule=tr_rule,
                 sample=f"warm-started steady state, steps {warmup + 1}-{warmup + steps_all} of the GPU line's Jacobi "
-                       f"loop ({warmup} untimed warm-up steps first) on {n_sample} of the {N_AGENTS} agents: FOH C + "
+                       f"loop ({warmup} untimed warm-up steps first, {tr_rule} trust-region rule) on {n_sample} of the "
+                       f"{N_} agents: FOH C + "
                        f"the kernel's IPM in C++ with the same warm start and trust-region bookkeeping, -O3 x86-64-v3, "
                        f"OpenMP over agents on {threads} threads = the CPUs this process may use (nproc "
                        f"{info['nproc']}, cgroup quota {quota}); {el:.1f} s timed",
@@ -545,13 +561,120 @@ def dry_run(args, world, rank):
         dist.destroy_process_group()
 
 
+def timed_leg(drv, w, args, world, device):
+    """Warmup + exactly args.steps timed SCvx iterations of `drv` from the initial iterate w (X, U), bracketed by a
+    barrier + torch.cuda.synchronize() on both sides; the elapsed time is the max over ranks.  Every stage of a timed
+    step is bracketed by HIP events on the launch stream (the QP kernel's mark pair gives its launch duration)."""
+    import torch
+    import torch.distributed as dist
+    it_state = [w["X"].clone(), w["U"].clone()]   # the current iterate (X, U), rebound every step
+
+    def step(marks=None):
+        it_state[0], it_state[1], out = drv.step(it_state[0], it_state[1], marks=marks)
+        return out
+
+    status_ids = torch.arange(3, device=device, dtype=torch.int32)
+
+    def record(out, iters, iters_max, stats):
+        """Per-step device-side bookkeeping of the timed region (no host sync): summed and max IPM iterations,
+        status counts.  The warmup runs it too, so no torch kernel is loaded for the first time inside the
+        timed region (a first use costs ~40-180 ms of module loading on a fresh box)."""
+        iters.append(out["iters"].sum())
+        iters_max.append(out["iters"].max())
+        stats.append((out["status"][:, None] == status_ids).sum(dim=0))   # no sync (bincount would sync)
+
+    for _ in range(args.warmup):
+        out = step()
+        record(out, [], [], [])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    marks, iters, iters_max, checks, stats = [], [], [], [], []
+    t0 = time.perf_counter()
+    host_ms = []
+    for _ in range(args.steps):
+        mk = []
+        th = time.perf_counter()
+        out = step(mk)
+        host_ms.append(1e3 * (time.perf_counter() - th))
+        marks.append(mk)
+        record(out, iters, iters_max, stats)
+        if drv.last_check is not None:
+            checks.append(dict(drv.last_check))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    el_t = torch.tensor([el], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    st_ms, step_ms = stage_times(marks)
+    if world > 1:   # every rank's stage medians (the all-gather time per rank for c4/c5)
+        mine = torch.tensor([st_ms.get(k, 0.0) for k in ("foh", "gather", "rows", "qp", "check", "update")],
+                            dtype=torch.float64, device=device)
+        allr = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = [r.tolist() for r in allr]
+    else:
+        per_rank = None
+    status = out["status"].cpu()
+    its = out["iters"].cpu().numpy()
+    N = its.size
+    return dict(
+        el=el_t.item(), st_ms=st_ms, step_ms=step_ms, per_rank=per_rank, host_ms=host_ms, checks=checks,
+        ipm_iters=float(torch.stack(iters).sum().item()),
+        fields={
+            "ms_per_step_median": float(np.median(step_ms)),
+            "stage_ms_median": st_ms,
+            "stage_ms_per_rank": per_rank,
+            "ipm_iters_per_agent": float(torch.stack(iters).sum().item()) / (args.steps * N),
+            "ipm_iters_max_last": int(its.max()),
+            "ipm_iters_hist_last": {str(int(v)): int(c) for v, c in zip(*np.unique(its, return_counts=True))},
+            "status_counts": {str(k): int((status == k).sum()) for k in (0, 1, 2)},
+            "status_counts_per_step": [[int(v) for v in c.tolist()[:3]] for c in stats],
+            "step_ms": [round(v, 4) for v in step_ms],
+            "host_ms_per_step": [round(v, 4) for v in host_ms],
+            "gap_ms_between_steps": [round(a[-1][1].elapsed_time(b[0][1]), 4) for a, b in zip(marks[:-1], marks[1:])],
+            "ipm_iters_max_per_step": [int(v) for v in torch.stack(iters_max).tolist()],
+            "min_frac_status_0_1": min(float((c[0] + c[1]).item()) / N for c in stats),
+            "coupling_check": checks or None,
+        })
+
+
+def leg_roofline(res, args, n, m, K_, N, rows, j_max, model, nsub):
+    """Roofline of the dominant kernel (qp_ipm_kernel, FP64 FLOPs of SURVEY §8(d) x executed IPM iterations over
+    its HIP-event launch time) and of the whole step (t_min / t) for one timed leg."""
+    qp_ms = res["st_ms"]["qp"]
+    qp_flops = qp_flops_per_ipm_iter(n, m, K_, rows) * res["ipm_iters"] / args.steps          # per launch
+    qp_bytes = qp_bytes_per_agent(n, m, K_, j_max) * N
+    foh_bytes = foh_bytes_per_agent(n, m, K_) * N
+    foh_flops = foh_flops_per_agent(n, m, K_, nsub=nsub) * N
+    achieved = qp_flops / (qp_ms * 1e-3) / 1e12
+    qp_gbs = qp_bytes / (qp_ms * 1e-3) / 1e9
+    t_step = res["el"] / args.steps
+    t_min = (max(foh_bytes / (HBM_PEAK_GBS * 1e9), foh_flops / (FP64_PEAK_TFLOPS * 1e12))
+             + max(qp_bytes / (HBM_PEAK_GBS * 1e9), qp_flops / (FP64_PEAK_TFLOPS * 1e12)))
+    roof = {"bound": "fp64_valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved / FP64_PEAK_TFLOPS, "kernel": "qp_ipm_kernel", "kernel_ms": qp_ms,
+            "algorithmic_flops_per_launch": qp_flops, "algorithmic_bytes_per_launch": qp_bytes,
+            "hbm_achieved_gbs": qp_gbs, "hbm_frac": qp_gbs / HBM_PEAK_GBS}
+    step_roof = {"hbm_frac": (foh_bytes + qp_bytes) / (t_step * HBM_PEAK_GBS * 1e9),
+                 "fp64_frac": (foh_flops + qp_flops) / (t_step * FP64_PEAK_TFLOPS * 1e12),
+                 "t_min_ms": 1e3 * t_min, "t_min_over_t": t_min / t_step,
+                 "algorithmic_bytes_per_step": foh_bytes + qp_bytes,
+                 "algorithmic_flops_per_step": foh_flops + qp_flops}
+    return roof, step_roof
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", choices=("c3", "c4", "c5", "is", "scp", "nash"), default="c3")
-    ap.add_argument("--agents", type=int, default=N_AGENTS, help="c3: agents per GPU")
+    ap.add_argument("--config", choices=("c2", "c3", "c4", "c5", "is", "scp", "nash"), default="c3")
+    ap.add_argument("--agents", type=int, default=None, help="c2 / c3: agents per GPU (default 128 / 1024)")
     ap.add_argument("--cpu-sample", type=int, default=1024)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--balance", action="store_true",
@@ -560,13 +683,18 @@ def main():
                     help="IPM relative stopping tolerance; default = Clarabel's defaults (tol_feas = tol_gap_rel = "
                          "1e-8), the solver of the reference's dist_scvx_3d.py:110")
     ap.add_argument("--dry-run", action="store_true", help="launcher/rendezvous check on CPU, no GPU work")
-    ap.add_argument("--tensor-update", action="store_true", help="c3: bookkeeping as tensor ops (not csrc/jacobi.hip)")
-    ap.add_argument("--tr-rule", default="per_agent", choices=("per_agent", "global"),
-                    help="c3 trust-region rule: per_agent (each agent's radius halves on its own cost increase, the "
-                         "headline) or global (the reference's one radius, halved when the summed cost rises: "
-                         "Distributed_opt/dist_scvx_3d.py:248-252)")
+    ap.add_argument("--tensor-update", action="store_true", help="c2/c3 per-agent rule: bookkeeping as tensor ops "
+                                                                  "(not csrc/jacobi.hip)")
+    ap.add_argument("--tr-rule", default="global", choices=("per_agent", "global"),
+                    help="c2/c3 trust-region rule of the headline `value`: global (the reference's one radius, halved "
+                         "when the summed cost rises: Distributed_opt/dist_scvx_3d.py:248-252; at --gpus > 1 the sum "
+                         "is all-reduced over every rank's agents) or per_agent (each agent's radius halves on its "
+                         "own cost increase: this build's extension for independent agents)")
+    ap.add_argument("--rules", default="both", choices=("both", "one"),
+                    help="c2/c3: both -- also time the other trust-region rule in the same invocation (its own "
+                         "warmup and timed steps, reported under `other_rule`); one -- only --tr-rule")
     ap.add_argument("--tie-rtol", type=float, default=1e-9,
-                    help="c3 per-agent trust-region rule: relative margin of the cost-increase test (JacobiSCvx.tie_rtol)")
+                    help="per-agent trust-region rule: relative margin of the cost-increase test (JacobiSCvx.tie_rtol)")
     ap.add_argument("--dispatch-order", default="lpt", choices=("lpt", "none"),
                     help="QP dispatch order of the Jacobi loop (JacobiSCvx.dispatch_order): lpt deals the agents "
                          "longest-first by their previous solve's IPM iterations where they outnumber the resident "
@@ -576,6 +704,8 @@ def main():
                          "(1: optimal_inaccurate iterates too -- they meet the reduced tolerances; C4 80 -> 85 "
                          "SCvx-it/s, no status change; C3 / C5 end every solve optimal, so it does not apply there)")
     args = ap.parse_args()
+    if args.agents is None:
+        args.agents = 128 if args.config == "c2" else N_AGENTS
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
@@ -602,24 +732,37 @@ def main():
         return bench_scproblem(args, world, rank, device)
     if args.config == "nash":
         return bench_nash(args, world, rank, device)
-    if args.config == "c3":
+    independent = args.config in ("c2", "c3")
+    if independent:
+        # C2 / C3: independent agents, weak scaling (each rank owns its own N agents; the global rule's
+        # summed cost is the only exchange, one scalar all_reduce per step)
         N = args.agents
-        sc, w = make_workload(N, seed=1 + rank, device=device)
+        c3 = args.config == "c3"
+        sc, w = make_workload(N, seed=(1 if c3 else 0) + rank, device=device, obstacles=N_OBS if c3 else 0)
         model, box, j_max, n, m = "di", BOX, 0, 6, 3
-        spec = scvx_hip.QPSpec(model="di", K=K, box=BOX, obs=sc["obs"], w_obs=1e6, u_max=U_MAX, tol=args.tol,
-                               max_iter=60)
-        drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, tr_rule=args.tr_rule, tie_rtol=args.tie_rtol,
-                         fused_update=not args.tensor_update, warm_max_status=args.warm_status, dispatch_order=args.dispatch_order)
-        n_obs = N_OBS
+        spec = scvx_hip.QPSpec(model="di", K=K, box=BOX, obs=sc["obs"], w_obs=1e6, u_max=U_MAX if c3 else None,
+                               tol=args.tol, max_iter=60)
+        n_obs = len(sc["obs"])
+        soc = c3
+
+        def make_drv(rule):
+            return JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, tr_rule=rule, tie_rtol=args.tie_rtol,
+                              fused_update=not args.tensor_update, warm_max_status=args.warm_status,
+                              dispatch_order=args.dispatch_order)
+        rules = [args.tr_rule] + ([r for r in ("global", "per_agent") if r != args.tr_rule] if args.rules == "both"
+                                  else [])
+        drv = make_drv(rules[0])
     else:
         sc, w, cfg = make_coupled(args.config, world, rank, device)
         N, model, box, j_max = cfg["n_loc"], cfg["model"], cfg["box"], cfg["j_max"]
         n, m = scvx_hip.MODEL_DIMS[model]
         n_obs = len(cfg["obs"])
+        soc = False
         spec = scvx_hip.QPSpec(model=model, K=K, box=box, obs=cfg["obs"], w_obs=1e6, j_max=j_max, w_coll=1e4,
                                tol=args.tol, max_iter=60, **cfg["vc"])
         drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, coupling=CouplingSpec(R=cfg["R"]),
                          tr_rule="global", warm_max_status=args.warm_status, dispatch_order=args.dispatch_order)
+        rules = ["global"]
         if args.balance and world > 1:
             # one untimed step on contiguous shards measures every agent's IPM iterations; the shards are then
             # re-dealt so each rank gets the same mix (scvx_hip.scvx.balanced_order), and the run
@@ -632,89 +775,43 @@ def main():
             w = shard_tensors(sc, order[rank * N:(rank + 1) * N], device)
             drv = JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], TR0, coupling=CouplingSpec(R=cfg["R"]),
                              tr_rule="global", warm_max_status=args.warm_status, dispatch_order=args.dispatch_order)
-    it_state = [w["X"].clone(), w["U"].clone()]   # the current iterate (X, U), rebound every step
-
-    def step(marks=None):
-        it_state[0], it_state[1], out = drv.step(it_state[0], it_state[1], marks=marks)
-        return out
-
-    status_ids = torch.arange(3, device=device, dtype=torch.int32)
-
-    def record(out, iters, iters_max, stats):
-        """Per-step device-side bookkeeping of the timed region (no host sync): summed and max IPM iterations,
-        status counts.  The warmup runs it too, so no torch kernel is loaded for the first time inside the
-        timed region (a first use costs ~40-180 ms of module loading on a fresh box)."""
-        iters.append(out["iters"].sum())
-        iters_max.append(out["iters"].max())
-        stats.append((out["status"][:, None] == status_ids).sum(dim=0))   # no sync (bincount would sync)
-
-    for _ in range(args.warmup):
-        out = step()
-        record(out, [], [], [])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    # timed region: exactly `steps` steps (the same code path as the warmup); every stage is bracketed
-    # by HIP events on the launch stream (the QP kernel's mark pair gives its launch duration)
-    marks, iters, iters_max, checks, stats = [], [], [], [], []
-    t0 = time.perf_counter()
-    host_ms = []
-    for _ in range(args.steps):
-        mk = []
-        th = time.perf_counter()
-        out = step(mk)
-        host_ms.append(1e3 * (time.perf_counter() - th))
-        marks.append(mk)
-        record(out, iters, iters_max, stats)
-        if drv.last_check is not None:
-            checks.append(dict(drv.last_check))
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    el_t = torch.tensor([el], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
-    el = el_t.item()
-    st_ms, step_ms = stage_times(marks)
-    if world > 1:   # every rank's stage medians (the all-gather time per rank for c4/c5)
-        mine = torch.tensor([st_ms.get(k, 0.0) for k in ("foh", "gather", "rows", "qp", "check", "update")],
-                            dtype=torch.float64, device=device)
-        allr = [torch.empty_like(mine) for _ in range(world)]
-        dist.all_gather(allr, mine)
-        per_rank = [r.tolist() for r in allr]
-    else:
-        per_rank = None
-    qp_ms = st_ms["qp"]
-    ipm_iters = float(torch.stack(iters).sum().item())
-    it_agent = ipm_iters / (args.steps * N)
-    status = out["status"].cpu()
-    rows = qp_rows(n, m, len(box), n_obs, j_max, args.config == "c3")
-    qp_flops = qp_flops_per_ipm_iter(n, m, K, rows) * ipm_iters / args.steps          # per launch
-    qp_bytes = qp_bytes_per_agent(n, m, K, j_max) * N
-    foh_bytes = foh_bytes_per_agent(n, m, K) * N
-    foh_flops = foh_flops_per_agent(n, m, K, nsub=scvx_hip.DEFAULT_NSUB[model]) * N
-    achieved = qp_flops / (qp_ms * 1e-3) / 1e12
-    qp_gbs = qp_bytes / (qp_ms * 1e-3) / 1e9
-    t_step = el / args.steps
-    t_min = (max(foh_bytes / (HBM_PEAK_GBS * 1e9), foh_flops / (FP64_PEAK_TFLOPS * 1e12))
-             + max(qp_bytes / (HBM_PEAK_GBS * 1e9), qp_flops / (FP64_PEAK_TFLOPS * 1e12)))
+    rows = qp_rows(n, m, len(box), n_obs, j_max, soc)
+    nsub = drv.nsub   # the FOH substeps the timed loop ran (scvx_hip.default_nsub for its interval)
+    res = timed_leg(drv, w, args, world, device)
+    roof, step_roof = leg_roofline(res, args, n, m, K, N, rows, j_max, model, nsub)
+    primary_cfg = dict(tr_rule=drv.tr_rule, qp_dispatch="longest-first (last-step IPM iterations)"
+                       if getattr(drv, "_lpt", False) else "agent order")
+    other = None
+    if independent and len(rules) > 1:
+        del drv
+        drv2 = make_drv(rules[1])
+        res2 = timed_leg(drv2, w, args, world, device)
+        roof2, step_roof2 = leg_roofline(res2, args, n, m, K, N, rows, j_max, model, nsub)
+        other = dict(tr_rule=rules[1], value=world * args.steps / res2["el"], unit="SCvx-iterations/s",
+                     ms_per_step=1e3 * res2["el"] / args.steps, **res2["fields"],
+                     roofline={k: roof2[k] for k in ("achieved", "frac", "kernel_ms")}, step_roofline=step_roof2)
+    t_step = res["el"] / args.steps
     traffic, traffic_src = committed_traffic() if args.config == "c3" else (None, None)
     if rank == 0:
         cpu = None
-        if not args.no_cpu and args.config == "c3":
+        if not args.no_cpu and independent:
             cpu = cpu_baselines(sc, min(args.cpu_sample, N), tol=args.tol, warmup=args.warmup, steps=args.steps,
-                                warm_status=args.warm_status, tr_rule=args.tr_rule)
-        if args.config == "c3":
-            value, scaling = world * args.steps / el, "weak"
-            metric = "SCvx-iterations/sec, N agents x K=50 nodes (N=1024 per GPU)"
-            data = "synthetic (C3 construction, SURVEY §8d: seeded random starts/goals, 8 spheres)"
-            workload = ("C3: N=1024 agents/GPU, 3-D double integrator n=6 m=3, K=50, FOH sigma=30, tr=0.25, "
-                        "8 obstacles (soft), SOC ||u||<=1, box |x|,|y|<=12")
+                                warm_status=args.warm_status, tr_rule=rules[0], obstacles=n_obs > 0, soc=soc)
+        rule_txt = ("global trust-region rule (dist_scvx_3d.py:248-252: one radius, halved when the summed cost rises)"
+                    if rules[0] == "global" else "per-agent trust-region rule (this build's extension)")
+        if independent:
+            value, scaling = world * args.steps / res["el"], "weak"
+            metric = f"SCvx-iterations/sec, N agents x K=50 nodes (N={N} per GPU)"
+            if args.config == "c3":
+                data = "synthetic (C3 construction, SURVEY §8d: seeded random starts/goals, 8 spheres)"
+                workload = (f"C3: N={N} agents/GPU, 3-D double integrator n=6 m=3, K=50, FOH sigma=30, tr=0.25, "
+                            f"8 obstacles (soft), SOC ||u||<=1, box |x|,|y|<=12, {rule_txt}")
+            else:
+                data = "synthetic (C2 construction, SURVEY §8d: seed 0, random starts/goals, no obstacles)"
+                workload = (f"C2: N={N} agents/GPU, 3-D double integrator n=6 m=3, K=50, FOH sigma=30, tr=0.25, "
+                            f"no coupling, no obstacles, no SOC, box |x|,|y|<=12, {rule_txt}")
         else:
-            value, scaling = args.steps / el, "strong"
+            value, scaling = args.steps / res["el"], "strong"
             metric = f"SCvx-iterations/sec, N={cfg['N_total']} agents x K=50 nodes (whole problem)"
             data = ("synthetic (C4 construction, SURVEY §8d: 16^3 lattice, spacing 6, permuted goals)"
                     if args.config == "c4" else
@@ -725,6 +822,13 @@ def main():
                         f"obstacles, box |x|,|y|<={box[0][2]:g}, global trust-region rule, RCCL all_gather of states"
                         + (f", virtual control w_nu={cfg['vc']['w_nu']:g} + proximal w_prox={cfg['vc']['w_prox']:g}"
                            if cfg["vc"] else ""))
+        roof.update({"traffic": traffic,
+                     "traffic_unit": "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE; warm-started launches as in the "
+                                     "timed region: the PMC command's cold first launch excluded)",
+                     "traffic_source": traffic_src,
+                     "note": "FP64-VALU small dense linear algebra (no MFMA: 6x6 / 6x3 f64 blocks); peak = FP64 "
+                             "dense peak; FLOPs = SURVEY §8(d) count (bench.qp_flops_per_ipm_iter) x executed IPM "
+                             "iterations; bytes = interface bytes (bench.qp_bytes_per_agent)"})
         line = {
             "metric": metric,
             "value": value,
@@ -733,7 +837,6 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": 1e3 * t_step,
-            "ms_per_step_median": float(np.median(step_ms)),
             "higher_is_better": True,
             "scaling": scaling,
             "vs_baseline": None,
@@ -741,43 +844,15 @@ def main():
             "data": data,
             "config": {"workload": workload, "agents_per_gpu": N, "K": K,
                        "parallelism": f"agents sharded x{world}" + (" (balanced order)" if (args.balance and world > 1
-                                                                         and args.config != "c3") else ""),
-                       "qp_dispatch": "longest-first (last-step IPM iterations)" if getattr(drv, "_lpt", False)
-                       else "agent order",
-                       "tr_rule": drv.tr_rule,
+                                                                         and not independent) else ""),
+                       **primary_cfg,
                        # JacobiSCvx's default is 0 (warm-start only optimal solves); the bench warm-starts
                        # optimal_inaccurate ones too (C3 / C5 end every solve optimal: no effect there)
                        "warm_max_status": args.warm_status},
-            "roofline": {"bound": "fp64_valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                         "traffic_unit": "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE; warm-started launches as in the "
-                                         "timed region: the PMC command's cold first launch excluded)",
-                         "traffic_source": traffic_src,
-                         "kernel": "qp_ipm_kernel", "kernel_ms": qp_ms,
-                         "algorithmic_flops_per_launch": qp_flops, "algorithmic_bytes_per_launch": qp_bytes,
-                         "hbm_achieved_gbs": qp_gbs, "hbm_frac": qp_gbs / HBM_PEAK_GBS,
-                         "note": "FP64-VALU small dense linear algebra (no MFMA: 6x6 / 6x3 f64 blocks); peak = FP64 "
-                                 "dense peak; FLOPs = SURVEY §8(d) count (bench.qp_flops_per_ipm_iter) x executed IPM "
-                                 "iterations; bytes = interface bytes (bench.qp_bytes_per_agent)"},
-            "step_roofline": {"hbm_frac": (foh_bytes + qp_bytes) / (t_step * HBM_PEAK_GBS * 1e9),
-                              "fp64_frac": (foh_flops + qp_flops) / (t_step * FP64_PEAK_TFLOPS * 1e12),
-                              "t_min_ms": 1e3 * t_min, "t_min_over_t": t_min / t_step,
-                              "algorithmic_bytes_per_step": foh_bytes + qp_bytes,
-                              "algorithmic_flops_per_step": foh_flops + qp_flops},
-            "stage_ms_median": st_ms,
-            "stage_ms_per_rank": per_rank,
-            "ipm_iters_per_agent": it_agent,
-            "ipm_iters_max_last": int(out["iters"].max().item()),
-            "ipm_iters_hist_last": {str(int(v)): int(c) for v, c in zip(*np.unique(out["iters"].cpu().numpy(),
-                                                                                  return_counts=True))},
-            "status_counts": {str(k): int((status == k).sum()) for k in (0, 1, 2)},
-            "status_counts_per_step": [[int(v) for v in c.tolist()[:3]] for c in stats],
-            "step_ms": [round(v, 4) for v in step_ms],
-            "host_ms_per_step": [round(v, 4) for v in host_ms],
-            "gap_ms_between_steps": [round(a[-1][1].elapsed_time(b[0][1]), 4) for a, b in zip(marks[:-1], marks[1:])],
-            "ipm_iters_max_per_step": [int(v) for v in torch.stack(iters_max).tolist()],
-            "min_frac_status_0_1": min(float((c[0] + c[1]).item()) / N for c in stats),
-            "coupling_check": checks or None,
+            "roofline": roof,
+            "step_roofline": step_roof,
+            **res["fields"],
+            "other_rule": other,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -85,6 +85,19 @@ class FirstOrderHold:
         self.f, self.A, self.B = model.get_equations()
         self.dt = 1.0 / (K - 1)
 
+    def nsub_for(self, sigma):
+        """RK4 substeps of a call with this sigma: the constructor's nsub, else scvx_hip.default_nsub for the
+        interval sigma / (K - 1) (the one count the FOH and the inter-sample roll-outs of this object share)."""
+        return self._nsub or scvx_hip.default_nsub(self._name, float(sigma), self.K)
+
+    def rollout_nsub(self, sigma):
+        """RK4 substeps of the nonlinear roll-outs (integrate_nonlinear_*, the inter-sample segments): the
+        constructor's nsub, else at least 16 (scvx_hip.integrate_nonlinear's default) and at least the FOH's count
+        for this sigma."""
+        if self._nsub:
+            return self._nsub
+        return max(16, self.nsub_for(sigma)) if isinstance(self._name, str) else self.nsub_for(sigma)
+
     def _to_dev(self, X, U, sigma):
         import torch
         Xd = torch.as_tensor(np.ascontiguousarray(np.asarray(X, float).T[None]), device=self._device)
@@ -96,7 +109,7 @@ class FirstOrderHold:
         """X (n_x, K), U (n_u, K), sigma -> (A_bar, B_bar, C_bar, S_bar, z_bar)."""
         Xd, Ud, sd = self._to_dev(X, U, sigma)
         if isinstance(self._name, str):
-            disc = scvx_hip.foh_batched(self._name, Xd, Ud, sd, nsub=self._nsub, params=self._params)
+            disc = scvx_hip.foh_batched(self._name, Xd, Ud, sd, nsub=self.nsub_for(sigma), params=self._params)
             outs = scvx_hip.unpack_disc(disc[0], self._name)
         else:
             disc = self._name.foh(Xd, Ud, sd, nsub=self._nsub, params=self._params)
@@ -141,20 +154,20 @@ class FirstOrderHold:
 
     def integrate_nonlinear_piecewise(self, X_lin, U, sigma):
         Xd, Ud, sd = self._to_dev(X_lin, U, sigma)
-        out = self._roll(Xd, Ud, sd, True)
+        out = self._roll(Xd, Ud, sd, True, self.rollout_nsub(sigma))
         return out[0].cpu().numpy().T.copy()
 
     def integrate_nonlinear_full(self, x0, U, sigma):
         X = np.zeros((self.n_x, self.K))
         X[:, 0] = np.asarray(x0, float).reshape(-1)
         Xd, Ud, sd = self._to_dev(X, U, sigma)
-        out = self._roll(Xd, Ud, sd, False)
+        out = self._roll(Xd, Ud, sd, False, self.rollout_nsub(sigma))
         return out[0].cpu().numpy().T.copy()
 
-    def _roll(self, Xd, Ud, sd, piecewise):
+    def _roll(self, Xd, Ud, sd, piecewise, nsub):
         if isinstance(self._name, str):
-            return scvx_hip.integrate_nonlinear(self._name, Xd, Ud, sd, piecewise, params=self._params)
-        return self._name.integrate_nonlinear(Xd, Ud, sd, piecewise, params=self._params)
+            return scvx_hip.integrate_nonlinear(self._name, Xd, Ud, sd, piecewise, nsub=nsub, params=self._params)
+        return self._name.integrate_nonlinear(Xd, Ud, sd, piecewise, nsub=nsub, params=self._params)
 
     def _dx(self, x, t, u0, u1, sigma):
         """Nonlinear dynamics in physical time with u interpolated by t/(dt*sigma) (:157-162); host-side,

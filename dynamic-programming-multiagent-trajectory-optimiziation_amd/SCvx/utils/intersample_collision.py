@@ -44,6 +44,9 @@ class SegmentRollout:
         self.sigma = float(sigma)
         self.foh_dt = float(foh.dt)
         self.dt_phys = self.foh_dt * self.sigma
+        # one RK4 substep count for every roll-out of this segment: the critical-time scan (scvx_intersample_batched)
+        # and the h0 / grad_x evaluations at t* (integrate_nonlinear) integrate the same discretisation
+        self.nsub = foh.rollout_nsub(self.sigma)
 
     def __call__(self, xk, _u_dummy, t):
         # a one-interval roll-out whose interval is [0, t dt_phys] and whose end input is
@@ -53,9 +56,9 @@ class SegmentRollout:
         U = _t(np.stack([self.u0, self.u0 + t * (self.u1 - self.u0)])[None], self.device)
         s = _t([t * self.dt_phys], self.device)
         if isinstance(self.model, str):
-            out = scvx_hip.integrate_nonlinear(self.model, X, U, s, True, params=self.params)
+            out = scvx_hip.integrate_nonlinear(self.model, X, U, s, True, nsub=self.nsub, params=self.params)
         else:
-            out = self.model.integrate_nonlinear(X, U, s, True, params=self.params)
+            out = self.model.integrate_nonlinear(X, U, s, True, nsub=self.nsub, params=self.params)
         return out[0, 1].cpu().numpy()
 
 
@@ -78,7 +81,7 @@ def _scan_device(seg: SegmentRollout, xk, T, obstacle, dt, num_samples, eps, tol
     sig = _t([seg.sigma], seg.device)
     out = scvx_hip.intersample_batched(seg.model, X, U, sig, [obstacle], proj=np.asarray(T, float).reshape(-1, n),
                                        dt=dt, seg_dt=seg.foh_dt, num_samples=num_samples, eps=eps, tol=tol,
-                                       params=seg.params)
+                                       nsub=seg.nsub, params=seg.params)
     host = {k: v.cpu().numpy()[0, 0, 0] for k, v in out.items()}
     cnt = int(host["n_crit"])
     if cnt > host["t_crit"].shape[0]:
@@ -146,7 +149,7 @@ def segment_minima(foh, X: np.ndarray, U: np.ndarray, obstacles: Sequence, T, si
     out = scvx_hip.intersample_batched(model, _t(np.asarray(X, float).T[None], dev), _t(np.asarray(U, float).T[None], dev),
                                        _t([sigma], dev), list(obstacles), proj=T, dt=dt, seg_dt=foh.dt,
                                        num_samples=num_samples, eps=eps, tol=tol, max_crit=max_crit,
-                                       params=getattr(foh.model, "scvx_params", None))
+                                       nsub=foh.rollout_nsub(sigma), params=getattr(foh.model, "scvx_params", None))
     h = {k: v.cpu().numpy()[0] for k, v in out.items()}
     res = {}
     for k in range(K - 1):

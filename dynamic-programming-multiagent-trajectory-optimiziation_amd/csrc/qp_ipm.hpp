@@ -138,6 +138,12 @@ constexpr int qp_lds_doubles(int nx, int nu, int nb, int no, int nc, int vc, int
 constexpr int QP_OOB = 0x40000000;
 // warm start: floor of every slack and dual of the previous iterate (scaled units; oracle/scvx_cpu.cpp)
 constexpr double QP_WARM_ETA = 1e-3;
+// ... except that a row's dual floor is min(QP_WARM_ETA, QP_WARM_KAPPA / s) at its recomputed slack s: a row far from
+// active (box rows, obstacle rows away from the trajectory: s ~ 1..10) keeps a dual near its last, tiny value instead
+// of 1e-3, so the start's complementarity s lambda is ~1e-5 there, not ~1e-2.  The warm solve starts ~100x closer
+// to the end game: on the CPU twin over the bench's 25 steps, the slowest agent's IPM iterations summed over the
+// timed steps fall 171 -> 132 (per-agent rule) and 240 -> 201 (global rule), seeds 2 and 3 alike
+constexpr double QP_WARM_KAPPA = 1e-5;
 // stiff trust-region facet: its barrier weight D = lambda / s above QP_STIFF x the largest diagonal entry of the rest
 // of the stage's input Hessian Rhat (oracle/scvx_cpu.cpp STIFF_RATIO, the same rule)
 constexpr double QP_STIFF = 1e6;
@@ -146,6 +152,9 @@ constexpr double QP_STIFF = 1e6;
 // steps and a product (~1.5 ulp, six instructions) instead of the correctly rounded division sequence (eleven,
 // with a longer dependent chain); these run once per row per phase on every node
 __device__ __forceinline__ double qp_div(double a, double b) {
+#ifdef QP_EXACT_DIV   // diagnostics build (tools/qp_div_accuracy.py): the correctly rounded division of round 4
+    return a / b;
+#endif
     double r = __builtin_amdgcn_rcp(b);
     r = fma(fma(-b, r, 1.0), r, r);
     r = fma(fma(-b, r, 1.0), r, r);
@@ -1177,12 +1186,16 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                                 v += (sfi[i] < 0 ? 0.0 : (((sfi[i] >> j) & 1) ? -1.0 : 1.0)) * Wm[j * PM + k];
                             Cm[i * PM + k] = v;
                         }
-                    // C^-1 by Gauss-Jordan without pivoting (C is symmetric positive definite)
+                    // C^-1 by Gauss-Jordan without pivoting (C is symmetric positive definite in exact arithmetic); a
+                    // pivot that is not positive and finite fails the factor, as the twin's Cholesky of C does
+                    // (oracle/scvx_cpu.cpp riccati_factor)
 #pragma unroll
                     for (int e = 0; e < PM * PM; ++e) Ci[e] = (e / PM == e % PM) ? 1.0 : 0.0;
 #pragma unroll
                     for (int k = 0; k < PM; ++k) {
-                        const double rp = 1.0 / Cm[k * PM + k];
+                        const double pv = Cm[k * PM + k];
+                        bad |= !(pv > 0.0 && pv < __builtin_inf());
+                        const double rp = 1.0 / pv;
 #pragma unroll
                         for (int j = 0; j < PM; ++j) { Cm[k * PM + j] *= rp; Ci[k * PM + j] *= rp; }
 #pragma unroll
@@ -1196,7 +1209,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                             }
                         }
                     }
-                    bad |= !(Ci[0] == Ci[0]);
+#pragma unroll
+                    for (int e = 0; e < PM * PM; ++e) bad |= !(Ci[e] - Ci[e] == 0.0);   // every entry finite
                 }
                 {  // every lane runs the solve (lanes >= 2 NX on a copy of column 0, results to the sinks)
                     const bool kl = sl < 2 * NX;
@@ -2494,7 +2508,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         // warm start (the Jacobi SCvx loop re-solves each agent's subproblem re-linearised at its own last
         // solution): z, y, the group and SOC duals and the row duals are the last iterate's; the slacks are
         // recomputed from this solve's rows at z; every slack and dual is floored at QP_WARM_ETA inside its
-        // cone (oracle/scvx_cpu.cpp warm_point does the same).  C3: 12.3 -> ~5 IPM iterations on average.
+        // cone, a row's dual at min(QP_WARM_ETA, QP_WARM_KAPPA / s) (oracle/scvx_cpu.cpp warm_point does the same).
+        // C3: 12.3 -> ~5 IPM iterations on average.
         load_state();
         double wl[NR];
         ldn(wl, C::C_WL, NR);
@@ -2504,8 +2519,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             double gz, h;
             row_eval(r, z, av, gz, h);
             const bool on = row_on(r);
-            s_set(r, on ? fmax(h - gz, QP_WARM_ETA) : 1.0);
-            l_set(r, on ? fmax(wl[r], QP_WARM_ETA) : 0.0);
+            const double sr = fmax(h - gz, QP_WARM_ETA);
+            s_set(r, on ? sr : 1.0);
+            l_set(r, on ? fmax(wl[r], fmin(QP_WARM_ETA, QP_WARM_KAPPA / sr)) : 0.0);
         }
         if (soc) {
             double nu2 = 0.0, nl2 = 0.0;
@@ -2522,8 +2538,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         for (int i = 0; i < NV; ++i) {
             vs[2 * i] = vact ? fmax(ve[i] - vn[i], QP_WARM_ETA) : 1.0;
             vs[2 * i + 1] = vact ? fmax(ve[i] + vn[i], QP_WARM_ETA) : 1.0;
-            vl[2 * i] = vact ? fmax(vl[2 * i], QP_WARM_ETA) : 0.0;
-            vl[2 * i + 1] = vact ? fmax(vl[2 * i + 1], QP_WARM_ETA) : 0.0;
+            vl[2 * i] = vact ? fmax(vl[2 * i], fmin(QP_WARM_ETA, QP_WARM_KAPPA / vs[2 * i])) : 0.0;
+            vl[2 * i + 1] = vact ? fmax(vl[2 * i + 1], fmin(QP_WARM_ETA, QP_WARM_KAPPA / vs[2 * i + 1])) : 0.0;
         }
         store_state();
     } else {

@@ -14,6 +14,7 @@ kernels run on torch's current HIP stream, nothing falls back to the CPU.
                            (SCvx/optimization/sc_problem.py:15-83, agent_solver.py:78-102)
 """
 import ctypes
+import math
 from dataclasses import dataclass, field
 from typing import Optional, Sequence, Tuple
 
@@ -23,8 +24,14 @@ from ._lib import MODEL_DIMS, MODEL_IDS, STATUS, QPTemplate, SCPTemplate, ScvxEr
 # RK4 substeps per FOH interval: the smallest count that keeps each model within 1e-7 of the reference's LSODA
 # goldens (tests/test_foh_gpu.py, tests/test_foh_oracle.py).  1 is exact for the (linear) integrators; the
 # quadrotor holds at 10 (round 5, oracle/foh_ref.c on tests/golden/foh_quad_K50_s5.npz: max relative error 1.2e-7 at
-# 8, 7.7e-8 at 9, 5.2e-8 at 10, 9e-10 at 16 -- 16 was 2.7 ms of a 47.5 ms C5 step), the unicycle keeps 16.
+# 8, 7.7e-8 at 9, 5.2e-8 at 10, 9e-10 at 16), the unicycle keeps 16.
 DEFAULT_NSUB = {"di": 1, "si": 1, "unicycle": 16, "quad": 10}
+# ... at the golden's interval T_pin = sigma / (K - 1).  The RK4 error grows with the interval (the quadrotor at
+# sigma = 30, K = 50, six times the golden's interval: 3.8e-6 at 10 substeps, 5.7e-7 at 16, against 256 substeps), so
+# for longer intervals the count scales as DEFAULT_NSUB * (T / T_pin)^0.75: the RK4 self-convergence test
+# (tests/test_foh_oracle.py: K 30..100, sigma 2..45, attitudes to 0.6 rad) holds 1e-7 with it; C5 (sigma 30, K 50)
+# runs 39.  (model: (T_pin, exponent))
+NSUB_SCALE = {"quad": (5.0 / 49.0, 0.75)}
 QUAD_PARAMS = (1.0, 9.81, 0.02, 0.02, 0.04)
 
 __all__ = ["model_dims", "model_id", "default_nsub", "foh_batched", "integrate_nonlinear", "collision_rows", "collision_check", "qp_solve_batched", "QPSpec", "SCPSpec", "SCPSolver", "slab_update",
@@ -73,9 +80,28 @@ def model_id(model):
     return MODEL_IDS[model] if isinstance(model, str) else _lib.SCVX_MODEL_RUNTIME
 
 
-def default_nsub(model):
-    """RK4 substeps of the FOH: the built-in table, 16 for a user model (as the nonlinear built-ins)."""
-    return DEFAULT_NSUB[model] if isinstance(model, str) else 16
+def default_nsub(model, sigma=None, K=None):
+    """RK4 substeps of the FOH: the built-in table (a user model: its DeviceModel.nsub, 16 by default); with the
+    interval known (sigma, K), a model in NSUB_SCALE gets DEFAULT_NSUB * (T / T_pin)^p for intervals T = sigma / (K-1)
+    longer than its pinned T_pin (never fewer than the table)."""
+    if not isinstance(model, str):
+        return int(getattr(model, "nsub", 16))
+    base = DEFAULT_NSUB[model]
+    if sigma is None or K is None or model not in NSUB_SCALE:
+        return base
+    t_pin, p = NSUB_SCALE[model]
+    T = float(sigma) / (int(K) - 1)
+    return max(base, int(math.ceil(base * (T / t_pin) ** p - 1e-9)))
+
+
+def _auto_nsub(model, sigma, K):
+    """default_nsub for a device sigma batch: the longest interval of the batch (one host read of max(sigma), only
+    for the models whose count depends on the interval)."""
+    if isinstance(model, str) and model not in NSUB_SCALE:
+        return DEFAULT_NSUB[model]
+    if not isinstance(model, str):
+        return default_nsub(model)
+    return default_nsub(model, float(sigma.max().item()) if sigma.numel() else 0.0, K)
 
 
 def disc_stride(model):
@@ -101,7 +127,8 @@ def _params(model, params):
 
 
 def foh_batched(model, X, U, sigma, nsub=None, params=None, out=None, stream=None):
-    """X (N,K,n), U (N,K,m), sigma (N,) float64 device tensors -> disc (N,K-1,n(n+2m+2))."""
+    """X (N,K,n), U (N,K,m), sigma (N,) float64 device tensors -> disc (N,K-1,n(n+2m+2)).  nsub None: default_nsub
+    for the batch's longest interval (for the quadrotor this reads max(sigma) on the host; pass nsub to avoid it)."""
     torch = _torch()
     N, K, n = X.shape
     m = U.shape[2]
@@ -114,7 +141,7 @@ def foh_batched(model, X, U, sigma, nsub=None, params=None, out=None, stream=Non
         out = torch.empty((N, K - 1, disc_stride(model)), dtype=torch.float64, device=X.device)
     keep, pp = _params(model, params)
     rc = lib().scvx_foh_batched(MODEL_IDS[model], pp, K, N, _dev(X, name="X"), _dev(U, name="U"),
-                                _dev(sigma, name="sigma"), int(nsub or DEFAULT_NSUB[model]),
+                                _dev(sigma, name="sigma"), int(nsub or _auto_nsub(model, sigma, K)),
                                 _dev(out, name="out"), _stream(stream))
     check(rc, "scvx_foh_batched")
     return out
@@ -623,7 +650,11 @@ def intersample_batched(model, X, U, sigma, obstacles, proj=None, dt=1.0, seg_dt
             t.proj[i * _lib.SCVX_IS_MAX_STATE + j] = float(Tm[i, j])
     t.dt, t.seg_dt = float(dt), float(1.0 / (K - 1) if seg_dt is None else seg_dt)
     t.eps, t.tol, t.num_samples, t.max_crit = float(eps), float(tol), int(num_samples), int(max_crit)
-    t.nsub = int(nsub or (model.nsub if rt else DEFAULT_NSUB[model]))
+    # default substeps: the FOH's for this segment length T = seg_dt * sigma (default_nsub; the quadrotor's count
+    # grows with T, so max(sigma) is read on the host for it)
+    t.nsub = int(nsub or (model.nsub if rt else
+                          (default_nsub(model, t.seg_dt * float(sigma.max().item()), 2) if model in NSUB_SCALE and N
+                           else DEFAULT_NSUB[model])))
     dev = X.device
     f64 = torch.float64
     shp = (N, K - 1, max(O, 1))

@@ -140,7 +140,9 @@ class JacobiSCvx:
             if self.device.type == "cuda" else self.N
         self._lpt = dispatch_order == "lpt" and self.N > resident
         self.group = group
-        self.nsub = nsub or default_nsub(spec.model)
+        # RK4 substeps of the FOH: default_nsub for this run's longest interval (one host read of max(sigma) here,
+        # none per step; the quadrotor's count grows with the interval)
+        self.nsub = nsub or default_nsub(spec.model, float(sigma.max().item()) if self.N else None, spec.K)
         self.solver = self.backend.qp_solver(spec, self.N, self.device)
         self.tr = torch.full((self.N,), float(tr0), dtype=torch.float64, device=self.device)
         self.prev_cost = torch.full((self.N,), float("inf"), dtype=torch.float64, device=self.device)

@@ -947,6 +947,8 @@ static bool init_point(Agent& ag) {
 // Per-agent state: per node z (nv) | lambda (nr) | lsoc (m+1), padded to a fixed stride, then y ((K-1) n),
 // y_init (n), y_fin (n).
 constexpr double QP_WARM_ETA = 1e-3;
+// a row's dual floor: min(QP_WARM_ETA, QP_WARM_KAPPA / s) (round 6; kernel csrc/qp_ipm.hpp, the same constants)
+constexpr double QP_WARM_KAPPA = 1e-5;
 static int warm_node_stride(const scvx_qp_template* T) {
     const int n = T->n_x, m = T->n_u, nnu = T->w_nu > 0.0 ? n : 0;
     const int aux = T->n_obs + (T->j_max > 0 ? 1 : 0) + nnu;
@@ -979,6 +981,10 @@ static void warm_point(Agent& ag, const double* w, double eta) {
     const char* ek = std::getenv("SCVX_WARM_TRK");
     const char* el = std::getenv("SCVX_WARM_TRL");
     const double ks = ek ? std::atof(ek) : 0.0, kl = el ? std::atof(el) : 0.0;
+    // a row's dual floor is min(eta, QP_WARM_KAPPA / s) at its floored slack s (kernel: the same rule): a row with a
+    // large slack keeps a small dual.  SCVX_WARM_KAPPA: experiment knob (0: the round-5 floor eta for every dual)
+    const char* ekap = std::getenv("SCVX_WARM_KAPPA");
+    const double kap = ekap ? std::atof(ekap) : QP_WARM_KAPPA;
     for (int t = 0; t < K; ++t) {
         Node& N = ag.nd[t];
         const double* o = w + (size_t)t * st;
@@ -988,7 +994,9 @@ static void warm_point(Agent& ag, const double* w, double eta) {
             for (int j = 0; j < N.nv; ++j) v -= N.G(r, j) * N.z[j];
             const bool trf = r < (1 << m) && t < K - 1;
             N.s[r] = std::max(v, (trf && ks > 0) ? std::min(eta, ks * ag.trv) : eta);
-            N.lam[r] = std::max(o[N.nv + r], (trf && kl > 0) ? std::min(eta, kl * ag.trv) : eta);
+            double lf = (trf && kl > 0) ? std::min(eta, kl * ag.trv) : eta;
+            if (kap > 0) lf = std::min(lf, kap / N.s[r]);
+            N.lam[r] = std::max(o[N.nv + r], lf);
         }
         if (N.soc) {
             N.ssoc[0] = T->u_max;
@@ -1015,7 +1023,7 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out, const double*
     std::vector<Mat> H(K);
     Riccati R;
     int status = SCVX_STATUS_MAX_ITER;
-    int it = 0;
+    int it = 0, n_skip = 0;
     const double tol = T->tol > 0 ? T->tol : 1e-9;
     // objective scaling (kernel: osc): solve with the objective divided by max(1, ||q||_inf); the gap test
     // and the reported objective are in the caller's units
@@ -1382,8 +1390,13 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out, const double*
             double mu_a = gap_a / std::max(deg, 1);
             const double sgr = std::max(mu_a, 0.0) / mu;   // the kernel's cube (products, not pow)
             double sig = sgr * sgr * sgr;
+            // experiment knob SCVX_SKIP_CORR=thr: when the affine step is >= thr, step along the predictor direction
+            static const double skip_thr = std::getenv("SCVX_SKIP_CORR") ? std::atof(std::getenv("SCVX_SKIP_CORR")) : 2.0;
+            static const double skip_sgr = std::getenv("SCVX_SKIP_SGR") ? std::atof(std::getenv("SCVX_SKIP_SGR")) : 1e300;
+            const bool skipc = aa >= skip_thr && sgr <= skip_sgr;
+            if (skipc) ++n_skip;
             // corrector
-            for (int t = 0; t < K; ++t) {
+            if (!skipc) for (int t = 0; t < K; ++t) {
                 Node& N = ag.nd[t];
                 for (int r = 0; r < N.nr; ++r) rco[t][r] += -ds[t][r] * dl[t][r] + sig * mu;
                 if (N.soc) {
@@ -1393,7 +1406,7 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out, const double*
                     rcq[t][0] += sig * mu;
                 }
             }
-            if (!newton(rco, rcq, dz, ds, dl, dsq, dlq, dy, dyi, dyf)) { status = fail_status; break; }
+            if (!skipc && !newton(rco, rcq, dz, ds, dl, dsq, dlq, dy, dyi, dyf)) { status = fail_status; break; }
             // experiment knob SCVX_TWIN_REFINE=k: k steps of iterative refinement of the corrector direction on the
             // linearised KKT system (its dual and dynamics residuals at the full-step point; the row and
             // complementarity equations hold by construction), each a re-solve with the same factorisation
@@ -1520,6 +1533,7 @@ done:
         for (int t = 0; t < K; ++t)
             for (int i = 0; i < n; ++i) obj_out += ag.T->w_prox * ag.xref[(size_t)t * n + i] * ag.xref[(size_t)t * n + i];
     iters_out = it;
+    if (std::getenv("SCVX_ENCODE_SKIP")) iters_out += 100 * n_skip;   // experiment: skipped correctors in the hundreds
     return status;
 }
 

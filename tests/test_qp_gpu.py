@@ -17,6 +17,29 @@ def _t(x, cuda, dtype=None):
     return torch.tensor(np.ascontiguousarray(x), device=cuda, dtype=dtype or torch.float64)
 
 
+def _kernel_pnorm(X, U, S, Xref, Uref, x_init, x_final, tr, box, rows, cnt, c_dyn=0.0):
+    """The kernel's primal normalisation max(1, ||b|| + ||x|| + ||s||) (qp_ipm.hpp residual phase: Clarabel's relative
+    primal test, inf-norms over every constant, variable and slack of its formulation) evaluated at a returned
+    solution: b = x_init, x_final, the dynamics constants, every row's right-hand side (trust-region facets
+    tr + s'ubar, box bounds, collision rows -b); x = (X, U, the shared collision slack S); s = every row's slack
+    (facets tr - s'(u - ubar) at most tr + ||u - ubar||_1, box hi - x / x - lo, collision rows -b + g'p + S, the
+    slack's sign row S).  Inequality rows live on nodes t < K-1 (ineq_last = 0)."""
+    K = X.shape[0]
+    nb = max(np.abs(x_init).max(), np.abs(x_final).max(), float(np.max(np.abs(c_dyn))))
+    nb = max(nb, tr + np.abs(Uref[:K - 1]).sum(axis=1).max(), max(max(abs(lo), abs(hi)) for _, lo, hi in box))
+    nx = max(np.abs(X).max(), np.abs(U).max(), np.abs(S).max())
+    ns = (tr + np.abs(U[:K - 1] - Uref[:K - 1]).sum(axis=1)).max()
+    for b, lo, hi in box:
+        ns = max(ns, (hi - X[:K - 1, b]).max(), (X[:K - 1, b] - lo).max())
+    ns = max(ns, np.abs(S[:K - 1]).max())
+    for t in range(K - 1):
+        for j in range(cnt[t]):
+            g, bb = rows[t, j, :3], rows[t, j, 3]
+            nb = max(nb, abs(bb))
+            ns = max(ns, -bb + g @ X[t, :3] + S[t])
+    return max(1.0, nb + nx + ns)
+
+
 def test_dist_scvx_3d_first_iteration_matches_dense_oracle(cuda):
     sc = pb.dist3_scenario()
     T = sc["T"]
@@ -51,9 +74,12 @@ def test_dist_scvx_3d_first_iteration_matches_dense_oracle(cuda):
         U = out["U"][i].cpu().numpy()
         S = out["slack_coll"][i].cpu().numpy()
         viol = qd.constraint_violation(prob, X, U, S)
-        # Clarabel's primal test is relative: tol (1e-9) x (||b|| + ||x|| + ||s||), positions and the box bounds
-        # here reach ~22 and the box slacks ~44: up to ~1e-7 (measured 5.6e-8 on the terminal state)
-        assert max(viol.values()) < 1e-7, viol
+        # Clarabel's primal test is relative: tol (1e-9) x (||b|| + ||x|| + ||s||) of the kernel's own formulation
+        # (_kernel_pnorm at this solution: ~66 here, positions and box bounds ~22, box slacks ~23); the reference-form
+        # violation of a row is at most its residual in the kernel's form, plus the rounding of d = X - Xref
+        bound = spec.tol * _kernel_pnorm(X, U, S, Xref[i], Uref[i], Xref[i, 0], xdes[i], sc["tr"], box, rows[i],
+                                         cnt[i]) + 1e-14 * max(1.0, np.abs(X).max())
+        assert max(viol.values()) <= bound, (viol, bound)
         obj = out["obj"][i].item()
         assert abs(obj - objd) <= 1e-8 * max(1.0, abs(objd))
         if objd < 1e3:  # slack-free agents: the quadratic part pins the trajectory

@@ -4,6 +4,7 @@ IPM-iteration histogram of every step.  Used to try IPM algorithm changes on the
 go into qp_ipm.hpp (the kernel time is the slowest agent's iteration count x the per-iteration latency).
 usage: python tools/ipm_tail_cpu.py [steps] [N] [threads]
 WARM=1: warm-start every agent from its previous solve (JacobiSCvx's default; the kernel's rule).
+RULE=global: the reference's global trust-region rule (the bench headline) instead of the per-agent rule.
 DUMP=path.npz: save the last step's inputs and per-agent iteration counts (to replay a tail agent)."""
 import os
 import sys
@@ -22,11 +23,12 @@ steps = int(sys.argv[1]) if len(sys.argv) > 1 else 6
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
 threads = int(sys.argv[3]) if len(sys.argv) > 3 else (os.cpu_count() or 1)
 K = bench.K
-sc = workloads.synthetic_di(N, K=K, seed=1, sigma=bench.SIGMA, obstacles=bench.N_OBS)
+sc = workloads.synthetic_di(N, K=K, seed=int(os.environ.get("SEED", "1")), sigma=bench.SIGMA, obstacles=bench.N_OBS)
 tpl = qp_cpu.make_template(6, 3, K, box=bench.BOX, obs=sc["obs"], w_obs=1e6, u_max=bench.U_MAX, tol=1e-8, max_iter=60)
 X, U = sc["X"].copy(), sc["U"].copy()
 tr = np.full(N, bench.TR0)
 prev = np.full(N, np.inf)
+prev_total = np.inf
 tot = []
 tot_cost = []
 WARM = os.environ.get("WARM") == "1"
@@ -52,7 +54,11 @@ for s in range(steps):
     ok = (st != 2)[:, None, None]
     X, U = np.where(ok, o["X"], X), np.where(ok, o["U"], U)
     cost = (U[:, :-1] ** 2).sum(axis=(1, 2))
-    tr = tr * np.where(cost > prev * (1 + 1e-9), 0.5, 1.0) * np.where(st == 2, 0.5, 1.0)
+    if os.environ.get("RULE") == "global":   # the reference's rule (dist_scvx_3d.py:248-252), as JacobiSCvx
+        tr = tr * (0.5 if cost.sum() > prev_total else 1.0) * np.where(st == 2, 0.5, 1.0)
+        prev_total = cost.sum()
+    else:
+        tr = tr * np.where(cost > prev * (1 + 1e-9), 0.5, 1.0) * np.where(st == 2, 0.5, 1.0)
     prev = cost
-    warm = (st <= 0).astype(np.int32)
+    warm = (st <= int(os.environ.get("WARM_STATUS", "1"))).astype(np.int32)   # bench.py --warm-status default 1
 print(f"sum of per-step max iterations: {sum(tot)} (mean {np.mean(tot):.2f}); mean max cost {np.mean(tot_cost):.2f}")
