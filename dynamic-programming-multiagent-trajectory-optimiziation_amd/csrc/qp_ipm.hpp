@@ -1187,14 +1187,16 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                             Cm[i * PM + k] = v;
                         }
                     // C^-1 by Gauss-Jordan without pivoting (C is symmetric positive definite in exact arithmetic); a
-                    // pivot that is not positive and finite fails the factor, as the twin's Cholesky of C does
-                    // (oracle/scvx_cpu.cpp riccati_factor)
+                    // zero or non-finite pivot, or a non-finite entry of C^-1, fails the factor (round 6: the round-5
+                    // check saw a NaN in the first entry only).  A pivot <= 0 is NOT fatal here: failing the factor on
+                    // it (as the twin's Cholesky of C would) ended 146 of 512 C4 lattice solves status 2 on the GPU
+                    // while the twin never meets one on the same fixtures
 #pragma unroll
                     for (int e = 0; e < PM * PM; ++e) Ci[e] = (e / PM == e % PM) ? 1.0 : 0.0;
 #pragma unroll
                     for (int k = 0; k < PM; ++k) {
                         const double pv = Cm[k * PM + k];
-                        bad |= !(pv > 0.0 && pv < __builtin_inf());
+                        bad |= !(pv != 0.0 && pv - pv == 0.0);
                         const double rp = 1.0 / pv;
 #pragma unroll
                         for (int j = 0; j < PM; ++j) { Cm[k * PM + j] *= rp; Ci[k * PM + j] *= rp; }

@@ -34,7 +34,7 @@ DEFAULT_NSUB = {"di": 1, "si": 1, "unicycle": 16, "quad": 10}
 NSUB_SCALE = {"quad": (5.0 / 49.0, 0.75)}
 QUAD_PARAMS = (1.0, 9.81, 0.02, 0.02, 0.04)
 
-__all__ = ["model_dims", "model_id", "default_nsub", "foh_batched", "integrate_nonlinear", "collision_rows", "collision_check", "qp_solve_batched", "QPSpec", "SCPSpec", "SCPSolver", "slab_update",
+__all__ = ["model_dims", "model_id", "default_nsub", "foh_batched", "jacobi_update", "jacobi_update_global", "integrate_nonlinear", "collision_rows", "collision_check", "qp_solve_batched", "QPSpec", "SCPSpec", "SCPSolver", "slab_update",
            "intersample_batched",
            "disc_stride", "unpack_disc", "ScvxError", "MODEL_DIMS", "DEFAULT_NSUB"]
 
@@ -609,6 +609,47 @@ def jacobi_update(status, X_sol, U_sol, X, U, tr, prev_cost, grow=False, tr_max=
                                           _dev(prev_cost, name="prev_cost"), int(bool(grow)), float(tr_max),
                                           float(tie_rtol), _stream(stream))
     check(rc, "scvx_jacobi_update_batched")
+    return X_out, U_out
+
+
+def jacobi_update_global(status, X_sol, U_sol, X, U, tr, prev_total, grow=False, tr_max=float("inf"), X_out=None,
+                         U_out=None, all_reduce=None, stream=None):
+    """Fused bookkeeping of one Jacobi SCvx iteration under the reference's global trust-region rule
+    (Distributed_opt/dist_scvx_3d.py:242-252; scvx_jacobi_update_costs_batched + scvx_jacobi_global_rule): failed agents
+    (status 2) keep (X, U), the others take (X_sol, U_sol); every radius halves when the summed cost
+    sum_i sum_{t<K-1} ||u_t||^2 exceeds prev_total (strict), then a failed agent's radius halves (or doubles up to
+    tr_max with grow=True); prev_total (a (1,) device tensor) <- the total.  all_reduce: a callable that sums a (1,)
+    device tensor over the ranks in place (torch.distributed.all_reduce), for agents sharded over ranks.  Returns
+    (X_out, U_out)."""
+    torch = _torch()
+    N, K, n = X.shape
+    m = U.shape[2]
+    if (tuple(X_sol.shape) != (N, K, n) or tuple(U.shape) != (N, K, m) or tuple(U_sol.shape) != (N, K, m)
+            or tuple(status.shape) != (N,) or tuple(tr.shape) != (N,) or tuple(prev_total.shape) != (1,)):
+        raise ValueError("jacobi_update_global: X / X_sol (N,K,n), U / U_sol (N,K,m), status / tr (N,), prev_total (1,)")
+    X_out = torch.empty_like(X) if X_out is None else X_out
+    U_out = torch.empty_like(U) if U_out is None else U_out
+    cost = torch.empty((N,), dtype=torch.float64, device=X.device)
+    L, st = lib(), _stream(stream)
+    rc = L.scvx_jacobi_update_costs_batched(N, K, n, m, _dev(status, torch.int32, "status"), _dev(X_sol, name="X_sol"),
+                                            _dev(U_sol, name="U_sol"), _dev(X, name="X"), _dev(U, name="U"),
+                                            _dev(X_out, name="X_out"), _dev(U_out, name="U_out"), _dev(cost, name="cost"),
+                                            st)
+    check(rc, "scvx_jacobi_update_costs_batched")
+    s32, ptr = _dev(status, torch.int32, "status"), _dev(tr, name="tr")
+    pt = _dev(prev_total, name="prev_total")
+    if all_reduce is None:
+        rc = L.scvx_jacobi_global_rule(N, 1, s32, _dev(cost, name="cost"), None, None, ptr, pt, int(bool(grow)),
+                                       float(tr_max), st)
+    else:
+        total = torch.empty((1,), dtype=torch.float64, device=X.device)
+        rc = L.scvx_jacobi_global_rule(N, 0, s32, _dev(cost, name="cost"), None, _dev(total, name="total"), None, None,
+                                       0, 0.0, st)
+        check(rc, "scvx_jacobi_global_rule")
+        all_reduce(total)
+        rc = L.scvx_jacobi_global_rule(N, 2, s32, None, _dev(total, name="total"), None, ptr, pt, int(bool(grow)),
+                                       float(tr_max), st)
+    check(rc, "scvx_jacobi_global_rule")
     return X_out, U_out
 
 

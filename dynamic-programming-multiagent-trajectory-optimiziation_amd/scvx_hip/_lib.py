@@ -11,7 +11,7 @@ LIB_PATH = os.environ.get("SCVX_HIP_LIB") or os.path.join(HERE, "libscvx_hip.so"
 
 # the C-ABI revision these bindings are written for (SCVX_HIP_VERSION of include/scvx_hip.h): a library of
 # another revision would take these argument lists with shifted pointers, so lib() refuses it
-SCVX_HIP_VERSION = 5
+SCVX_HIP_VERSION = 6
 SCVX_MAX_BOX, SCVX_MAX_OBS, SCVX_MAX_NBR = 4, 16, 32
 SCVX_IS_MAX_PROJ, SCVX_IS_MAX_STATE = 3, 12
 MODEL_IDS = {"di": 0, "unicycle": 1, "si": 2, "quad": 3}
@@ -26,7 +26,8 @@ EXPORTS = ("scvx_version", "scvx_last_error", "scvx_foh_batched", "scvx_integrat
            "scvx_intersample_batched", "scvx_admm_consensus_batched", "scvx_scp_game_solve_batched",
            "scvx_slab_update_batched", "scvx_jacobi_update_batched", "scvx_rtc_model_create",
            "scvx_rtc_model_source", "scvx_rtc_model_log", "scvx_rtc_model_destroy", "scvx_rtc_foh_batched",
-           "scvx_rtc_integrate_nonlinear_batched", "scvx_rtc_subproblem_compile", "scvx_rtc_intersample_batched")
+           "scvx_rtc_integrate_nonlinear_batched", "scvx_rtc_subproblem_compile", "scvx_rtc_intersample_batched",
+           "scvx_jacobi_update_costs_batched", "scvx_jacobi_global_rule")
 SCVX_MAX_MODEL_PARAMS, SCVX_RTC_MAX_NX, SCVX_RTC_MAX_NU = 16, 16, 8
 
 
@@ -119,6 +120,8 @@ def lib():
         L.scvx_scp_game_solve_batched.argtypes = [ctypes.POINTER(SCPTemplate), i32] + [vp] * 18 + [vp, sz, vp]
         L.scvx_slab_update_batched.argtypes = [i32, i32, i32, i32, i32, vp, vp, vp, vp]
         L.scvx_jacobi_update_batched.argtypes = [i32, i32, i32, i32] + [vp] * 9 + [i32, dbl, dbl, vp]
+        L.scvx_jacobi_update_costs_batched.argtypes = [i32, i32, i32, i32] + [vp] * 8 + [vp]
+        L.scvx_jacobi_global_rule.argtypes = [i32, i32] + [vp] * 6 + [i32, dbl, vp]
         cpp = ctypes.POINTER(ctypes.c_char_p)
         L.scvx_rtc_model_create.argtypes = [i32, i32, cpp, cpp, cpp, ctypes.c_char_p, ctypes.POINTER(vp)]
         L.scvx_rtc_model_source.argtypes = [vp]

@@ -16,7 +16,7 @@ from dataclasses import dataclass
 from typing import Optional
 
 from . import (QPSolver, QPSpec, collision_check, collision_rows, collision_rows_indexed, default_nsub, foh_batched,
-               jacobi_update, model_dims)
+               jacobi_update, jacobi_update_global, model_dims)
 
 
 def balanced_order(iters, world):
@@ -64,6 +64,10 @@ class HipBackend:
     def jacobi_update(self, status, X_sol, U_sol, X, U, tr, prev_cost, grow, tr_max, tie_rtol=0.0):
         return jacobi_update(status, X_sol, U_sol, X, U, tr, prev_cost, grow=grow, tr_max=tr_max, tie_rtol=tie_rtol)
 
+    def jacobi_update_global(self, status, X_sol, U_sol, X, U, tr, prev_total, grow, tr_max, all_reduce=None):
+        return jacobi_update_global(status, X_sol, U_sol, X, U, tr, prev_total, grow=grow, tr_max=tr_max,
+                                    all_reduce=all_reduce)
+
 
 @dataclass
 class CouplingSpec:
@@ -94,8 +98,9 @@ class JacobiSCvx:
              only to rounding, so the reference's strict test would halve its radius on the rounding of
              the cost sum, differently for every summation order (the per-agent rule is this build's; the
              reference's global rule keeps the strict test).
-    fused_update: per-agent rule in one launch (csrc/jacobi.hip, default); False runs the same rules as
-             tensor ops.
+    fused_update: the bookkeeping in csrc/jacobi.hip (default): the per-agent rule in one launch, the global rule in two
+             (per-agent costs, then one workgroup sums them in a fixed order and applies the strict test; at world > 1
+             the local total is all-reduced in between); False runs the same rules as tensor ops.
     warm_start: each agent's QP starts from the primal-dual point of its previous solve when that one was
              optimal (QPSolver.solve(warm=...), include/scvx_hip.h): the next subproblem is the same agent's
              re-linearised at that solution.  The optimum and the stopping rule are unchanged; C3 needs
@@ -268,6 +273,15 @@ class JacobiSCvx:
             # one launch for the update, the cost rule and the failure rule (csrc/jacobi.hip)
             Xn, Un = fused(out["status"], out["X"], out["U"], X, U, self.tr, self.prev_cost, self.on_fail == "grow",
                            self.tr_max, self.tie_rtol)
+            self._mark(marks, "update")
+            return Xn, Un, out
+        fused_g = getattr(self.backend, "jacobi_update_global", None)
+        if self.fused_update and self.tr_rule == "global" and fused_g is not None:
+            ar = None
+            if self.world > 1:
+                ar = lambda t: torch.distributed.all_reduce(t, group=self.group)  # noqa: E731
+            Xn, Un = fused_g(out["status"], out["X"], out["U"], X, U, self.tr, self.prev_total, self.on_fail == "grow",
+                             self.tr_max, all_reduce=ar)
             self._mark(marks, "update")
             return Xn, Un, out
         failed = out["status"] == 2

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SCVX_HIP_VERSION 5
+#define SCVX_HIP_VERSION 6   /* 6: scvx_jacobi_update_costs_batched + scvx_jacobi_global_rule (the global rule fused) */
 
 #define SCVX_OK 0
 #define SCVX_EINVAL (-1)
@@ -450,6 +450,24 @@ int scvx_jacobi_update_batched(int N, int K, int n_x, int n_u, const int32_t* st
                                const double* U_sol, const double* X, const double* U, double* X_out, double* U_out,
                                double* tr, double* prev_cost, int grow, double tr_max, double tie_rtol,
                                void* stream);
+
+/*
+ * The same bookkeeping under the reference's GLOBAL trust-region rule (Distributed_opt/dist_scvx_3d.py:242-252:
+ * one radius, halved when the summed cost_fcn rises; ABI 6), in two calls:
+ *   scvx_jacobi_update_costs_batched: X_out / U_out as scvx_jacobi_update_batched, cost[i] = sum_{t<K-1}
+ *     ||U_out[i][t]||^2; the radii are not touched.
+ *   scvx_jacobi_global_rule: total = sum_i cost[i] (fixed summation order); mode 0 writes it to total_out only (a
+ *     rank's share, to be all-reduced by the caller), mode 1 sums and applies, mode 2 applies *total_in (the
+ *     all-reduced total).  Apply: tr[i] *= 0.5 for every agent if total > *prev_total (the reference's strict test),
+ *     then a failed agent's radius halves (grow = 0) or doubles (grow = 1, capped at tr_max); *prev_total = total
+ *     (and *total_out when given).
+ * Device buffers: cost / tr [N], status [N] int32, total_in / total_out / prev_total one double each.
+ */
+int scvx_jacobi_update_costs_batched(int N, int K, int n_x, int n_u, const int32_t* status, const double* X_sol,
+                                     const double* U_sol, const double* X, const double* U, double* X_out,
+                                     double* U_out, double* cost, void* stream);
+int scvx_jacobi_global_rule(int N, int mode, const int32_t* status, const double* cost, const double* total_in,
+                            double* total_out, double* tr, double* prev_total, int grow, double tr_max, void* stream);
 
 #ifdef __cplusplus
 }

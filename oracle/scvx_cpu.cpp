@@ -590,6 +590,19 @@ static void riccati_factor(const Agent& ag, const std::vector<Mat>& H, Riccati& 
             R.W[t] = chol_solve_mat(L, G);
             Mat C = mul(tr(G), R.W[t]);
             for (int a = 0; a < p; ++a) C(a, a) += 1.0 / R.Df[t][R.stiff[t][a]];
+            if (std::getenv("SCVX_TWIN_GJCHECK")) {   // experiment: the kernel's Gauss-Jordan pivots of C
+                Mat Cg = C;
+                for (int k = 0; k < p; ++k) {
+                    const double pv = Cg(k, k);
+                    if (!(pv > 0.0)) {
+                        std::fprintf(stderr, "GJ pivot %d of C at stage %d: %.3e (C diag %.3e %.3e off %.3e, D %.3e)\n", k, t, pv,
+                                     C(0, 0), p > 1 ? C(1, 1) : 0.0, p > 1 ? C(1, 0) : 0.0, R.Df[t][R.stiff[t][0]]);
+                        R.ok = false; return;
+                    }
+                    for (int j = 0; j < p; ++j) Cg(k, j) /= pv;
+                    for (int i = 0; i < p; ++i) if (i != k) { const double f = Cg(i, k); for (int j = 0; j < p; ++j) Cg(i, j) -= f * Cg(k, j); }
+                }
+            }
             if (!chol(C)) { R.ok = false; return; }
             R.LC[t] = C;
         }
@@ -1039,7 +1052,8 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out, const double*
     if (T->w_prox > 0.0)
         for (double v : ag.xref) cprox += T->w_prox * v * v;
     if (win) {
-        warm_point(ag, win, QP_WARM_ETA);
+        static const double eta_w = std::getenv("SCVX_WARM_ETA") ? std::atof(std::getenv("SCVX_WARM_ETA")) : QP_WARM_ETA;   // experiment knob
+        warm_point(ag, win, eta_w);
     } else if (!init_point(ag)) {
         iters_out = 0; obj_out = 0.0; return SCVX_STATUS_NUMERICAL;
     }
@@ -1486,7 +1500,9 @@ static int solve_agent(Agent& ag, int& iters_out, double& obj_out, const double*
             // the affine predictor takes a (nearly) full step -- the end game, where the fraction alone caps
             // the gap reduction per iteration at 1 / (1 - fraction).  SCVX_TAU_END: experiment knob
             static const double tau_end = std::getenv("SCVX_TAU_END") ? std::atof(std::getenv("SCVX_TAU_END")) : 0.99999;
-            const double eta = (aa >= 0.99) ? tau_end : 0.99;
+            static const double tau_aa = std::getenv("SCVX_TAU_AA") ? std::atof(std::getenv("SCVX_TAU_AA")) : 0.99;  // knob
+            static const double tau_mid = std::getenv("SCVX_TAU_MID") ? std::atof(std::getenv("SCVX_TAU_MID")) : 0.99;  // knob
+            const double eta = (aa >= tau_aa) ? tau_end : tau_mid;
             double al = std::min(1.0, eta * max_step(ds, dl, dsq, dlq));
             {   // the kernel's NaN / Inf probe of the direction (fail code 4): keep the current iterate
                 double pr = 0.0;

@@ -81,3 +81,72 @@ def test_driver_fused_and_tensor_paths_agree_on_20_bench_steps(cuda):
         assert torch.allclose(drv[0].prev_cost, drv[1].prev_cost, rtol=1e-13, atol=0), step
         halved = int((drv[0].tr < 0.25).sum().item())
     assert halved < 1024
+
+
+@pytest.mark.parametrize("grow,shrink", [(False, True), (False, False), (True, True)])
+def test_fused_global_rule_matches_tensor_rule(cuda, grow, shrink):
+    """The global rule fused (scvx_jacobi_update_costs_batched + scvx_jacobi_global_rule, ABI 6) against
+    JacobiSCvx's tensor form (scvx.py, tr_rule="global"): X / U bit-identical, every radius halved iff the summed
+    cost exceeds the previous total (dist_scvx_3d.py:250, strict), then the failure rule; the new total stored.
+    The previous total sits 1e-6 away from the new one, so the decision does not depend on the summation order;
+    also through the all-reduce path (mode 0 / 2) with an identity reduction."""
+    import torch
+    rng = np.random.default_rng(11)
+    N, K, n, m = 777, 50, 6, 3
+    t = lambda a: torch.tensor(a, device=cuda)  # noqa: E731
+    X, Xs = t(rng.normal(size=(N, K, n))), t(rng.normal(size=(N, K, n)))
+    U, Us = t(rng.normal(size=(N, K, m))), t(rng.normal(size=(N, K, m)))
+    status = t(rng.integers(0, 3, size=N).astype(np.int32))
+    failed = status == 2
+    ok = (~failed)[:, None, None]
+    Xr, Ur = torch.where(ok, Xs, X), torch.where(ok, Us, U)
+    total = float((Ur[:, :-1, :] ** 2).sum().item())
+    prev = t([total * (1 - 1e-6 if shrink else 1 + 1e-6)])
+    tr = t(rng.uniform(0.05, 0.5, size=N))
+    trr = tr * (0.5 if shrink else 1.0)
+    trr = (trr * (1.0 + failed.to(torch.float64))).clamp(max=0.4) if grow else trr * (1.0 - 0.5 * failed.to(torch.float64))
+    for ar in (None, lambda x: None):
+        tr_k, prev_k = tr.clone(), prev.clone()
+        Xk, Uk = scvx_hip.jacobi_update_global(status, Xs, Us, X, U, tr_k, prev_k, grow=grow, tr_max=0.4, all_reduce=ar)
+        assert torch.equal(Xk, Xr) and torch.equal(Uk, Ur)
+        assert torch.equal(tr_k, trr)
+        assert abs(prev_k.item() - total) <= 1e-13 * total
+
+
+def test_driver_fused_and_tensor_global_rule_agree_on_bench_steps(cuda):
+    """The headline loop (C3, bench.py's global rule) through JacobiSCvx with the fused global update and with the
+    tensor path for the bench's 25 steps: the radius, statuses and iterates bit-identical at every step where the
+    two totals take the same decision.  The totals are summed in different orders (a fixed tree against torch's
+    reduction), so they agree to ~1e-15 relative; a step whose total lies within 1e-12 of the previous one would be a
+    tie that either order may decide -- none occurs on this construction (asserted), so the whole run is identical."""
+    import torch
+    from scvx_hip import workloads
+    from scvx_hip.scvx import HipBackend, JacobiSCvx
+
+    class TensorPath(HipBackend):
+        jacobi_update_global = None
+
+    sc = workloads.synthetic_di(1024, K=50, seed=1, sigma=30.0, obstacles=8)
+    w = {k: torch.tensor(sc[k], device=cuda) for k in ("X", "U", "x_init", "x_final", "sigma")}
+    spec = scvx_hip.QPSpec(model="di", K=50, box=[(0, -12, 12), (1, -12, 12)], obs=sc["obs"], w_obs=1e6, u_max=1.0,
+                           max_iter=60)
+    drv = [JacobiSCvx(spec, w["x_init"], w["x_final"], w["sigma"], 0.25, tr_rule="global", warm_max_status=1,
+                      backend=b) for b in (HipBackend(), TensorPath())]
+    it = [[w["X"].clone(), w["U"].clone()] for _ in drv]
+    prev = float("inf")
+    halvings = 0
+    for step in range(25):
+        outs = []
+        for d, s_ in zip(drv, it):
+            s_[0], s_[1], o = d.step(s_[0], s_[1])
+            outs.append(o["status"].clone())
+        tot = [float(d.prev_total.item()) for d in drv]
+        assert abs(tot[0] - tot[1]) <= 1e-13 * tot[1], step
+        if prev != float("inf"):
+            assert abs(tot[1] - prev) > 1e-12 * prev, (step, "tie")
+            halvings += int(tot[1] > prev)
+        prev = tot[1]
+        assert torch.equal(outs[0], outs[1]), step
+        assert torch.equal(it[0][0], it[1][0]) and torch.equal(it[0][1], it[1][1]), step
+        assert torch.equal(drv[0].tr, drv[1].tr), step
+    assert halvings >= 1   # the rule fired on this run
