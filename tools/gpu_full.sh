@@ -14,6 +14,6 @@ timeout -k 10 300 python -u bench.py > gpurun_out/bench_$TAG.log 2>&1
 timeout -k 10 300 python -u bench.py --config c2 > gpurun_out/bench_c2_$TAG.log 2>&1
 timeout -k 10 300 python -u bench.py --config c4 --no-cpu > gpurun_out/bench_c4_$TAG.log 2>&1
 timeout -k 10 300 python -u bench.py --config c5 --no-cpu > gpurun_out/bench_c5_$TAG.log 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 -u bench.py --no-cpu --steps 10 --warmup 3 > gpurun_out/bench_prof_$TAG.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 -u bench.py --no-cpu --rules one --steps 10 --warmup 3 > gpurun_out/bench_prof_$TAG.log 2>&1
 timeout -k 10 60 rocprofv3 -L > gpurun_out/counters_list.txt 2>&1 || true
 echo done
