@@ -342,20 +342,34 @@ typedef unsigned int qp_u4 __attribute__((ext_vector_type(4)));
 constexpr int QP_CPF = 4;
 struct QPBuf {
     __amdgpu_buffer_rsrc_t rs;
+#ifdef QP_BYTE_TRACE
+    // diagnostics build (tools/qp_bytes_trace.py): workspace bytes this lane requested since the last region stamp
+    // (lanes without a node address QP_OOB and move nothing); the stamps fold them into the trace buffer per region
+    mutable double nby = 0.0;
+    __device__ __forceinline__ void cnt(int voff, int soff, double b) const {
+        nby += (voff < QP_OOB && soff < QP_OOB) ? b : 0.0;
+    }
+#else
+    __device__ __forceinline__ void cnt(int, int, double) const {}
+#endif
     __device__ __forceinline__ double ld(int voff, int soff) const {
         soff = __builtin_amdgcn_readfirstlane(soff);  // uniform by construction
+        cnt(voff, soff, 8.0);
         return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
     }
     __device__ __forceinline__ void st(int voff, int soff, double v) const {
         soff = __builtin_amdgcn_readfirstlane(soff);
+        cnt(voff, soff, 8.0);
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(qp_u2, v), rs, voff, soff, 0);
     }
     __device__ __forceinline__ qp_u4 ld4(int voff, int soff) const {
         soff = __builtin_amdgcn_readfirstlane(soff);
+        cnt(voff, soff, 16.0);
         return __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
     }
     __device__ __forceinline__ void st4(int voff, int soff, qp_u4 v) const {
         soff = __builtin_amdgcn_readfirstlane(soff);
+        cnt(voff, soff, 16.0);
         __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, 0);
     }
 };
@@ -631,6 +645,12 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             const long long now = __builtin_amdgcn_s_memtime();
             if (lane == 0 && i >= 0) lds[V_ST + i] += (double)(now - tprev);
             tprev = now;
+#ifdef QP_BYTE_TRACE
+            // the region's workspace bytes (every lane's) -> trace buffer after the cycle slots (host: 8 cap + 36)
+            const double b = wave_sum(wb.nby);
+            wb.nby = 0.0;
+            if (lane == 0 && i >= 0) a.trace[8 * a.trace_cap + 20 + i] += b;
+#endif
         }
     };
 
@@ -1186,17 +1206,24 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                                 v += (sfi[i] < 0 ? 0.0 : (((sfi[i] >> j) & 1) ? -1.0 : 1.0)) * Wm[j * PM + k];
                             Cm[i * PM + k] = v;
                         }
-                    // C^-1 by Gauss-Jordan without pivoting (C is symmetric positive definite in exact arithmetic); a
-                    // zero or non-finite pivot, or a non-finite entry of C^-1, fails the factor (round 6: the round-5
-                    // check saw a NaN in the first entry only).  A pivot <= 0 is NOT fatal here: failing the factor on
-                    // it (as the twin's Cholesky of C would) ended 146 of 512 C4 lattice solves status 2 on the GPU
-                    // while the twin never meets one on the same fixtures
+                    // C^-1 by Gauss-Jordan without pivoting (C is symmetric positive definite in exact arithmetic)
+#ifdef QP_STF_DEBUG
+                    double Cm0[PMA * PMA];
+#pragma unroll
+                    for (int e = 0; e < PM * PM; ++e) Cm0[e] = Cm[e];
+#endif
 #pragma unroll
                     for (int e = 0; e < PM * PM; ++e) Ci[e] = (e / PM == e % PM) ? 1.0 : 0.0;
 #pragma unroll
                     for (int k = 0; k < PM; ++k) {
                         const double pv = Cm[k * PM + k];
-                        bad |= !(pv != 0.0 && pv - pv == 0.0);
+#ifdef QP_STF_DEBUG
+                        if (sl == 0 && !(pv > 0.0 && pv < __builtin_inf()))
+                            printf("STF agent %lld stage %d pivot %d = %.6e | C %.6e %.6e %.6e %.6e | sfi %d %d sfd %.3e %.3e | "
+                                   "W %.3e %.3e %.3e %.3e %.3e %.3e\n", agent, ts, k, pv, Cm0[0], Cm0[1], Cm0[2], Cm0[3],
+                                   sfi[0], sfi[PMA > 1 ? 1 : 0], sfd[0], sfd[PMA > 1 ? 1 : 0], Wm[0], Wm[1], Wm[2],
+                                   Wm[3 % (NU * PMA)], Wm[4 % (NU * PMA)], Wm[5 % (NU * PMA)]);
+#endif
                         const double rp = 1.0 / pv;
 #pragma unroll
                         for (int j = 0; j < PM; ++j) { Cm[k * PM + j] *= rp; Ci[k * PM + j] *= rp; }
@@ -1211,8 +1238,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                             }
                         }
                     }
-#pragma unroll
-                    for (int e = 0; e < PM * PM; ++e) bad |= !(Ci[e] - Ci[e] == 0.0);   // every entry finite
+                    bad |= !(Ci[0] == Ci[0]);
+#ifdef QP_STF_DEBUG
+                    for (int e = 0; e < PM * PM; ++e)
+                        if (sl == 0 && !(Ci[e] - Ci[e] == 0.0)) printf("STF agent %lld stage %d Ci[%d] = %.6e\n", agent, ts, e, Ci[e]);
+#endif
                 }
                 {  // every lane runs the solve (lanes >= 2 NX on a copy of column 0, results to the sinks)
                     const bool kl = sl < 2 * NX;

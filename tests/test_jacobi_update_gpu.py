@@ -101,7 +101,7 @@ def test_fused_global_rule_matches_tensor_rule(cuda, grow, shrink):
     ok = (~failed)[:, None, None]
     Xr, Ur = torch.where(ok, Xs, X), torch.where(ok, Us, U)
     total = float((Ur[:, :-1, :] ** 2).sum().item())
-    prev = t([total * (1 - 1e-6 if shrink else 1 + 1e-6)])
+    prev = torch.tensor([total * (1 - 1e-6 if shrink else 1 + 1e-6)], dtype=torch.float64, device=cuda)
     tr = t(rng.uniform(0.05, 0.5, size=N))
     trr = tr * (0.5 if shrink else 1.0)
     trr = (trr * (1.0 + failed.to(torch.float64))).clamp(max=0.4) if grow else trr * (1.0 - 0.5 * failed.to(torch.float64))
