@@ -9,8 +9,13 @@
 
 namespace scvx {
 
+// FOH_MIN_WAVES: minimum waves per SIMD the register allocation must allow (diagnostics A/B; the quadrotor's kernel
+// takes 356 of 512 registers, one wave per SIMD)
+#ifndef FOH_MIN_WAVES
+#define FOH_MIN_WAVES 1
+#endif
 template <class Mdl>
-__global__ __launch_bounds__(256) void foh_kernel(const double* __restrict__ X, const double* __restrict__ U,
+__global__ __launch_bounds__(256, FOH_MIN_WAVES) void foh_kernel(const double* __restrict__ X, const double* __restrict__ U,
                                                   const double* __restrict__ sigma, double* __restrict__ out,
                                                   int K, int N, int nsub, ModelParams P) {
     __shared__ double stage[256 * Mdl::N];

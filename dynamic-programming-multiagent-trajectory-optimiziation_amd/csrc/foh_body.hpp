@@ -36,8 +36,16 @@
 #ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
 #endif
+#include <type_traits>
 
 namespace scvx {
+
+// a model may provide fab(x, u, v, w, f_out, Av_out, Bw_out, P): f, (df/dx) v and (df/du) w in one call sharing its
+// common subexpressions (the quadrotor's sines and cosines); the integrator then calls it instead of f, Av, Bw
+template <class M, class = void>
+struct foh_has_fab : std::false_type {};
+template <class M>
+struct foh_has_fab<M, std::void_t<decltype(&M::fab)>> : std::true_type {};
 
 #define SCVX_MAX_MODEL_PARAMS 16
 
@@ -87,11 +95,15 @@ __device__ __forceinline__ void foh_body(const double* __restrict__ X, const dou
             const double e = (j == jcol) ? 1.0 : 0.0;
             w[j] = isB ? alpha * e : (isC ? beta * e : -dZ * u[j]);
         }
-        Mdl::f(xs, u, fv, P);
 #pragma unroll
         for (int i = 0; i < n; ++i) tmp[i] = cs[i] - dZ * xs[i];
-        Mdl::Av(xs, u, tmp, Aw, P);
-        Mdl::Bw(xs, u, w, Bwv, P);
+        if constexpr (foh_has_fab<Mdl>::value) {
+            Mdl::fab(xs, u, tmp, w, fv, Aw, Bwv, P);
+        } else {
+            Mdl::f(xs, u, fv, P);
+            Mdl::Av(xs, u, tmp, Aw, P);
+            Mdl::Bw(xs, u, w, Bwv, P);
+        }
 #pragma unroll
         for (int i = 0; i < n; ++i) {
             dx[i] = s * fv[i];

@@ -124,6 +124,48 @@ struct Quadrotor12 {
         o[6] = 0.0; o[7] = 0.0; o[8] = 0.0;
         o[9] = w[1] / Jx; o[10] = w[2] / Jy; o[11] = w[3] / Jz;
     }
+    // f, (df/dx) v and (df/du) w at one (x, u) with one set of sines / cosines and reciprocals (the FOH's right-hand
+    // side evaluates all three at every RK4 stage: three separate calls cost nine FP64 sincos, each a range reduction
+    // and two polynomials).  The same expressions as f / Av / Bw above, term for term.
+    __device__ __forceinline__ static void fab(const double* x, const double* u, const double* v, const double* wv,
+                                               double* fo, double* ao, double* bo, const ModelParams& P) {
+        const double mass = P.p[0], g = P.p[1], Jx = P.p[2], Jy = P.p[3], Jz = P.p[4];
+        double sf, cf, st, ct, sp, cp;
+        sincos(x[6], &sf, &cf);
+        sincos(x[7], &st, &ct);
+        sincos(x[8], &sp, &cp);
+        const double p = x[9], q = x[10], r = x[11], a = u[0] / mass;
+        const double r1 = cf * st * cp + sf * sp, r2 = cf * st * sp - sf * cp, r3 = cf * ct;
+        const double w = q * sf + r * cf, wd = q * cf - r * sf;
+        fo[0] = x[3]; fo[1] = x[4]; fo[2] = x[5];
+        fo[3] = a * r1;
+        fo[4] = a * r2;
+        fo[5] = a * r3 - g;
+        fo[6] = p + w * st / ct;
+        fo[7] = q * cf - r * sf;
+        fo[8] = w / ct;
+        fo[9] = (u[1] + (Jy - Jz) * q * r) / Jx;
+        fo[10] = (u[2] + (Jz - Jx) * p * r) / Jy;
+        fo[11] = (u[3] + (Jx - Jy) * p * q) / Jz;
+        const double tt = st / ct, ic = 1.0 / ct;
+        ao[0] = v[3]; ao[1] = v[4]; ao[2] = v[5];
+        ao[3] = a * ((-sf * st * cp + cf * sp) * v[6] + (cf * ct * cp) * v[7] + (-cf * st * sp + sf * cp) * v[8]);
+        ao[4] = a * ((-sf * st * sp - cf * cp) * v[6] + (cf * ct * sp) * v[7] + (cf * st * cp + sf * sp) * v[8]);
+        ao[5] = a * ((-sf * ct) * v[6] + (-cf * st) * v[7]);
+        ao[6] = wd * tt * v[6] + w * ic * ic * v[7] + v[9] + sf * tt * v[10] + cf * tt * v[11];
+        ao[7] = -w * v[6] + cf * v[10] - sf * v[11];
+        ao[8] = wd * ic * v[6] + w * st * ic * ic * v[7] + sf * ic * v[10] + cf * ic * v[11];
+        ao[9] = (Jy - Jz) / Jx * (r * v[10] + q * v[11]);
+        ao[10] = (Jz - Jx) / Jy * (r * v[9] + p * v[11]);
+        ao[11] = (Jx - Jy) / Jz * (q * v[9] + p * v[10]);
+        const double t = wv[0] / mass;
+        bo[0] = 0.0; bo[1] = 0.0; bo[2] = 0.0;
+        bo[3] = t * r1;
+        bo[4] = t * r2;
+        bo[5] = t * r3;
+        bo[6] = 0.0; bo[7] = 0.0; bo[8] = 0.0;
+        bo[9] = wv[1] / Jx; bo[10] = wv[2] / Jy; bo[11] = wv[3] / Jz;
+    }
 };
 
 // host-side: parameter block of a model id (quadrotor defaults: mass 1, g 9.81, J = diag(.02,.02,.04))

@@ -2546,6 +2546,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
         double wl[NR];
         ldn(wl, C::C_WL, NR);
         hold(wl, NR);
+        // the slack-relative dual floor, except in the classes with the stiff-facet stage system (the coupled double /
+        // single integrators: there it lengthened the C4 tail; the twin the same)
+        const bool kfl = !(C::STF && has_coll);
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
             double gz, h;
@@ -2553,7 +2556,7 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
             const bool on = row_on(r);
             const double sr = fmax(h - gz, QP_WARM_ETA);
             s_set(r, on ? sr : 1.0);
-            l_set(r, on ? fmax(wl[r], fmin(QP_WARM_ETA, QP_WARM_KAPPA / sr)) : 0.0);
+            l_set(r, on ? fmax(wl[r], kfl ? fmin(QP_WARM_ETA, QP_WARM_KAPPA / sr) : QP_WARM_ETA) : 0.0);
         }
         if (soc) {
             double nu2 = 0.0, nl2 = 0.0;

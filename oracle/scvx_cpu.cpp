@@ -996,8 +996,12 @@ static void warm_point(Agent& ag, const double* w, double eta) {
     const double ks = ek ? std::atof(ek) : 0.0, kl = el ? std::atof(el) : 0.0;
     // a row's dual floor is min(eta, QP_WARM_KAPPA / s) at its floored slack s (kernel: the same rule): a row with a
     // large slack keeps a small dual.  SCVX_WARM_KAPPA: experiment knob (0: the round-5 floor eta for every dual)
+    // The floor applies to the classes without the stiff-facet stage system (kernel: !(C::STF && has_coll)): on the
+    // C4 loop (coupled double integrators) it lengthened the tail (max 32-41 -> 46-60 IPM iterations per step) and
+    // ended three warm solves status 2 (profiles/round6_r6c_*), while the C3 (uncoupled) and C5 (quadrotor) loops gain.
     const char* ekap = std::getenv("SCVX_WARM_KAPPA");
-    const double kap = ekap ? std::atof(ekap) : QP_WARM_KAPPA;
+    const bool stf = T->j_max > 0 && n <= 8 && m >= 2 && m <= 4;
+    const double kap = stf ? 0.0 : (ekap ? std::atof(ekap) : QP_WARM_KAPPA);
     for (int t = 0; t < K; ++t) {
         Node& N = ag.nd[t];
         const double* o = w + (size_t)t * st;
