@@ -71,7 +71,8 @@ class _CpuQP:
 
     def solve(self, disc, sigma, Xref, Uref, x_init, x_final, tr, rows=None, count=None, n=None, warm=None):
         o = qp_cpu.solve_batched(self.tpl, disc.numpy(), sigma.numpy(), Xref.numpy(), Uref.numpy(), x_init.numpy(),
-                                 x_final.numpy(), tr.numpy(), rows.numpy(), count.numpy())
+                                 x_final.numpy(), tr.numpy(), None if rows is None else rows.numpy(),
+                                 None if count is None else count.numpy())
         return {k: torch.from_numpy(np.asarray(v)) for k, v in o.items()}
 
 
@@ -258,3 +259,54 @@ def test_world4_culled_coupling_matches_single_process(balanced):
     for k in range(ITERS):
         for key in ("violated", "resolved", "overflow"):
             assert sum(res[r][2][k][key] for r in range(4)) == ck_single[k][key], (k, key)
+
+
+def _run_indep(rank, world, port, q):
+    """The headline's C3 form: independent agents (no coupling), the reference's global trust-region rule over every
+    rank's agents (one scalar all_reduce per step, JacobiSCvx tensor path; the fused kernel path does the same with a
+    fixed-order local sum, tests/test_jacobi_update_gpu.py)."""
+    import scvx_hip
+    from scvx_hip.scvx import JacobiSCvx
+    if world > 1:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    sc = pb.synthetic_di(N_TOTAL, K=K, seed=7, spread=6.0)
+    n_loc = N_TOTAL // world
+    sl = slice(rank * n_loc, (rank + 1) * n_loc)
+    T = lambda a: torch.tensor(np.ascontiguousarray(a))  # noqa: E731
+    spec = scvx_hip.QPSpec(model="di", K=K, box=[(0, -20, 20)], tol=1e-10, max_iter=80)
+    drv = JacobiSCvx(spec, T(sc["x_init"][sl]), T(sc["x_final"][sl]), T(sc["sigma"][sl]), 0.3, tr_rule="global",
+                     backend=OracleBackend())
+    X, U = T(sc["X"][sl]).clone(), T(sc["U"][sl]).clone()
+    totals = []
+    for _ in range(ITERS + 1):
+        X, U, out = drv.step(X, U)
+        X, U = X.clone(), U.clone()
+        totals.append(float(drv.prev_total.item()))
+    q.put((rank, X.numpy(), drv.tr.numpy(), totals, int(out["status"].max())))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def test_sharded_global_rule_independent_agents_matches_single_process():
+    """bench.py's default line at --gpus 2 (C3 form: every rank its own agents, the global rule's summed cost
+    all-reduced): world 2 (gloo) against one process owning all agents -- the same totals (to the summation order's
+    rounding), the same radius and the same iterates at every step."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    _run_indep(0, 1, 0, q)
+    _, X_single, tr_single, tot_single, st = q.get()
+    assert st == 0
+    port = _free_port()
+    procs = [ctx.Process(target=_run_indep, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (x, tr, tot, s)) for r, x, tr, tot, s in (q.get(timeout=300) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    np.testing.assert_allclose(res[0][2], tot_single, rtol=1e-13)
+    np.testing.assert_allclose(res[1][2], tot_single, rtol=1e-13)
+    np.testing.assert_array_equal(np.concatenate([res[0][1], res[1][1]]), tr_single)
+    np.testing.assert_array_equal(np.concatenate([res[0][0], res[1][0]]), X_single)
+    assert all(res[r][3] == 0 for r in res)

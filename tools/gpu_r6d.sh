@@ -17,4 +17,6 @@ SCVX_HIP_LIB=variants/stfdebug/libscvx_hip.so timeout -k 10 300 python -u -m pyt
 SCVX_HIP_LIB=variants/bytetrace/libscvx_hip.so WHO=bulk timeout -k 10 200 python -u tools/qp_bytes_trace.py 10 gpurun_out/bytes_bulk_$T.json > gpurun_out/bytes_bulk_$T.log 2>&1
 SCVX_HIP_LIB=variants/bytetrace/libscvx_hip.so WHO=tail timeout -k 10 200 python -u tools/qp_bytes_trace.py 10 gpurun_out/bytes_tail_$T.json > gpurun_out/bytes_tail_$T.log 2>&1
 timeout -k 10 120 tools/ubench/mfma_stage > gpurun_out/mfma_stage_$T.log 2>&1
+timeout -k 10 200 python -u tools/qp_div_accuracy.py > gpurun_out/qpdiv_intree_$T.log 2>&1
+SCVX_HIP_LIB=variants/exactdiv/libscvx_hip.so timeout -k 10 200 python -u tools/qp_div_accuracy.py > gpurun_out/qpdiv_exact_$T.log 2>&1
 echo done
