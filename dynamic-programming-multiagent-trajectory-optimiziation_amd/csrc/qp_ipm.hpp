@@ -1128,6 +1128,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                     }
                     }
                 }
+#ifdef QP_STF_DEBUG
+                double Lm0[NU * NU];
+#pragma unroll
+                for (int e = 0; e < NU * NU; ++e) Lm0[e] = Lm[e];
+#endif
                 double dmax = 0.0;
 #pragma unroll
                 for (int j = 0; j < NU; ++j) dmax = fmax(dmax, fabs(Lm[j * NU + j]));
@@ -1218,11 +1223,24 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                     for (int k = 0; k < PM; ++k) {
                         const double pv = Cm[k * PM + k];
 #ifdef QP_STF_DEBUG
-                        if (sl == 0 && !(pv > 0.0 && pv < __builtin_inf()))
+                        if (sl == 0 && !(pv > 0.0 && pv < __builtin_inf())) {
                             printf("STF agent %lld stage %d pivot %d = %.6e | C %.6e %.6e %.6e %.6e | sfi %d %d sfd %.3e %.3e | "
                                    "W %.3e %.3e %.3e %.3e %.3e %.3e\n", agent, ts, k, pv, Cm0[0], Cm0[1], Cm0[2], Cm0[3],
                                    sfi[0], sfi[PMA > 1 ? 1 : 0], sfd[0], sfd[PMA > 1 ? 1 : 0], Wm[0], Wm[1], Wm[2],
                                    Wm[3 % (NU * PMA)], Wm[4 % (NU * PMA)], Wm[5 % (NU * PMA)]);
+                            printf("STF agent %lld stage %d R0 (folded, before LDL) %.6e %.6e %.6e | %.6e %.6e %.6e | %.6e %.6e %.6e"
+                                   " | Rhat %.6e %.6e %.6e %.6e %.6e %.6e %.6e %.6e %.6e | dinv %.6e %.6e %.6e | L %.6e %.6e %.6e\n",
+                                   agent, ts, Lm0[0], Lm0[1 % (NU * NU)], Lm0[2 % (NU * NU)], Lm0[3 % (NU * NU)],
+                                   Lm0[4 % (NU * NU)], Lm0[5 % (NU * NU)], Lm0[6 % (NU * NU)], Lm0[7 % (NU * NU)],
+                                   Lm0[8 % (NU * NU)], lds[C::F_RH + 0], lds[C::F_RH + 1], lds[C::F_RH + 2],
+                                   lds[C::F_RH + 3], lds[C::F_RH + 4 % (NU * NU)], lds[C::F_RH + 5 % (NU * NU)],
+                                   lds[C::F_RH + 6 % (NU * NU)], lds[C::F_RH + 7 % (NU * NU)], lds[C::F_RH + 8 % (NU * NU)], dinv[0],
+                                   dinv[1 % NU], dinv[2 % NU], Lm[3 % (NU * NU)], Lm[6 % (NU * NU)], Lm[7 % (NU * NU)]);
+                            double Df8[8];
+                            for (int f = 0; f < 8; ++f) Df8[f] = f < C::NTR ? lds[C::F_RING + C::P_FD + f] : 0.0;
+                            printf("STF agent %lld stage %d facets D %.3e %.3e %.3e %.3e %.3e %.3e %.3e %.3e\n", agent, ts,
+                                   Df8[0], Df8[1], Df8[2], Df8[3], Df8[4], Df8[5], Df8[6], Df8[7]);
+                        }
 #endif
                         const double rp = 1.0 / pv;
 #pragma unroll

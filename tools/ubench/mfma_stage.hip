@@ -27,9 +27,9 @@ __global__ __launch_bounds__(64) void k_valu(const double* A, const double* M0, 
     const int l = threadIdx.x;
     for (int e = l; e < 256; e += 64) { At[e] = A[e]; M[0][e] = M0[e]; M[1][e] = 0.0; }
     __syncthreads();
-    // column-major copies make every dot product two contiguous vectors (the QP kernel's packet layout)
-    __shared__ double Acm[256], Mcm[2][256];
-    for (int e = l; e < 256; e += 64) { Acm[e] = At[(e % 16) * 16 + e / 16]; Mcm[0][e] = M[0][(e % 16) * 16 + e / 16]; }
+    // a column-major copy of M makes every dot product two contiguous vectors (the QP kernel's packet layout)
+    __shared__ double Mcm[2][256];
+    for (int e = l; e < 256; e += 64) { Mcm[0][e] = M[0][(e % 16) * 16 + e / 16]; Mcm[1][e] = 0.0; }
     __syncthreads();
     long long t0 = __builtin_amdgcn_s_memtime();
     for (int s = 0; s < n; ++s) {
@@ -39,8 +39,8 @@ __global__ __launch_bounds__(64) void k_valu(const double* A, const double* M0, 
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
             const int o = l + 64 * r, oo = o < 144 ? o : 0, i = oo / 12, j = oo % 12;
-            const double* a = Acm + i * 16;   // row i of A' = column i of A ... stored contiguous
-            const double* b = src + j * 16;   // column j of M
+            const double* a = At + i * 16;    // row i of A' (row-major At: contiguous)
+            const double* b = src + j * 16;   // column j of M (column-major copy: contiguous)
             double a0 = 0.0, a1 = 0.0;
 #pragma unroll
             for (int k = 0; k < 12; ++k) { if (k & 1) a1 = fma(a[k], b[k], a1); else a0 = fma(a[k], b[k], a0); }
