@@ -124,7 +124,11 @@ int main() {
                 if (n == 6) {
                     cpu_ref(A, M0, n, R);
                     double err = 0.0, ref = 0.0;
-                    for (int e = 0; e < 256; ++e) { err = std::fmax(err, std::fabs(O[e] - R[e])); ref = std::fmax(ref, std::fabs(R[e])); }
+                    for (int e = 0; e < 256; ++e) {   // the 12 x 12 block (the VALU form parks its idle lanes' stores in (15, 15))
+                        if (e / 16 >= 12 || e % 16 >= 12) continue;
+                        err = std::fmax(err, std::fabs(O[e] - R[e]));
+                        ref = std::fmax(ref, std::fabs(R[e]));
+                    }
                     printf("%s: 6 chained products, max |err| %.2e of max |M| %.2e\n", v ? "mfma" : "valu", err, ref);
                     continue;
                 }
