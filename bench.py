@@ -573,33 +573,32 @@ def timed_leg(drv, w, args, world, device):
         it_state[0], it_state[1], out = drv.step(it_state[0], it_state[1], marks=marks)
         return out
 
-    status_ids = torch.arange(3, device=device, dtype=torch.int32)
+    hist = torch.empty((max(args.steps, 1), 2, w["X"].shape[0]), dtype=torch.int32, device=device)
 
-    def record(out, iters, iters_max, stats):
-        """Per-step device-side bookkeeping of the timed region (no host sync): summed and max IPM iterations,
-        status counts.  The warmup runs it too, so no torch kernel is loaded for the first time inside the
-        timed region (a first use costs ~40-180 ms of module loading on a fresh box)."""
-        iters.append(out["iters"].sum())
-        iters_max.append(out["iters"].max())
-        stats.append((out["status"][:, None] == status_ids).sum(dim=0))   # no sync (bincount would sync)
+    def record(out, i):
+        """Per-step device-side bookkeeping of the timed region: ONE launch copies the step's IPM iteration counts
+        and statuses into slot i of `hist` (reduced on the host after the timed region; no host sync inside it).  The
+        warmup runs it too, so no torch kernel is loaded for the first time inside the timed region (a first use
+        costs ~40-180 ms of module loading on a fresh box)."""
+        torch.stack((out["iters"], out["status"]), out=hist[i])
 
     for _ in range(args.warmup):
         out = step()
-        record(out, [], [], [])
+        record(out, 0)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    marks, iters, iters_max, checks, stats = [], [], [], [], []
+    marks, checks = [], []
     t0 = time.perf_counter()
     host_ms = []
-    for _ in range(args.steps):
+    for i in range(args.steps):
         mk = []
         th = time.perf_counter()
         out = step(mk)
         host_ms.append(1e3 * (time.perf_counter() - th))
         marks.append(mk)
-        record(out, iters, iters_max, stats)
+        record(out, i)
         if drv.last_check is not None:
             checks.append(dict(drv.last_check))
     torch.cuda.synchronize()
@@ -619,26 +618,27 @@ def timed_leg(drv, w, args, world, device):
         per_rank = [r.tolist() for r in allr]
     else:
         per_rank = None
-    status = out["status"].cpu()
-    its = out["iters"].cpu().numpy()
+    h = hist[:args.steps].cpu().numpy()   # (steps, 2, N): IPM iterations, status
+    its, status = h[-1, 0], h[-1, 1]
     N = its.size
+    stats = [[int((h[i, 1] == k).sum()) for k in (0, 1, 2)] for i in range(args.steps)]
     return dict(
         el=el_t.item(), st_ms=st_ms, step_ms=step_ms, per_rank=per_rank, host_ms=host_ms, checks=checks,
-        ipm_iters=float(torch.stack(iters).sum().item()),
+        ipm_iters=float(h[:, 0].sum()),
         fields={
             "ms_per_step_median": float(np.median(step_ms)),
             "stage_ms_median": st_ms,
             "stage_ms_per_rank": per_rank,
-            "ipm_iters_per_agent": float(torch.stack(iters).sum().item()) / (args.steps * N),
+            "ipm_iters_per_agent": float(h[:, 0].sum()) / (args.steps * N),
             "ipm_iters_max_last": int(its.max()),
             "ipm_iters_hist_last": {str(int(v)): int(c) for v, c in zip(*np.unique(its, return_counts=True))},
             "status_counts": {str(k): int((status == k).sum()) for k in (0, 1, 2)},
-            "status_counts_per_step": [[int(v) for v in c.tolist()[:3]] for c in stats],
+            "status_counts_per_step": stats,
             "step_ms": [round(v, 4) for v in step_ms],
             "host_ms_per_step": [round(v, 4) for v in host_ms],
             "gap_ms_between_steps": [round(a[-1][1].elapsed_time(b[0][1]), 4) for a, b in zip(marks[:-1], marks[1:])],
-            "ipm_iters_max_per_step": [int(v) for v in torch.stack(iters_max).tolist()],
-            "min_frac_status_0_1": min(float((c[0] + c[1]).item()) / N for c in stats),
+            "ipm_iters_max_per_step": [int(v) for v in h[:, 0].max(axis=1)],
+            "min_frac_status_0_1": min((c[0] + c[1]) / N for c in stats),
             "coupling_check": checks or None,
         })
 

@@ -136,6 +136,7 @@ class JacobiSCvx:
         self.tie_rtol = float(tie_rtol)
         self.warm_start = warm_start and spec.K >= 2 * model_dims(spec.model)[0]
         self.warm = None   # (N,) int32 device: the previous solve of the agent qualifies as a warm start
+        self._warm_buf = None
         self.warm_max_status = int(warm_max_status)
         if dispatch_order not in ("lpt", "none"):
             raise ValueError(f"dispatch_order must be 'lpt' or 'none', not {dispatch_order!r}")
@@ -256,8 +257,10 @@ class JacobiSCvx:
         kw = {"order": self.order} if self.order is not None else {}
         out = self.solver.solve(self.disc, self.sigma, X, U, self.x_init, self.x_final, self.tr, rows, count,
                                 warm=self.warm, **kw)
-        if self.warm_start:
-            self.warm = (out["status"] <= self.warm_max_status).to(torch.int32)
+        if self.warm_start:   # one launch: the comparison written straight into the int32 flag buffer
+            if self._warm_buf is None:
+                self._warm_buf = torch.empty((self.N,), dtype=torch.int32, device=self.device)
+            self.warm = torch.le(out["status"], self.warm_max_status, out=self._warm_buf)
         if self._lpt and getattr(self.solver, "supports_order", False):
             self.order = torch.argsort(out["iters"], descending=True, stable=True).to(torch.int32)
         self._mark(marks, "qp")
