@@ -1211,7 +1211,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                                 v += (sfi[i] < 0 ? 0.0 : (((sfi[i] >> j) & 1) ? -1.0 : 1.0)) * Wm[j * PM + k];
                             Cm[i * PM + k] = v;
                         }
-                    // C^-1 by Gauss-Jordan without pivoting (C is symmetric positive definite in exact arithmetic)
+                    // C^-1 by Gauss-Jordan without pivoting (C is symmetric positive definite in exact arithmetic); a
+                    // pivot that is not positive and finite, or a non-finite entry of C^-1, fails the factor, as the
+                    // twin's Cholesky of C does (oracle/scvx_cpu.cpp riccati_factor).  Written with __builtin_isfinite:
+                    // the same tests written as x - x == 0 / x < inf reported finite entries as non-finite in this
+                    // kernel's code (round 6)
 #ifdef QP_STF_DEBUG
                     double Cm0[PMA * PMA];
 #pragma unroll
@@ -1222,8 +1226,9 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
 #pragma unroll
                     for (int k = 0; k < PM; ++k) {
                         const double pv = Cm[k * PM + k];
+                        bad |= !(pv > 0.0 && __builtin_isfinite(pv));   // as the twin's Cholesky of C
 #ifdef QP_STF_DEBUG
-                        if (sl == 0 && !(pv > 0.0 && pv < __builtin_inf())) {
+                        if (sl == 0 && !(pv > 0.0 && __builtin_isfinite(pv))) {
                             printf("STF agent %lld stage %d pivot %d = %.6e | C %.6e %.6e %.6e %.6e | sfi %d %d sfd %.3e %.3e | "
                                    "W %.3e %.3e %.3e %.3e %.3e %.3e\n", agent, ts, k, pv, Cm0[0], Cm0[1], Cm0[2], Cm0[3],
                                    sfi[0], sfi[PMA > 1 ? 1 : 0], sfd[0], sfd[PMA > 1 ? 1 : 0], Wm[0], Wm[1], Wm[2],
@@ -1256,10 +1261,11 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                             }
                         }
                     }
-                    bad |= !(Ci[0] == Ci[0]);
+#pragma unroll
+                    for (int e = 0; e < PM * PM; ++e) bad |= !__builtin_isfinite(Ci[e]);
 #ifdef QP_STF_DEBUG
                     for (int e = 0; e < PM * PM; ++e)
-                        if (sl == 0 && !(Ci[e] - Ci[e] == 0.0)) printf("STF agent %lld stage %d Ci[%d] = %.6e\n", agent, ts, e, Ci[e]);
+                        if (sl == 0 && !__builtin_isfinite(Ci[e])) printf("STF agent %lld stage %d Ci[%d] = %.6e\n", agent, ts, e, Ci[e]);
 #endif
                 }
                 {  // every lane runs the solve (lanes >= 2 NX on a copy of column 0, results to the sinks)
