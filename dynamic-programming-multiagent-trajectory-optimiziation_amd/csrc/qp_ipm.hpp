@@ -1214,8 +1214,8 @@ __global__ __launch_bounds__(64) void qp_ipm_kernel(QPArgs a) {
                     // C^-1 by Gauss-Jordan without pivoting (C is symmetric positive definite in exact arithmetic); a
                     // pivot that is not positive and finite, or a non-finite entry of C^-1, fails the factor, as the
                     // twin's Cholesky of C does (oracle/scvx_cpu.cpp riccati_factor).  Written with __builtin_isfinite:
-                    // the same tests written as x - x == 0 / x < inf reported finite entries as non-finite in this
-                    // kernel's code (round 6)
+                    // with x = a * b, floating-point contraction turns x - x into fma(a, b, -x), the product's rounding
+                    // error, so x - x == 0 flagged finite entries (round 6)
 #ifdef QP_STF_DEBUG
                     double Cm0[PMA * PMA];
 #pragma unroll
