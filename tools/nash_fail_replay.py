@@ -13,7 +13,7 @@ import scvx_hip  # noqa: E402
 from SCvx.config import default_game as G  # noqa: E402
 from SCvx.models.game_model import GameUnicycleModel  # noqa: E402
 
-d = np.load(os.path.join(REPO, "dbg", "nash_fail.npz"))
+d = np.load(os.environ.get("NASH_FAIL") or os.path.join(REPO, "dbg", "nash_fail.npz"))
 p = G.AGENT_PARAMS[2]
 m = GameUnicycleModel(**{k: p[k] for k in ("r_init", "r_final", "obstacles", "control_weight", "collision_weight",
                                            "collision_radius", "control_rate_weight", "curvature_weight")})
