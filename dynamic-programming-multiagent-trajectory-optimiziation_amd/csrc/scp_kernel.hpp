@@ -1730,6 +1730,46 @@ __global__ __launch_bounds__(64 * NW) void scp_ipm_kernel(SCPArgs a, double* __r
         }
         const double mu_a = blk_sum(mual) / deg;
         const double sg = (mu_a / mu) * (mu_a / mu) * (mu_a / mu);
+#ifdef SCP_DEGEN
+        {   // diagnostics: which rows carry the predicted complementarity (s + aa ds)(l + aa dl) of the affine step, by
+            // row type (x / u / nu trust-region facets, bounds + slabs + node-0 rows, soft rows); "deg" counts rows whose
+            // slack and dual both fall to at least a quarter of their value (products >= 0.05 s l)
+            double share[5] = {0, 0, 0, 0, 0}, cntd[5] = {0, 0, 0, 0, 0};
+            for (int t = tid; t < K; t += NT) {
+                double* B = nb(t);
+                const int nh = (int)B[Ly.o_nh];
+                for (int r = 0; r < RL; ++r) {
+                    if (r >= nh && r < RH) continue;
+                    int ty = 4;
+                    if (r < RH) {
+                        const int q = r - (1 << NX) - (1 << NU);
+                        ty = r < (1 << NX) ? 0 : (q < 0 ? 1 : ((t < K - 1 && q < (1 << NX)) ? 2 : 3));
+                    }
+                    const double sv = B[Ly.o_s + r], lv = B[Ly.o_lam + r], ds = B[Ly.o_dsa + r], dl = B[Ly.o_dla + r];
+                    const double c = (sv + aa * ds) * (lv + aa * dl);
+                    if (agent == 0 && it >= 16 && t == 50 && c >= 0.05 * sv * lv) {
+                        const double* ar = B + Ly.o_rows + r * (NZ + 1);
+                        int nzi[4] = {-1, -1, -1, -1}, k = 0;
+                        for (int i = 0; i < NZ && k < 4; ++i)
+                            if (ar[i] != 0.0) nzi[k++] = i;
+                        printf("SCP_DEGEN_ROW it %d t %d r %d ty %d s %.3e l %.3e ds %.3e dl %.3e | nz %d %d %d %d coef %.3e h %.3e\n",
+                               it, t, r, ty, sv, lv, ds, dl, nzi[0], nzi[1], nzi[2], nzi[3], nzi[0] >= 0 ? ar[nzi[0]] : 0.0,
+                               ar[NZ]);
+                    }
+                    for (int q = 0; q < 5; ++q) {
+                        share[q] += q == ty ? c : 0.0;
+                        cntd[q] += (q == ty && c >= 0.05 * sv * lv) ? 1.0 : 0.0;
+                    }
+                }
+            }
+            for (int q = 0; q < 5; ++q) { share[q] = blk_sum(share[q]); cntd[q] = blk_sum(cntd[q]); }
+            if (agent == 0 && tid == 0)
+                printf("SCP_DEGEN it %d mu %.3e mu_aff/mu %.3f aa %.4f | share x %.3f u %.3f nu %.3f bnd %.3f soft %.3f | "
+                       "deg rows x %d u %d nu %d bnd %d soft %d\n", it, mu, mu_a / mu, aa, share[0] / (mu_a * deg),
+                       share[1] / (mu_a * deg), share[2] / (mu_a * deg), share[3] / (mu_a * deg), share[4] / (mu_a * deg),
+                       (int)cntd[0], (int)cntd[1], (int)cntd[2], (int)cntd[3], (int)cntd[4]);
+        }
+#endif
         __syncthreads();
         // step fraction 0.99, or 1 - 1e-5 once the affine predictor takes a (nearly) full step: the end game,
         // where a fixed 0.99 caps the gap reduction at 100x per iteration (qp_ipm.hpp QP_TAU_END, the same rule)
